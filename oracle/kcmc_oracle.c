@@ -1,0 +1,316 @@
+/*
+ * kcmc CPU oracle -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of the third-party numerics that the reference's
+ * per-frame alignment hot path calls (reference: /root/reference/VideoAligner.py,
+ * cited below as VA:<line>).  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker /
+ * the timed CPU baseline -- never as the product path.  The product path is the
+ * HIP library under keypoint-consensus-motion-correction_amd/csrc.
+ *
+ * Parity pinning:
+ *   - kcmc_oracle_ransac_rigid: pinned against the reference's own
+ *     _compute_euclidean_affine (VA:288-323, scikit-image 0.18.3 ransac) run in
+ *     the authoring container -> tests/golden/ransac_golden.npz.
+ *   - kcmc_oracle_knn2_l2u8 and kcmc_oracle_warp_affine_u16: OpenCV is absent
+ *     everywhere in this image, so these restate OpenCV 4.x's classic algorithms
+ *     (core/src/batch_distance.cpp batchDistL2_8u32f + K-insertion;
+ *     imgproc/src/imgwarp.cpp warpAffine/WarpAffineInvoker/remapBilinear) and
+ *     are pinned by hand-computed known-answer tests (tests/test_oracle.py).
+ *     "Parity vs real OpenCV: unpinned" -- see DESIGN.md.
+ *
+ * Build: gcc -O3 -march=x86-64-v3 -ffp-contract=off -fPIC -shared (oracle/Makefile).
+ * -ffp-contract=off matters: every product/sum below is rounded separately unless
+ * fma() is written explicitly, mirroring the reference platform.
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------- */
+/* K1 oracle: cv2.BFMatcher(crossCheck=False).knnMatch(query, train, k=2)     */
+/* (VA:194-195).  OpenCV default normType = NORM_L2; for CV_8U descriptors     */
+/* batchDistance uses dtype CV_32F and dist = sqrtf((float)sum (a-b)^2).       */
+/* The K=2 insertion compares float bit patterns as ints (positive floats) and */
+/* inserts row j iff d < best[K-1], shifting while best[k] > d: ties keep the  */
+/* lower train index first.                                                    */
+/* ------------------------------------------------------------------------- */
+int kcmc_oracle_knn2_l2u8(const uint8_t* query, int n_query, const uint8_t* train,
+                          int n_train, int D, int32_t* out_idx, float* out_dist) {
+  if (n_query < 0 || n_train < 0 || D <= 0) return -1;
+  for (int i = 0; i < n_query; ++i) {
+    const uint8_t* a = query + (size_t)i * D;
+    float bd[2] = {FLT_MAX, FLT_MAX};
+    int32_t bi[2] = {-1, -1};
+    for (int j = 0; j < n_train; ++j) {
+      const uint8_t* b = train + (size_t)j * D;
+      int ssd = 0;
+      for (int k = 0; k < D; ++k) {
+        int t = (int)a[k] - (int)b[k];
+        ssd += t * t;
+      }
+      float d = sqrtf((float)ssd);
+      int32_t di, b1;
+      memcpy(&di, &d, 4);
+      memcpy(&b1, &bd[1], 4);
+      if (di < b1) {
+        int k = 0;
+        int32_t b0;
+        memcpy(&b0, &bd[0], 4);
+        if (b0 > di) {
+          bd[1] = bd[0];
+          bi[1] = bi[0];
+          k = 0;
+        } else {
+          k = 1;
+        }
+        bd[k] = d;
+        bi[k] = j;
+      }
+    }
+    out_idx[2 * i] = bi[0];
+    out_idx[2 * i + 1] = bi[1];
+    out_dist[2 * i] = bd[0];
+    out_dist[2 * i + 1] = bd[1];
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* K3 oracle: cv2.warpAffine(img, M, (W, H), flags=INTER_LINEAR) on uint16     */
+/* (VA:455-458), BORDER_CONSTANT with value 0, classic fixed-point path.       */
+/* ------------------------------------------------------------------------- */
+static int cv_round(double v) { return (int)lrint(v); }     /* round-half-even */
+static int cv_roundf(float v) { return (int)lrintf(v); }
+static int16_t sat_short(int v) {
+  return (int16_t)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
+}
+static uint16_t sat_ushort_f(float v) {
+  int iv = cv_roundf(v);
+  return (uint16_t)((unsigned)iv <= 65535u ? iv : (iv > 0 ? 65535 : 0));
+}
+
+/* OpenCV's in-place inversion of a forward 2x3 map (warpAffine without
+ * WARP_INVERSE_MAP). */
+void kcmc_oracle_invert_affine(const double* Min, double* M) {
+  memcpy(M, Min, 6 * sizeof(double));
+  double D = M[0] * M[4] - M[1] * M[3];
+  D = D != 0 ? 1. / D : 0;
+  double A11 = M[4] * D, A22 = M[0] * D;
+  M[0] = A11;
+  M[1] *= -D;
+  M[3] *= -D;
+  M[4] = A22;
+  double b1 = -M[0] * M[2] - M[1] * M[5];
+  double b2 = -M[3] * M[2] - M[4] * M[5];
+  M[2] = b1;
+  M[5] = b2;
+}
+
+/* src [H,W,C] u16, dst [dH,dW,C] u16, M6 = forward 2x3 map (row-major). */
+int kcmc_oracle_warp_affine_u16(const uint16_t* src, int H, int W, int C,
+                                const double* M6, int inverse_map, uint16_t* dst,
+                                int dH, int dW) {
+  if (H <= 0 || W <= 0 || C <= 0 || dH < 0 || dW < 0) return -1;
+  const int AB_BITS = 10, AB_SCALE = 1 << AB_BITS, INTER_BITS = 5;
+  const int INTER_TAB_SIZE = 1 << INTER_BITS;
+  const int round_delta = AB_SCALE / INTER_TAB_SIZE / 2;
+  double M[6];
+  if (inverse_map)
+    memcpy(M, M6, sizeof(M));
+  else
+    kcmc_oracle_invert_affine(M6, M);
+  int* adelta = (int*)malloc(sizeof(int) * (size_t)(dW > 0 ? dW : 1));
+  int* bdelta = (int*)malloc(sizeof(int) * (size_t)(dW > 0 ? dW : 1));
+  if (!adelta || !bdelta) {
+    free(adelta);
+    free(bdelta);
+    return -2;
+  }
+  for (int x = 0; x < dW; ++x) {
+    adelta[x] = cv_round(M[0] * x * AB_SCALE);
+    bdelta[x] = cv_round(M[3] * x * AB_SCALE);
+  }
+  /* float bilinear weights, exactly as initInterTab1D/initInterTab2D build them */
+  float tab1[2 * 32];
+  for (int i = 0; i < INTER_TAB_SIZE; ++i) {
+    float x = i * (1.f / INTER_TAB_SIZE);
+    tab1[2 * i] = 1.f - x;
+    tab1[2 * i + 1] = x;
+  }
+  const size_t sstep = (size_t)W * C;
+  for (int y = 0; y < dH; ++y) {
+    int X0 = cv_round((M[1] * y + M[2]) * AB_SCALE) + round_delta;
+    int Y0 = cv_round((M[4] * y + M[5]) * AB_SCALE) + round_delta;
+    for (int x = 0; x < dW; ++x) {
+      int X = (X0 + adelta[x]) >> (AB_BITS - INTER_BITS);
+      int Y = (Y0 + bdelta[x]) >> (AB_BITS - INTER_BITS);
+      int sx = sat_short(X >> INTER_BITS), sy = sat_short(Y >> INTER_BITS);
+      int fx = X & (INTER_TAB_SIZE - 1), fy = Y & (INTER_TAB_SIZE - 1);
+      float w[4];
+      w[0] = tab1[2 * fy] * tab1[2 * fx];
+      w[1] = tab1[2 * fy] * tab1[2 * fx + 1];
+      w[2] = tab1[2 * fy + 1] * tab1[2 * fx];
+      w[3] = tab1[2 * fy + 1] * tab1[2 * fx + 1];
+      uint16_t* D = dst + ((size_t)y * dW + x) * C;
+      int inl = (unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1);
+      if (inl) {
+        const uint16_t* S = src + (size_t)sy * sstep + (size_t)sx * C;
+        for (int k = 0; k < C; ++k) {
+          float v = (float)S[k] * w[0] + (float)S[k + C] * w[1] + (float)S[sstep + k] * w[2] +
+                    (float)S[sstep + k + C] * w[3];
+          D[k] = sat_ushort_f(v);
+        }
+      } else if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
+        for (int k = 0; k < C; ++k) D[k] = 0;
+      } else {
+        int sx0 = (sx >= 0 && sx < W) ? sx : -1, sx1 = (sx + 1 >= 0 && sx + 1 < W) ? sx + 1 : -1;
+        int sy0 = (sy >= 0 && sy < H) ? sy : -1, sy1 = (sy + 1 >= 0 && sy + 1 < H) ? sy + 1 : -1;
+        for (int k = 0; k < C; ++k) {
+          float v0 = (sx0 >= 0 && sy0 >= 0) ? src[(size_t)sy0 * sstep + (size_t)sx0 * C + k] : 0;
+          float v1 = (sx1 >= 0 && sy0 >= 0) ? src[(size_t)sy0 * sstep + (size_t)sx1 * C + k] : 0;
+          float v2 = (sx0 >= 0 && sy1 >= 0) ? src[(size_t)sy1 * sstep + (size_t)sx0 * C + k] : 0;
+          float v3 = (sx1 >= 0 && sy1 >= 0) ? src[(size_t)sy1 * sstep + (size_t)sx1 * C + k] : 0;
+          float v = v0 * w[0] + v1 * w[1] + v2 * w[2] + v3 * w[3];
+          D[k] = sat_ushort_f(v);
+        }
+      }
+    }
+  }
+  free(adelta);
+  free(bdelta);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* K2 oracle: skimage 0.18.3 ransac(EuclideanTransform, min_samples=2, ...)   */
+/* as called at VA:309-316, in closed form.                                    */
+/* ------------------------------------------------------------------------- */
+
+/* numpy's pairwise summation of a contiguous float64 vector (np.sum, used for
+ * sum(r**2) at skimage fit.py:847): n<8 sequential, n<=128 eight strided
+ * accumulators, else split at n/2 rounded down to a multiple of 8. */
+double kcmc_oracle_pairwise_sum(const double* a, int n) {
+  if (n < 8) {
+    double res = 0.;
+    for (int i = 0; i < n; ++i) res += a[i];
+    return res;
+  } else if (n <= 128) {
+    double r[8];
+    int i;
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    for (i = 8; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  } else {
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return kcmc_oracle_pairwise_sum(a, n2) + kcmc_oracle_pairwise_sum(a + n2, n - n2);
+  }
+}
+
+/* Rigid least-squares fit (skimage _umeyama without scaling, _geometric.py:72-144)
+ * in closed form: R = rotation maximising tr(R^T A), A = sum dst_d src_d^T.
+ * Means are sequential axis-0 sums divided by n (numpy mean).  Returns 0 and the
+ * 2x3 [R|t] when A != 0, else 1 (skimage: rank(A) == 0 -> NaN model). */
+static int rigid_fit(const double* src, const double* dst, const int* sel, int n, double* P) {
+  double ms0 = 0, ms1 = 0, md0 = 0, md1 = 0;
+  for (int k = 0; k < n; ++k) {
+    int q = sel ? sel[k] : k;
+    ms0 += src[2 * q];
+    ms1 += src[2 * q + 1];
+    md0 += dst[2 * q];
+    md1 += dst[2 * q + 1];
+  }
+  ms0 /= n;
+  ms1 /= n;
+  md0 /= n;
+  md1 /= n;
+  double a00 = 0, a01 = 0, a10 = 0, a11 = 0;
+  for (int k = 0; k < n; ++k) {
+    int q = sel ? sel[k] : k;
+    double s0 = src[2 * q] - ms0, s1 = src[2 * q + 1] - ms1;
+    double d0 = dst[2 * q] - md0, d1 = dst[2 * q + 1] - md1;
+    a00 += d0 * s0;
+    a01 += d0 * s1;
+    a10 += d1 * s0;
+    a11 += d1 * s1;
+  }
+  double a = a00 + a11, b = a10 - a01;
+  if (a == 0 && b == 0) return 1;
+  double h = sqrt(a * a + b * b);
+  double c = a / h, s = b / h;
+  P[0] = c;
+  P[1] = -s;
+  P[3] = s;
+  P[4] = c;
+  P[2] = md0 - (c * ms0 - s * ms1);
+  P[5] = md1 - (s * ms0 + c * ms1);
+  return 0;
+}
+
+/* src = frame keypoints, dst = template keypoints (VA:310).  hyp = [T,2] sample
+ * indices (trial t uses hyp[t]; numpy RandomState(seed).choice(N, 2, False)).
+ * out_params [2,3] (NaN when no model), out_inliers [N] (0/1).
+ * Returns 0 when a model was fitted, 1 when skimage would return None. */
+int kcmc_oracle_ransac_rigid(const double* src, const double* dst, int N, const int32_t* hyp,
+                             int T, double thresh, double* out_params, uint8_t* out_inliers,
+                             int32_t* out_best_trial, int32_t* out_n_inliers) {
+  double* r2 = (double*)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1));
+  uint8_t* cur = (uint8_t*)malloc((size_t)(N > 0 ? N : 1));
+  int* sel = (int*)malloc(sizeof(int) * (size_t)(N > 0 ? N : 1));
+  if (!r2 || !cur || !sel) {
+    free(r2);
+    free(cur);
+    free(sel);
+    return -2;
+  }
+  int best_n = 0, best_t = -1;
+  double best_S = INFINITY;
+  memset(out_inliers, 0, (size_t)N);
+  for (int t = 0; t < T; ++t) {
+    int pair[2] = {hyp[2 * t], hyp[2 * t + 1]};
+    double P[6];
+    if (rigid_fit(src, dst, pair, 2, P)) continue; /* NaN model: count 0, S NaN */
+    int cnt = 0;
+    for (int k = 0; k < N; ++k) {
+      double x = src[2 * k], y = src[2 * k + 1];
+      double xp = fma(y, P[1], x * P[0]) + P[2];
+      double yp = fma(y, P[4], x * P[3]) + P[5];
+      double dx = xp - dst[2 * k], dy = yp - dst[2 * k + 1];
+      double r = sqrt(dx * dx + dy * dy);
+      cur[k] = r < thresh;
+      cnt += cur[k];
+      r2[k] = r * r;
+    }
+    double S = kcmc_oracle_pairwise_sum(r2, N);
+    if (cnt > best_n || (cnt == best_n && S < best_S)) {
+      best_n = cnt;
+      best_S = S;
+      best_t = t;
+      memcpy(out_inliers, cur, (size_t)N);
+      if (best_S <= 0) break; /* stop_residuals_sum = 0 (fit.py:862-869) */
+    }
+  }
+  int rc = 1;
+  if (best_n > 0) {
+    int m = 0;
+    for (int k = 0; k < N; ++k)
+      if (out_inliers[k]) sel[m++] = k;
+    rc = rigid_fit(src, dst, sel, m, out_params);
+  }
+  if (rc) {
+    for (int k = 0; k < 6; ++k) out_params[k] = NAN;
+    if (best_n == 0) memset(out_inliers, 0, (size_t)N);
+  }
+  *out_best_trial = best_t;
+  *out_n_inliers = best_n;
+  free(r2);
+  free(cur);
+  free(sel);
+  return rc;
+}
