@@ -1,0 +1,161 @@
+/*
+ * kcmc.h -- C ABI of the MI355X (gfx950) alignment hot path.
+ *
+ * Drop-in boundary for the per-frame hot path of VideoAligner
+ * (reference: /root/reference/VideoAligner.py, cited as VA:<line>).  The reference
+ * farms three per-frame functions out to a joblib process pool through
+ * VideoAligner._parallelize (VA:460-471).  Each entry point below replaces one of
+ * those per-frame calls with ONE batched call over all frames of a slab:
+ *
+ *   kcmc_match_frames      <- _get_frame_keypoints matching part (VA:194-214):
+ *                             cv2.BFMatcher(crossCheck=False).knnMatch(des_t, des_q, k=2),
+ *                             best-match reorder, ratio filter, median filter.
+ *   kcmc_knn2_l2u8         <- cv2.BFMatcher().knnMatch(..., k=2) alone (VA:194-195).
+ *   kcmc_consensus         <- _get_consensus_kps + _lookup_consensus_kps (VA:224-286),
+ *                             host-only, reproducing CPython set/Counter ordering.
+ *   kcmc_ransac_rigid      <- _compute_euclidean_affine (VA:288-323), i.e. skimage 0.18.3
+ *                             ransac(EuclideanTransform, 2, 2, max_trials, random_state).
+ *   kcmc_warp_affine_u16   <- _apply_affine (VA:455-458): cv2.warpAffine(img, M, (W,H),
+ *                             INTER_LINEAR), BORDER_CONSTANT 0, classic fixed-point path.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Pointers named *_dev are device (HBM) pointers
+ *     owned by the caller (e.g. torch ROCm tensors' data_ptr()); *_host are host
+ *     pointers.  The library never frees caller memory.
+ *   - Launch entry points are asynchronous on `stream` (a hipStream_t; NULL = the
+ *     null stream), perform no allocation and no synchronisation, and are therefore
+ *     capturable into a hipGraph.  kcmc_ransac_prepare allocates and synchronises.
+ *   - Return value: KCMC_OK (0) or an error code; kcmc_last_error() returns the
+ *     calling thread's last message.  Per-frame model failure is NOT an error: it is
+ *     NaN in the output parameters, as in the reference (VA:321-322).
+ *   - One kcmc_ctx per device; contexts are independent (no global mutable state
+ *     except the thread-local error string).
+ */
+#ifndef KCMC_H_
+#define KCMC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KCMC_ABI_VERSION 1
+
+enum {
+  KCMC_OK = 0,
+  KCMC_EINVAL = 1,       /* bad argument (maps to ValueError on the Python side) */
+  KCMC_EHIP = 2,         /* HIP runtime / launch failure */
+  KCMC_ENOMEM = 3,       /* allocation failure */
+  KCMC_EUNSUPPORTED = 4, /* shape outside what the kernels implement */
+  KCMC_EALIGN = 5        /* too few consensus keypoints (VideoAligner.AlignmentError, VA:241-244) */
+};
+
+typedef struct kcmc_ctx kcmc_ctx;
+typedef void* kcmc_stream_t; /* hipStream_t */
+
+int kcmc_abi_version(void);
+const char* kcmc_last_error(void);
+
+/* Create / destroy the per-device context (holds the uploaded RANSAC hypothesis
+ * tables).  `device` is a HIP device ordinal. */
+int kcmc_create(int device, kcmc_ctx** out);
+int kcmc_destroy(kcmc_ctx* ctx);
+
+/* ---------------------------------------------------------------- K1: matching
+ * Brute-force k=2 nearest neighbours under OpenCV NORM_L2 on uint8 descriptors
+ * (cv2.BFMatcher default normType, VA:194), batched over frames.
+ *   des_tpl_dev [n_tpl, D] u8      template ("query" in OpenCV terms), shared
+ *   des_q_dev   [P, D] u8          all frames' descriptors, frame f = rows
+ *                                  q_off[f] .. q_off[f+1]-1 ("train" in OpenCV terms)
+ *   q_off_dev   [n_frames+1] i32   CSR offsets (device)
+ *   max_nq                          max_f (q_off[f+1]-q_off[f]) (host-known bound)
+ *   out_idx_dev [n_frames, n_tpl, 2] i32   train index of best / second best (-1: none)
+ *   out_dist_dev[n_frames, n_tpl, 2] f32   sqrtf of the exact integer SSD (FLT_MAX: none)
+ * Ties go to the lower frame-keypoint index, as OpenCV's K-insertion does.
+ * 1 <= D <= 64. */
+int kcmc_knn2_l2u8(kcmc_ctx* ctx, const uint8_t* des_tpl_dev, int n_tpl, int D,
+                   const uint8_t* des_q_dev, const int32_t* q_off_dev, int n_frames, int max_nq,
+                   int32_t* out_idx_dev, float* out_dist_dev, kcmc_stream_t stream);
+
+/* kcmc_knn2_l2u8 + VA:196-214 per frame:
+ *   out_kp_ordered_dev [n_frames, n_tpl, 2] f64 = kp_q[best match] for every template row
+ *   out_keep_bits_dev  [n_frames, ceil(n_tpl/32)] u32  bit i = template row i survived the
+ *                      ratio filter (d0 < ratio*d1, in double) and the displacement filter
+ *                      (d_lo*median <= |kp_t - kp_q| <= d_hi*median over ratio survivors)
+ *   out_counts_dev     [n_frames, 4] i32 = the four numbers of the reference's per-frame
+ *                      debug log (VA:215-221): len(kp_query) (== n_tpl after the reorder),
+ *                      len(matches), #ratio survivors, #distance survivors.
+ * kp_tpl_dev [n_tpl, 2] f64, kp_q_dev [P, 2] f64 (cv2 KeyPoint.pt promoted to f64).
+ * Every frame must have >= 2 keypoints (the reference raises otherwise, VA:203). */
+int kcmc_match_frames(kcmc_ctx* ctx, const uint8_t* des_tpl_dev, const double* kp_tpl_dev, int n_tpl,
+                      int D, const uint8_t* des_q_dev, const double* kp_q_dev,
+                      const int32_t* q_off_dev, int n_frames, int max_nq, double ratio, double d_lo,
+                      double d_hi, int32_t* out_idx_dev, float* out_dist_dev,
+                      double* out_kp_ordered_dev, uint32_t* out_keep_bits_dev,
+                      int32_t* out_counts_dev, kcmc_stream_t stream);
+
+/* ------------------------------------------------------- host: keypoint consensus
+ * VA:224-286 on the host, reproducing CPython 3 set/Counter iteration order exactly:
+ *   keep_bits_host [n_frames, ceil(n_tpl/32)] u32 (output of kcmc_match_frames)
+ *   out_consensus_host [n_kp_global] i32  template indices in Counter.most_common order
+ *   out_votes_host     [n_kp_global] i32  their vote counts
+ *   *out_n_consensus   number of entries written (<= n_kp_global)
+ *   out_pt_off_host [n_frames+1] i32, out_pt_idx_host [n_frames * n_kp_global] i32:
+ *       per-frame template indices of list(consensus_set.intersection(frame_set)),
+ *       i.e. the RANSAC point order of VA:274.
+ * Returns KCMC_EALIGN if fewer than n_min keypoints received any vote (VA:241-244). */
+int kcmc_consensus(const uint32_t* keep_bits_host, int n_frames, int n_tpl, int n_kp_global,
+                   int n_min, int32_t* out_consensus_host, int32_t* out_votes_host,
+                   int* out_n_consensus, int32_t* out_pt_off_host, int32_t* out_pt_idx_host);
+
+/* --------------------------------------------------------------- K2: RANSAC
+ * The seeded sample stream skimage 0.18.3 consumes: trial t of a frame with n points
+ * uses np.random.RandomState(seed).choice(n, min_samples, replace=False) drawn t+1-th
+ * (fit.py:791, 819-826), i.e. the first min_samples entries of the t-th legacy
+ * MT19937 permutation.  out_host [trials, min_samples] i32.  Host only. */
+int kcmc_hypothesis_table(int n, int trials, uint32_t seed, int min_samples, int32_t* out_host);
+
+/* Build (host, cached per context) and upload the rigid (min_samples = 2) tables for
+ * the point counts n_values_host[0..count) (each in [3, 65535]).  Allocates and
+ * synchronises when a new count appears; call before kcmc_ransac_rigid with every
+ * point count that frame batch will run RANSAC on. */
+int kcmc_ransac_prepare(kcmc_ctx* ctx, const int32_t* n_values_host, int count, int trials, uint32_t seed);
+
+/* Batched rigid RANSAC, one frame per workgroup.
+ * Point k of frame f (k < N_f = pt_off[f+1]-pt_off[f]):
+ *   pt_idx_dev == NULL: src = src_dev[pt_off[f]+k], dst = dst_dev[pt_off[f]+k]
+ *   pt_idx_dev != NULL: q = pt_idx[pt_off[f]+k]; src = src_dev[f*src_frame_stride + q],
+ *                       dst = dst_dev[q]        (src = kcmc_match_frames' kp_ordered,
+ *                                                dst = template keypoints: VA:275-276)
+ * src = frame keypoints, dst = template keypoints (VA:310).  Frames with
+ * N_f < n_skip (VideoAligner.N_KP_FRAME_SKIP) or with no inlier get NaN params.
+ *   out_params_dev   [n_frames, 2, 3] f64  model.params[:2], translation * spatial_rate
+ *   out_inliers_dev  [P] u8                best hypothesis' inlier mask (skimage ransac's
+ *                                          second return value), CSR like the points
+ *   out_n_inliers_dev[n_frames] i32, out_best_trial_dev[n_frames] i32 (-1: none)
+ * max_n >= every N_f; every N_f >= max(n_skip, 3) must have been prepared with the same
+ * `trials` (kcmc_ransac_prepare); a missing table yields NaN for that frame and
+ * n_inliers = -1. */
+int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src_dev, const double* dst_dev,
+                      const int32_t* pt_idx_dev, const int32_t* pt_off_dev, int src_frame_stride,
+                      int n_frames, int max_n, int trials, double residual_threshold,
+                      double spatial_rate, int n_skip, double* out_params_dev,
+                      uint8_t* out_inliers_dev, int32_t* out_n_inliers_dev,
+                      int32_t* out_best_trial_dev, kcmc_stream_t stream);
+
+/* ------------------------------------------------------------------ K3: warp
+ * cv2.warpAffine(frame, M_f, (W, H), flags=INTER_LINEAR [| WARP_INVERSE_MAP]) for
+ * every frame: src_dev/dst_dev [n_frames, H, W, C] u16 (C interleaved, C=1 for the
+ * reference's grayscale stacks), M_dev [n_frames, 2, 3] f64 forward maps (inverted
+ * in double exactly as OpenCV does unless inverse_map != 0).  Out-of-image taps
+ * read 0.  Bit-exact to the classic OpenCV fixed-point algorithm on platforms
+ * without FMA contraction. */
+int kcmc_warp_affine_u16(kcmc_ctx* ctx, const uint16_t* src_dev, uint16_t* dst_dev,
+                         const double* M_dev, int n_frames, int H, int W, int C, int inverse_map,
+                         kcmc_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KCMC_H_ */

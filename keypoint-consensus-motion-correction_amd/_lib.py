@@ -1,0 +1,156 @@
+"""ctypes binding of libkcmc.so (the C ABI declared in include/kcmc.h).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot be
+loaded, every entry point raises ``KcmcLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+from . import build as _build
+
+KCMC_OK = 0
+KCMC_EINVAL = 1
+KCMC_EHIP = 2
+KCMC_ENOMEM = 3
+KCMC_EUNSUPPORTED = 4
+KCMC_EALIGN = 5
+ABI_VERSION = 1
+
+# Every symbol include/kcmc.h declares (checked by tests/test_capi.py).
+EXPORTED_SYMBOLS = (
+    "kcmc_abi_version",
+    "kcmc_last_error",
+    "kcmc_create",
+    "kcmc_destroy",
+    "kcmc_knn2_l2u8",
+    "kcmc_match_frames",
+    "kcmc_consensus",
+    "kcmc_hypothesis_table",
+    "kcmc_ransac_prepare",
+    "kcmc_ransac_rigid",
+    "kcmc_warp_affine_u16",
+)
+
+
+class KcmcLibraryError(RuntimeError):
+    """libkcmc.so is missing or failed to load (no CPU fallback exists)."""
+
+
+class KcmcError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"kcmc error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+_lock = threading.Lock()
+_lib: Optional[ctypes.CDLL] = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+D = ctypes.c_double
+U32 = ctypes.c_uint32
+
+_SIGNATURES = {
+    "kcmc_abi_version": ([], I),
+    "kcmc_last_error": ([], ctypes.c_char_p),
+    "kcmc_create": ([I, ctypes.POINTER(P)], I),
+    "kcmc_destroy": ([P], I),
+    "kcmc_knn2_l2u8": ([P, P, I, I, P, P, I, I, P, P, P], I),
+    "kcmc_match_frames": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
+    "kcmc_consensus": ([P, I, I, I, I, P, P, P, P, P], I),
+    "kcmc_hypothesis_table": ([I, I, U32, I, P], I),
+    "kcmc_ransac_prepare": ([P, P, I, I, U32], I),
+    "kcmc_ransac_rigid": ([P, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, P], I),
+    "kcmc_warp_affine_u16": ([P, P, P, P, I, I, I, I, I, P], I),
+}
+
+
+def lib_path() -> str:
+    return _build.LIB_PATH
+
+
+def load(auto_build: bool = True) -> ctypes.CDLL:
+    """Load libkcmc.so (building it with hipcc first when allowed and stale)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = lib_path()
+        if auto_build and os.environ.get("KCMC_NO_BUILD", "0") != "1":
+            try:
+                if not _build.up_to_date():
+                    _build.build()
+            except Exception as e:  # pragma: no cover - only when hipcc is broken
+                if not os.path.exists(path):
+                    raise KcmcLibraryError(f"cannot build {path}: {e}") from e
+        if not os.path.exists(path):
+            raise KcmcLibraryError(
+                f"{path} not found: build it with `python -m kcmc_amd.build` (hipcc, gfx950). "
+                "There is no CPU fallback for the alignment hot path."
+            )
+        try:
+            L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            raise KcmcLibraryError(f"failed to load {path}: {e}") from e
+        for name, (args, res) in _SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        if L.kcmc_abi_version() != ABI_VERSION:
+            raise KcmcLibraryError(f"{path}: ABI version {L.kcmc_abi_version()} != {ABI_VERSION}")
+        _lib = L
+        return L
+
+
+def check(rc: int) -> None:
+    if rc != KCMC_OK:
+        msg = load().kcmc_last_error().decode(errors="replace")
+        if rc == KCMC_EINVAL:
+            raise ValueError(msg)
+        if rc == KCMC_EALIGN:
+            from .video_aligner import AlignmentError
+
+            raise AlignmentError(msg)
+        raise KcmcError(rc, msg)
+
+
+class Context:
+    """A per-device kcmc_ctx (owns the uploaded RANSAC hypothesis tables)."""
+
+    def __init__(self, device: int):
+        self.device = device
+        self._h = P()
+        check(load().kcmc_create(device, ctypes.byref(self._h)))
+
+    @property
+    def handle(self) -> P:
+        return self._h
+
+    def close(self) -> None:
+        if self._h:
+            load().kcmc_destroy(self._h)
+            self._h = P()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_contexts = {}
+
+
+def context(device: int) -> Context:
+    with _lock:
+        ctx = _contexts.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        with _lock:
+            _contexts[device] = ctx
+    return ctx

@@ -1,0 +1,89 @@
+"""Host-side affine post-processing between RANSAC and the warp (VA:325-453).
+
+O(F) scalar work on a few KB; it stays on the host, as in the reference, but is
+written with array operations and only loops over NaN gaps.  Results are
+identical to the reference's (pinned by tests/golden/affines_golden.npz), including
+its quirks: trailing extrapolated frames are not reported as interpolated
+(VA:400), rotation is recovered as arccos(a00) (sign lost, VA:452), and gap
+interpolation lerps arccos/arcsin of the four rotation entries independently
+(VA:423-436).
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+
+class AlignmentError(BaseException):
+    """Raised when alignment cannot proceed (VA:16-17); same base class as the reference."""
+
+
+def process_affines(affines_sample: Sequence[np.ndarray], frame_downsample_rate: int) -> Tuple[np.ndarray, List[int]]:
+    """VA:326-345: stack, record NaN sample frames, NaN-pad the temporally skipped frames."""
+    a = np.stack(affines_sample)
+    rate = int(frame_downsample_rate)
+    skipped = [int(i) * rate for i in np.flatnonzero(np.isnan(a).reshape(len(a), -1).any(axis=1))]
+    out = np.full((len(a) * rate,) + a.shape[1:], np.nan, dtype=np.result_type(a.dtype, np.float64))
+    out[::rate] = a
+    return out, skipped
+
+
+def _lerp_gap(a_prev: np.ndarray, a_next: np.ndarray, x_lo: int, x_hi: int, xs: np.ndarray) -> np.ndarray:
+    """VA:410-437 for one gap: scipy interp1d(kind='linear') evaluated the way scipy does,
+    y = slope * (x - x_lo) + y_lo with slope = (y_hi - y_lo) / (x_hi - x_lo)."""
+    base = np.array((a_prev, a_next), dtype=np.float64)
+    base[:, 0, 0] = np.arccos(base[:, 0, 0])
+    base[:, 0, 1] = np.arcsin(base[:, 0, 1])
+    base[:, 1, 0] = np.arcsin(base[:, 1, 0])
+    base[:, 1, 1] = np.arccos(base[:, 1, 1])
+    y_lo, y_hi = base[0], base[1]
+    slope = (y_hi - y_lo) / (float(x_hi) - float(x_lo))
+    out = slope[None] * (xs.astype(np.float64) - float(x_lo))[:, None, None] + y_lo[None]
+    out[:, 0, 0] = np.cos(out[:, 0, 0])
+    out[:, 0, 1] = np.sin(out[:, 0, 1])
+    out[:, 1, 0] = np.sin(out[:, 1, 0])
+    out[:, 1, 1] = np.cos(out[:, 1, 1])
+    return out
+
+
+def interpolate_affines(affines: np.ndarray) -> Tuple[np.ndarray, List[int]]:
+    """VA:347-407: fill NaN frames (edge-fill at the ends, per-gap lerp inside)."""
+    aff = np.array(affines, dtype=np.float64, copy=True)
+    n = len(aff)
+    missing = np.isnan(aff.reshape(n, -1)).any(axis=1)
+    if not missing.any():
+        return aff, []
+    if missing.all():
+        raise AlignmentError(
+            "No transformations were calculated because too few keypoints were identified "
+            "(probably because too few keypoints were identified)"
+        )
+    present = np.flatnonzero(~missing)
+    interpolated: List[int] = []
+    first = int(present[0])
+    if first > 0:  # extrapolate leading frames (VA:383-387)
+        aff[:first] = aff[first]
+        interpolated += list(range(first))
+    for lo, hi in zip(present[:-1], present[1:]):  # interior gaps (VA:389-395)
+        lo, hi = int(lo), int(hi)
+        if hi - lo > 1:
+            xs = np.arange(lo + 1, hi)
+            aff[lo + 1 : hi] = _lerp_gap(aff[lo], aff[hi], lo, hi, xs)
+            interpolated += list(range(lo + 1, hi))
+    last = int(present[-1])
+    if last < n - 1:  # extrapolate trailing frames (VA:397-400: reported range is empty)
+        aff[last + 1 :] = aff[last]
+    if aff.shape[1:] != (2, 3):
+        raise AlignmentError(
+            "An error occurred interpolating affine transforms for frames which had no affine transform estimate"
+        )
+    return aff, interpolated
+
+
+def euclidean_transforms(affines: np.ndarray) -> np.ndarray:
+    """VA:440-453: [x_translation, y_translation, arccos(a00)] per frame."""
+    t = np.zeros((affines.shape[0], 3))
+    t[:, :2] = affines[:, :, 2]
+    t[:, 2] = np.arccos(affines[:, 0, 0])
+    return t

@@ -1,0 +1,127 @@
+// Context lifetime, error reporting and the RANSAC table upload of the kcmc C ABI.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kcmc_internal.h"
+
+namespace kcmc {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(int code, const std::string& msg) {
+  set_error(msg);
+  return code;
+}
+
+int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return KCMC_OK;
+  return fail(KCMC_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int launch_check(const char* what) { return hip_check(hipGetLastError(), what); }
+
+// Defined in hostalg.cpp.
+int hypothesis_table_impl(int n, int trials, uint32_t seed, int min_samples, int32_t* out);
+
+}  // namespace kcmc
+
+using namespace kcmc;
+
+static void free_tables(kcmc_ctx* ctx);
+
+extern "C" int kcmc_abi_version(void) { return KCMC_ABI_VERSION; }
+
+extern "C" const char* kcmc_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int kcmc_create(int device, kcmc_ctx** out) {
+  if (!out) return fail(KCMC_EINVAL, "kcmc_create: out is NULL");
+  int n = 0;
+  KCMC_TRY(hip_check(hipGetDeviceCount(&n), "hipGetDeviceCount"));
+  if (device < 0 || device >= n)
+    return fail(KCMC_EINVAL, "kcmc_create: device " + std::to_string(device) + " out of range");
+  auto* c = new (std::nothrow) kcmc_ctx();
+  if (!c) return fail(KCMC_ENOMEM, "kcmc_create: out of host memory");
+  c->device = device;
+  *out = c;
+  return KCMC_OK;
+}
+
+extern "C" int kcmc_destroy(kcmc_ctx* ctx) {
+  if (!ctx) return KCMC_OK;
+  if (ctx->hyp || ctx->hyp_off) {
+    int prev = 0;
+    hipGetDevice(&prev);
+    hipSetDevice(ctx->device);
+    free_tables(ctx);
+    hipSetDevice(prev);
+  }
+  delete ctx;
+  return KCMC_OK;
+}
+
+static void free_tables(kcmc_ctx* ctx) {
+  if (ctx->hyp) hipFree(ctx->hyp);
+  if (ctx->hyp_off) hipFree(ctx->hyp_off);
+  ctx->hyp = nullptr;
+  ctx->hyp_off = nullptr;
+  ctx->hyp_off_len = 0;
+}
+
+extern "C" int kcmc_ransac_prepare(kcmc_ctx* ctx, const int32_t* n_values, int count, int trials, uint32_t seed) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_ransac_prepare: ctx is NULL");
+  if (count < 0 || (count > 0 && !n_values) || trials < 1)
+    return fail(KCMC_EINVAL, "kcmc_ransac_prepare: bad arguments");
+  if (ctx->hyp_trials != trials || ctx->hyp_seed != seed) {
+    ctx->hyp_host.clear();
+    ctx->hyp_trials = trials;
+    ctx->hyp_seed = seed;
+  }
+  bool changed = ctx->hyp == nullptr;
+  std::vector<int32_t> tab((size_t)trials * 2);
+  for (int k = 0; k < count; ++k) {
+    const int n = n_values[k];
+    if (n < 3 || n > 65535) return fail(KCMC_EINVAL, "kcmc_ransac_prepare: point counts must be in [3, 65535]");
+    if (ctx->hyp_host.count(n)) continue;
+    KCMC_TRY(hypothesis_table_impl(n, trials, seed, 2, tab.data()));
+    std::vector<uint32_t> packed((size_t)trials);
+    for (int t = 0; t < trials; ++t) packed[(size_t)t] = (uint32_t)tab[2 * t] | ((uint32_t)tab[2 * t + 1] << 16);
+    ctx->hyp_host.emplace(n, std::move(packed));
+    changed = true;
+  }
+  if (!changed) return KCMC_OK;
+  // (re)upload every cached table
+  const int off_len = ctx->hyp_host.empty() ? 1 : ctx->hyp_host.rbegin()->first + 1;
+  std::vector<int32_t> off((size_t)off_len, -1);
+  std::vector<uint32_t> all;
+  all.reserve(ctx->hyp_host.size() * (size_t)trials);
+  for (const auto& kv : ctx->hyp_host) {
+    off[(size_t)kv.first] = (int32_t)all.size();
+    all.insert(all.end(), kv.second.begin(), kv.second.end());
+  }
+  if (all.size() > (size_t)INT32_MAX) return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_prepare: tables too large");
+  if (all.empty()) all.push_back(0);
+  int prev = 0;
+  hipGetDevice(&prev);
+  KCMC_TRY(hip_check(hipSetDevice(ctx->device), "hipSetDevice"));
+  free_tables(ctx);
+  int rc = hip_check(hipMalloc(&ctx->hyp, all.size() * sizeof(uint32_t)), "hipMalloc(hyp)");
+  if (rc == KCMC_OK) rc = hip_check(hipMalloc(&ctx->hyp_off, off.size() * sizeof(int32_t)), "hipMalloc(hyp_off)");
+  if (rc == KCMC_OK)
+    rc = hip_check(hipMemcpy(ctx->hyp, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice),
+                   "hipMemcpy(hyp)");
+  if (rc == KCMC_OK)
+    rc = hip_check(hipMemcpy(ctx->hyp_off, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice),
+                   "hipMemcpy(hyp_off)");
+  hipSetDevice(prev);
+  if (rc != KCMC_OK) {
+    free_tables(ctx);
+    ctx->hyp_host.clear();
+    return rc;
+  }
+  ctx->hyp_off_len = off_len;
+  return KCMC_OK;
+}

@@ -1,0 +1,42 @@
+// Internal helpers shared by the kcmc translation units (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/kcmc.h"
+
+struct kcmc_ctx {
+  int device = 0;
+  // RANSAC hypothesis tables, built on demand per point count n: `hyp_trials` packed
+  // (i | j << 16) u32 samples per n.  Device: hyp (all tables back to back) and
+  // hyp_off[n] = start of n's table in hyp, or -1 (n in [0, hyp_off_len)).
+  std::map<int, std::vector<uint32_t>> hyp_host;
+  uint32_t* hyp = nullptr;
+  int32_t* hyp_off = nullptr;
+  int hyp_off_len = 0;
+  int hyp_trials = 0;
+  uint32_t hyp_seed = 0;
+};
+
+namespace kcmc {
+
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+// Check a HIP call / the last launch; on failure record the message and return KCMC_EHIP.
+int hip_check(hipError_t e, const char* what);
+int launch_check(const char* what);
+
+inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace kcmc
+
+#define KCMC_TRY(expr)            \
+  do {                            \
+    int _rc = (expr);             \
+    if (_rc != KCMC_OK) return _rc; \
+  } while (0)

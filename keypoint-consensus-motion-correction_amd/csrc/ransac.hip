@@ -1,0 +1,415 @@
+// K2: batched rigid RANSAC with scikit-image 0.18.3 semantics.
+//
+// Reference: VA:288-323 (_compute_euclidean_affine) ->
+//   skimage.measure.ransac((kp_query, kp_template), EuclideanTransform, min_samples=2,
+//   residual_threshold=2, max_trials=1000, random_state=42)   (fit.py:621-881)
+//
+// One workgroup (4 waves) per frame.  The frame's N point pairs are staged in LDS
+// (structure of arrays, read as broadcasts); each thread scores whole hypotheses:
+//   model      closed-form 2-point rigid Umeyama (the rotation maximising tr(R^T A),
+//              A = sum dst_d src_d^T; identical to skimage's SVD branch up to
+//              rounding; A == 0 -> NaN model, never selected)
+//   residual   r_k = sqrt(dx^2 + dy^2), x' = fma(y, -s, x*c) + tx (the order OpenBLAS
+//              dgemm uses for skimage's [x y 1] @ M^T), inlier iff r_k < threshold
+//   score      S = sum r_k^2 in numpy's pairwise-summation order (8 accumulators,
+//              blocks of 128), so that hypotheses tie-break exactly like np.sum
+// Selection: max inliers, then min S, then earliest trial (skimage's strict
+// comparisons); skimage's early exit (best S <= 0) is emulated sequentially in the
+// rare frames where some S == 0.  The hypothesis (sample pair) of trial t is the
+// t-th RandomState(seed).choice(N, 2, replace=False), precomputed on the host per N
+// (kcmc_ransac_prepare) -- it depends on N only because every frame reseeds.
+// Refit: rigid Umeyama over the best inlier set with workgroup reductions.
+#include <cfloat>
+#include <cmath>
+
+#include "kcmc_internal.h"
+
+namespace kcmc {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxN = 4096;  // numpy's pairwise split tree has depth <= 6 for n <= 4096
+constexpr int kPwDepth = 6;
+
+struct Model {
+  double c, s, tx, ty;
+  bool ok;
+};
+
+// Closed-form rigid fit of two correspondences (skimage _umeyama, estimate_scale=False).
+__device__ __forceinline__ Model fit2(double sx0, double sy0, double sx1, double sy1, double dx0, double dy0,
+                                      double dx1, double dy1) {
+  Model m;
+  const double ms0 = (sx0 + sx1) / 2.0, ms1 = (sy0 + sy1) / 2.0;
+  const double md0 = (dx0 + dx1) / 2.0, md1 = (dy0 + dy1) / 2.0;
+  const double a0 = sx0 - ms0, a1 = sy0 - ms1, b0 = sx1 - ms0, b1 = sy1 - ms1;
+  const double p0 = dx0 - md0, p1 = dy0 - md1, q0 = dx1 - md0, q1 = dy1 - md1;
+  const double a00 = p0 * a0 + q0 * b0;
+  const double a01 = p0 * a1 + q0 * b1;
+  const double a10 = p1 * a0 + q1 * b0;
+  const double a11 = p1 * a1 + q1 * b1;
+  const double a = a00 + a11, b = a10 - a01;
+  m.ok = !(a == 0.0 && b == 0.0);
+  const double hn = sqrt(a * a + b * b);
+  m.c = a / hn;
+  m.s = b / hn;
+  m.tx = md0 - (m.c * ms0 - m.s * ms1);
+  m.ty = md1 - (m.s * ms0 + m.c * ms1);
+  return m;
+}
+
+struct Pts {
+  const double* sx;
+  const double* sy;
+  const double* dx;
+  const double* dy;
+};
+
+__device__ __forceinline__ double resid2(const Model& m, const Pts& P, int k, double thresh, int& cnt) {
+  const double x = P.sx[k], y = P.sy[k];
+  const double xp = fma(y, -m.s, x * m.c) + m.tx;
+  const double yp = fma(y, m.c, x * m.s) + m.ty;
+  const double ex = xp - P.dx[k], ey = yp - P.dy[k];
+  const double r = sqrt(ex * ex + ey * ey);
+  cnt += (r < thresh) ? 1 : 0;
+  return r * r;
+}
+
+// numpy pairwise_sum over residual^2 of points [start, start+n) for n <= 128:
+// n < 8 sequential, else 8 strided accumulators + sequential remainder.
+__device__ __forceinline__ double pw_leaf(const Model& m, const Pts& P, int start, int n, double thresh, int& cnt) {
+  if (n < 8) {
+    double res = 0.0;
+    for (int i = 0; i < n; ++i) res += resid2(m, P, start + i, thresh, cnt);
+    return res;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = resid2(m, P, start + j, thresh, cnt);
+  int i = 8;
+  const int nfull = n - (n % 8);
+  for (; i < nfull; i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] += resid2(m, P, start + i + j, thresh, cnt);
+  }
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += resid2(m, P, start + i, thresh, cnt);
+  return res;
+}
+
+// For n > 128 numpy recurses: pairwise(a, n) = pairwise(a, n2) + pairwise(a + n2, n - n2)
+// with n2 = n/2 rounded down to a multiple of 8.  The split tree depends on N only, so
+// one thread writes it once per frame as a post-order plan: leaves in order, each with
+// the number of "pop b, pop a, push a+b" combines that follow it.  Every thread then
+// evaluates its hypotheses with one copy of the leaf loop and a per-thread stack in LDS.
+constexpr int kMaxLeaves = 128;
+constexpr int kMaxStack = kPwDepth + 2;
+
+struct Plan {
+  int16_t start[kMaxLeaves];
+  int16_t len[kMaxLeaves];
+  int8_t pops[kMaxLeaves];
+  int n;
+};
+
+template <int DEPTH>
+__device__ __forceinline__ void plan_gen(Plan& p, int s, int n) {
+  if (DEPTH == 0 || n <= 128) {
+    p.start[p.n] = (int16_t)s;
+    p.len[p.n] = (int16_t)n;
+    p.pops[p.n] = 0;
+    ++p.n;
+    return;
+  }
+  if constexpr (DEPTH > 0) {
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    plan_gen<DEPTH - 1>(p, s, n2);
+    plan_gen<DEPTH - 1>(p, s + n2, n - n2);
+    ++p.pops[p.n - 1];
+  }
+}
+
+// (count desc, S asc, t asc); invalid trials (NaN S, or 0 inliers with S = inf) never win.
+__device__ __forceinline__ bool better(int c, double S, int t, int bc, double bS, int bt) {
+  if (c != bc) return c > bc;
+  if (S != bS) return S < bS;
+  return t < bt;
+}
+
+__device__ double block_sum(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int w = 0; w < kThreads / 64; ++w) s += red[w];
+  return s;
+}
+
+// LARGE = false handles frames with N <= 128 (one pairwise leaf, fully in registers)
+// and the NaN frames; LARGE = true handles 128 < N <= kMaxN through the split plan.
+template <bool LARGE>
+__global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
+    const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
+    const int32_t* __restrict__ pt_off, int src_stride, const uint32_t* __restrict__ hyp,
+    const int32_t* __restrict__ hyp_off, int hyp_off_len,
+    int T, double thresh, double rate, int n_skip, double* __restrict__ out_params,
+    uint8_t* __restrict__ out_inl, int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ double red[kThreads / 64 * 4];
+  __shared__ int s_best[kThreads / 64 * 2];
+  __shared__ double s_bestS[kThreads / 64];
+  __shared__ int s_any_zero;
+  __shared__ int s_final_t;
+  __shared__ Plan s_plan;
+
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int p0 = pt_off[f];
+  const int N = pt_off[f + 1] - p0;
+
+  const bool skip_frame = N < n_skip || N < 3 || N > kMaxN;
+  const int hoff = (!skip_frame && N < hyp_off_len) ? hyp_off[N] : -1;
+  const bool nan_frame = skip_frame || hoff < 0;
+  if (LARGE != (!nan_frame && N > 128)) return;  // the other launch owns this frame
+  if (nan_frame) {
+    if (tid < 6) out_params[6 * (size_t)f + tid] = NAN;
+    for (int k = tid; k < N; k += kThreads) out_inl[p0 + k] = 0;
+    if (tid == 0) {
+      out_nin[f] = skip_frame ? 0 : -1;  // -1: no hypothesis table was prepared for N
+      out_best[f] = -1;
+    }
+    return;
+  }
+
+  // LDS: sx, sy, dx, dy [N] f64 | trial S [T] f64 | [LARGE: stack [kMaxStack][256] f64]
+  //      | trial count [T] i32 | inlier flags [N] u8
+  double* sx = smem;
+  double* sy = sx + N;
+  double* dxs = sy + N;
+  double* dys = dxs + N;
+  double* tS = dys + N;
+  double* stk = tS + T;
+  int* tC = reinterpret_cast<int*>(stk + (LARGE ? kMaxStack * kThreads : 0));
+  uint8_t* inl = reinterpret_cast<uint8_t*>(tC + T);
+  if (LARGE && tid == 0) {
+    s_plan.n = 0;
+    plan_gen<kPwDepth>(s_plan, 0, N);
+  }
+
+  for (int k = tid; k < N; k += kThreads) {
+    size_t si, di;
+    if (pt_idx) {
+      const int q = pt_idx[p0 + k];
+      si = (size_t)f * src_stride + q;
+      di = (size_t)q;
+    } else {
+      si = di = (size_t)(p0 + k);
+    }
+    sx[k] = src[2 * si];
+    sy[k] = src[2 * si + 1];
+    dxs[k] = dst[2 * di];
+    dys[k] = dst[2 * di + 1];
+  }
+  if (tid == 0) s_any_zero = 0;
+  __syncthreads();
+
+  const Pts P{sx, sy, dxs, dys};
+  const uint32_t* H = hyp + hoff;
+  int bc = -1, bt = INT_MAX;
+  double bS = INFINITY;
+  bool any_zero = false;
+  for (int t = tid; t < T; t += kThreads) {
+    const uint32_t pr = H[t];
+    const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
+    const Model m = fit2(sx[i], sy[i], sx[j], sy[j], dxs[i], dys[i], dxs[j], dys[j]);
+    int cnt = 0;
+    double S = NAN;
+    if (m.ok) {
+      if (!LARGE) {
+        S = pw_leaf(m, P, 0, N, thresh, cnt);
+      } else {
+        int sp = 0;
+        for (int l = 0; l < s_plan.n; ++l) {
+          stk[sp++ * kThreads + tid] = pw_leaf(m, P, s_plan.start[l], s_plan.len[l], thresh, cnt);
+          for (int c = s_plan.pops[l]; c > 0; --c) {
+            const double b = stk[--sp * kThreads + tid];
+            const double a = stk[(sp - 1) * kThreads + tid];
+            stk[(sp - 1) * kThreads + tid] = a + b;
+          }
+        }
+        S = stk[tid];
+      }
+    }
+    tS[t] = S;
+    tC[t] = cnt;
+    const bool valid = !isnan(S) && (cnt > 0 || S < INFINITY);
+    if (valid) {
+      if (S <= 0.0) any_zero = true;
+      if (better(cnt, S, t, bc, bS, bt)) {
+        bc = cnt;
+        bS = S;
+        bt = t;
+      }
+    }
+  }
+  // workgroup argmax of (count, -S, -t)
+  for (int o = 32; o > 0; o >>= 1) {
+    const int oc = __shfl_xor(bc, o);
+    const double oS = __shfl_xor(bS, o);
+    const int ot = __shfl_xor(bt, o);
+    if (better(oc, oS, ot, bc, bS, bt)) {
+      bc = oc;
+      bS = oS;
+      bt = ot;
+    }
+  }
+  if (lane == 0) {
+    s_best[2 * wave] = bc;
+    s_best[2 * wave + 1] = bt;
+    s_bestS[wave] = bS;
+  }
+  if (any_zero) atomicOr(&s_any_zero, 1);
+  __syncthreads();
+  if (tid == 0) {
+    int fc = -1, ft = INT_MAX;
+    double fS = INFINITY;
+    for (int w = 0; w < kThreads / 64; ++w)
+      if (better(s_best[2 * w], s_bestS[w], s_best[2 * w + 1], fc, fS, ft)) {
+        fc = s_best[2 * w];
+        fS = s_bestS[w];
+        ft = s_best[2 * w + 1];
+      }
+    if (s_any_zero) {
+      // skimage stops as soon as the running best has S <= 0 (fit.py:862-869):
+      // replay the trial sequence to find where it stopped.
+      int c0 = 0, t0 = -1;
+      double S0 = INFINITY;
+      for (int t = 0; t < T; ++t) {
+        const double S = tS[t];
+        const int c = tC[t];
+        if (isnan(S)) continue;
+        if (c > c0 || (c == c0 && S < S0)) {
+          c0 = c;
+          S0 = S;
+          t0 = t;
+          if (S0 <= 0.0) break;
+        }
+      }
+      ft = t0;
+      fc = c0;
+    }
+    s_final_t = (ft == INT_MAX) ? -1 : ft;
+  }
+  __syncthreads();
+  const int best_t = s_final_t;
+
+  // inlier mask of the best hypothesis (same arithmetic as the scoring loop)
+  int nin_local = 0;
+  Model bm{0, 0, 0, 0, false};
+  if (best_t >= 0) {
+    const uint32_t pr = H[best_t];
+    const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
+    bm = fit2(sx[i], sy[i], sx[j], sy[j], dxs[i], dys[i], dxs[j], dys[j]);
+  }
+  for (int k = tid; k < N; k += kThreads) {
+    int c = 0;
+    if (bm.ok) resid2(bm, P, k, thresh, c);
+    inl[k] = (uint8_t)c;
+    out_inl[p0 + k] = (uint8_t)c;
+    nin_local += c;
+  }
+  __syncthreads();
+  // refit on the inliers (skimage fit.py:871-875 -> _umeyama over d[best_inliers])
+  double s0 = 0, s1 = 0, s2 = 0, s3 = 0, cntd = 0;
+  for (int k = tid; k < N; k += kThreads)
+    if (inl[k]) {
+      s0 += sx[k];
+      s1 += sy[k];
+      s2 += dxs[k];
+      s3 += dys[k];
+      cntd += 1.0;
+    }
+  const double n_in = block_sum(cntd, red);
+  const double ms0 = block_sum(s0, red) / n_in;
+  const double ms1 = block_sum(s1, red) / n_in;
+  const double md0 = block_sum(s2, red) / n_in;
+  const double md1 = block_sum(s3, red) / n_in;
+  double a00 = 0, a01 = 0, a10 = 0, a11 = 0;
+  for (int k = tid; k < N; k += kThreads)
+    if (inl[k]) {
+      const double u0 = sx[k] - ms0, u1 = sy[k] - ms1;
+      const double v0 = dxs[k] - md0, v1 = dys[k] - md1;
+      a00 += v0 * u0;
+      a01 += v0 * u1;
+      a10 += v1 * u0;
+      a11 += v1 * u1;
+    }
+  a00 = block_sum(a00, red);
+  a01 = block_sum(a01, red);
+  a10 = block_sum(a10, red);
+  a11 = block_sum(a11, red);
+  if (tid == 0) {
+    double* o = out_params + 6 * (size_t)f;
+    const double a = a00 + a11, b = a10 - a01;
+    if (n_in > 0.0 && !(a == 0.0 && b == 0.0)) {
+      const double hn = sqrt(a * a + b * b);
+      const double c = a / hn, s = b / hn;
+      o[0] = c;
+      o[1] = -s;
+      o[2] = (md0 - (c * ms0 - s * ms1)) * rate;
+      o[3] = s;
+      o[4] = c;
+      o[5] = (md1 - (s * ms0 + c * ms1)) * rate;
+    } else {
+      for (int k = 0; k < 6; ++k) o[k] = NAN;
+    }
+    out_nin[f] = (int32_t)n_in;
+    out_best[f] = best_t;
+  }
+  (void)nin_local;
+}
+
+}  // namespace
+}  // namespace kcmc
+
+using namespace kcmc;
+
+extern "C" int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src, const double* dst, const int32_t* pt_idx,
+                                 const int32_t* pt_off, int src_frame_stride, int n_frames, int max_n, int trials,
+                                 double thresh, double rate, int n_skip, double* out_params, uint8_t* out_inliers,
+                                 int32_t* out_n_inliers, int32_t* out_best_trial, kcmc_stream_t stream) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_ransac_rigid: ctx is NULL");
+  if (n_frames < 0 || max_n < 0 || trials < 1) return fail(KCMC_EINVAL, "kcmc_ransac_rigid: bad sizes");
+  if (n_frames == 0) return KCMC_OK;
+  if (!pt_off || !out_params || !out_n_inliers || !out_best_trial || (max_n > 0 && (!src || !dst || !out_inliers)))
+    return fail(KCMC_EINVAL, "kcmc_ransac_rigid: NULL pointer");
+  if (max_n > kMaxN) return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_rigid: max_n > 4096 points per frame");
+  if (pt_idx && src_frame_stride <= 0) return fail(KCMC_EINVAL, "kcmc_ransac_rigid: src_frame_stride must be > 0");
+  const int need = max_n < 3 ? 3 : max_n;
+  if (!ctx->hyp || ctx->hyp_trials != trials)
+    return fail(KCMC_EINVAL, "kcmc_ransac_rigid: hypothesis tables not prepared for trials=" +
+                                 std::to_string(trials) + " (call kcmc_ransac_prepare)");
+  const int n_small = need < 128 ? need : 128;
+  const size_t lds_small =
+      (size_t)n_small * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) + (size_t)n_small + 16;
+  const size_t lds_large = (size_t)need * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) +
+                           (size_t)kMaxStack * kThreads * sizeof(double) + (size_t)need + 16;
+  if ((max_n > 128 ? lds_large : lds_small) > 150 * 1024)
+    return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_rigid: max_n/trials exceed the LDS budget");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(ransac_rigid_kernel<false>, dim3(n_frames), dim3(kThreads), lds_small, s, src, dst, pt_idx,
+                     pt_off, src_frame_stride, ctx->hyp, ctx->hyp_off, ctx->hyp_off_len, trials, thresh, rate, n_skip, out_params,
+                     out_inliers, out_n_inliers, out_best_trial);
+  KCMC_TRY(launch_check("ransac_rigid_kernel<small>"));
+  if (max_n > 128) {
+    hipLaunchKernelGGL(ransac_rigid_kernel<true>, dim3(n_frames), dim3(kThreads), lds_large, s, src, dst, pt_idx,
+                       pt_off, src_frame_stride, ctx->hyp, ctx->hyp_off, ctx->hyp_off_len, trials, thresh, rate, n_skip, out_params,
+                       out_inliers, out_n_inliers, out_best_trial);
+    KCMC_TRY(launch_check("ransac_rigid_kernel<large>"));
+  }
+  return KCMC_OK;
+}

@@ -1,0 +1,146 @@
+"""The batched alignment hot path of one frame slab on one GPU.
+
+match (K1, GPU) -> consensus (host, native) -> RANSAC (K2, GPU) -> affine
+post-processing (host) -> warp (K3, GPU).  This is VideoAligner.align_images
+(VA:57-158) after detection, with the three joblib stages (VA:117-123, 137-142, 150)
+replaced by one batched launch each.  Frames and keypoints stay resident in HBM;
+only survivor bitmasks (F x n_tpl/8 B), RANSAC point lists and 2x3 affines cross
+PCIe.
+"""
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import affines as _aff
+from . import stages
+
+
+@dataclass
+class AlignConfig:
+    """The reference's class constants that steer the hot path (VA:19-45)."""
+
+    n_kp_global: int
+    n_kp_global_min: int = 5            # N_KP_GLOBAL_MIN
+    n_kp_frame_skip: int = 3            # N_KP_FRAME_SKIP
+    ratio: float = 0.75                 # DESCRIPTOR_DISTANCE_RATIO_THRESH
+    d_lo: float = 0.5                   # (d_1, d_2) hard-coded at VA:209
+    d_hi: float = 2.0
+    ransac_trials: int = 1000           # RANSAC_MAX_TRIALS
+    ransac_threshold: float = 2.0       # RANSAC_RESIDUAL_THRESH
+    ransac_min_samples: int = 2         # RANSAC_MIN_SAMPLES
+    seed: int = 42                      # RANDOM_SEED
+    spatial_rate: float = 1             # SPATIAL_DOWNSAMPLE_RATE
+    frame_downsample_rate: int = 1      # max(1, frame_rate // FRAME_SAMPLE_RATE)
+
+
+@dataclass
+class SlabInputs:
+    """Device-resident inputs of one slab.  Keypoints/descriptors are per SAMPLE frame
+    (images[::frame_downsample_rate]); frames are the full uint16 stack to warp."""
+
+    frames: torch.Tensor          # [F, H, W] (or [F, H, W, C]) uint16
+    des_tpl: torch.Tensor         # [n_tpl, D] uint8
+    kp_tpl: torch.Tensor          # [n_tpl, 2] float64
+    des_q: torch.Tensor           # [P, D] uint8, CSR over sample frames
+    kp_q: torch.Tensor            # [P, 2] float64
+    q_off: torch.Tensor           # [S+1] int32 (device)
+    q_off_host: np.ndarray        # same offsets on the host
+
+
+@dataclass
+class SlabResult:
+    aligned: torch.Tensor
+    affines: np.ndarray           # [S*rate, 2, 3] after interpolation (VA:143-144)
+    euclidean: np.ndarray         # [S*rate, 3]
+    skipped: List[int]
+    interpolated: List[int]
+    match: Optional[stages.MatchResult] = None
+    consensus: Optional[stages.Consensus] = None
+    ransac: Optional[stages.RansacResult] = None
+    log_counts: Optional[np.ndarray] = None
+    extras: dict = field(default_factory=dict)
+
+
+def log_frame_counts(logger: logging.Logger, counts: np.ndarray, first_index: int = 0) -> None:
+    """The per-frame debug lines of VA:215-221 / VA:125-126."""
+    if not logger.isEnabledFor(logging.DEBUG):
+        return
+    for k, c in enumerate(counts):
+        logger.debug(
+            f"frame {first_index + k}:\n"
+            f"\t{int(c[0])} unfiltered features identified\n"
+            f"\t{int(c[1])} matches identified between frame and template\n"
+            f"\t{int(c[2])} matches after feature-space ratio filter\n"
+            f"\t{int(c[3])} matches after distance-based outlier rejection"
+        )
+
+
+def match_stage(inp: SlabInputs, cfg: AlignConfig) -> stages.MatchResult:
+    return stages.match_frames(inp.des_tpl, inp.kp_tpl, inp.des_q, inp.kp_q, inp.q_off, inp.q_off_host,
+                               ratio=cfg.ratio, d_lo=cfg.d_lo, d_hi=cfg.d_hi)
+
+
+def consensus_stage(keep_bits_host: np.ndarray, n_tpl: int, n_frames: int, cfg: AlignConfig,
+                    logger: Optional[logging.Logger] = None) -> stages.Consensus:
+    cons = stages.consensus(keep_bits_host, n_tpl, cfg.n_kp_global, cfg.n_kp_global_min)
+    if logger is not None and logger.isEnabledFor(logging.INFO):
+        rates = np.array(cons.votes, dtype=np.int64) / n_frames
+        logger.info(f"top n keypoints match rates: {rates}")
+        ns = np.diff(cons.pt_off)
+        for i in np.flatnonzero(ns < cfg.n_kp_frame_skip):
+            logger.info(
+                f"transform for frame {int(i)} not estimated due to low keypoint count: "
+                f"({int(ns[i])}). Will be interpolated based on other frames instead"
+            )
+    return cons
+
+
+def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.Consensus,
+                 cfg: AlignConfig) -> stages.RansacResult:
+    dev = kp_tpl.device
+    F, n_tpl = match.kp_ordered.shape[:2]
+    pt_off = torch.from_numpy(cons.pt_off).to(dev, non_blocking=False)
+    pt_idx = torch.from_numpy(cons.pt_idx if cons.pt_idx.size else np.zeros(1, np.int32)).to(dev)
+    return stages.ransac_rigid(match.kp_ordered.view(F * n_tpl, 2), kp_tpl, pt_off, cons.pt_off, pt_idx=pt_idx,
+                               src_frame_stride=n_tpl, trials=cfg.ransac_trials,
+                               residual_threshold=cfg.ransac_threshold, spatial_rate=cfg.spatial_rate,
+                               n_skip=cfg.n_kp_frame_skip, seed=cfg.seed, min_samples=cfg.ransac_min_samples)
+
+
+def postprocess_affines(params_host: np.ndarray, cfg: AlignConfig):
+    """VA:143-145 on the host: NaN-pad, interpolate, Euclidean summary."""
+    affines, skipped = _aff.process_affines(list(params_host), cfg.frame_downsample_rate)
+    affines, interpolated = _aff.interpolate_affines(affines)
+    return affines, skipped, interpolated, _aff.euclidean_transforms(affines)
+
+
+def warp_stage(frames: torch.Tensor, affines: np.ndarray, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    F = frames.shape[0]
+    a = torch.from_numpy(np.ascontiguousarray(affines[:F], dtype=np.float64)).to(frames.device)
+    return stages.warp_affine_u16(frames, a, out=out)
+
+
+def align_slab(inp: SlabInputs, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
+               out: Optional[torch.Tensor] = None, keep_intermediates: bool = False) -> SlabResult:
+    """Run the whole hot path for one slab on the slab's device."""
+    logger = logger or logging.getLogger("VideoAligner")
+    n_tpl = inp.des_tpl.shape[0]
+    n_sample = inp.q_off.numel() - 1
+    match = match_stage(inp, cfg)
+    counts = match.counts.cpu().numpy() if logger.isEnabledFor(logging.DEBUG) else None
+    if counts is not None:
+        log_frame_counts(logger, counts)
+    keep = match.keep_bits.cpu().numpy()
+    cons = consensus_stage(keep, n_tpl, n_sample, cfg, logger)
+    rr = ransac_stage(match, inp.kp_tpl, cons, cfg)
+    params = rr.params.cpu().numpy()
+    affines, skipped, interpolated, eu = postprocess_affines(params, cfg)
+    aligned = warp_stage(inp.frames, affines, out=out)
+    return SlabResult(aligned, affines, eu, skipped, interpolated,
+                      match if keep_intermediates else None, cons if keep_intermediates else None,
+                      rr if keep_intermediates else None, counts)

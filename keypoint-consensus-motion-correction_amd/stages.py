@@ -1,0 +1,270 @@
+"""Batched hot-path stages on device-resident buffers (torch ROCm tensors as memory).
+
+Each function launches HIP kernels from libkcmc.so through the C ABI
+(include/kcmc.h) on the tensors' device and torch's current stream for that
+device; nothing here computes on the CPU except the consensus, which is host
+logic in the reference too (VA:224-286) and runs in native code.
+
+Reference seams replaced (reference: /root/reference/VideoAligner.py):
+  match_frames   <- _parallelize_i(_get_frame_keypoints, ...) matching part, VA:117-123 / VA:194-214
+  consensus      <- _get_consensus_kps + _lookup_consensus_kps, VA:131-132 / VA:224-286
+  ransac_rigid   <- _parallelize(_compute_euclidean_affine, ...), VA:137-142 / VA:288-323
+  warp_affine    <- _parallelize(_apply_affine, images, affines), VA:150 / VA:455-458
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_P = ctypes.c_void_p
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return _P(t.data_ptr()) if t is not None and t.numel() > 0 else _P(0)
+
+
+def _np_ptr(a: Optional[np.ndarray]):
+    return a.ctypes.data_as(_P) if a is not None and a.size > 0 else _P(0)
+
+
+def _require(t: torch.Tensor, name: str, dtype: torch.dtype, device: torch.device, ndim: Optional[int] = None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor, got {type(t).__name__}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected dtype {dtype}, got {t.dtype}")
+    if t.device != device:
+        raise ValueError(f"{name}: expected device {device}, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+    if ndim is not None and t.dim() != ndim:
+        raise ValueError(f"{name}: expected {ndim} dims, got shape {tuple(t.shape)}")
+
+
+def _device_of(t: torch.Tensor) -> torch.device:
+    if t.device.type != "cuda":
+        raise _lib.KcmcLibraryError(
+            "kcmc runs on the GPU only: pass device tensors (torch ROCm 'cuda' device); "
+            "there is no CPU fallback for the alignment hot path"
+        )
+    return t.device
+
+
+def _stream(device: torch.device):
+    return _P(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ctx(device: torch.device) -> _lib.Context:
+    return _lib.context(device.index if device.index is not None else torch.cuda.current_device())
+
+
+# ----------------------------------------------------------------------- K1
+@dataclass
+class MatchResult:
+    idx: torch.Tensor          # [F, n_tpl, 2] i32  frame-keypoint index of best / 2nd best
+    dist: torch.Tensor         # [F, n_tpl, 2] f32  OpenCV NORM_L2 distance
+    kp_ordered: torch.Tensor   # [F, n_tpl, 2] f64  kp_query reordered to the template (VA:197-200)
+    keep_bits: torch.Tensor    # [F, ceil(n_tpl/32)] i32 (bit pattern of u32) survivors of VA:202-213
+    counts: torch.Tensor       # [F, 4] i32  numbers of the per-frame debug log (VA:215-221)
+
+
+def _check_offsets(q_off_host: np.ndarray, n_frames: int) -> None:
+    if q_off_host.shape != (n_frames + 1,) or q_off_host[0] != 0 or np.any(np.diff(q_off_host) < 0):
+        raise ValueError("q_off must be [F+1] non-decreasing CSR offsets starting at 0")
+
+
+def knn2_l2u8(des_tpl: torch.Tensor, des_q: torch.Tensor, q_off: torch.Tensor, max_nq: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """cv2.BFMatcher().knnMatch(des_tpl, des_q[frame], k=2) for every frame at once."""
+    dev = _device_of(des_tpl)
+    _require(des_tpl, "des_tpl", torch.uint8, dev, 2)
+    _require(des_q, "des_q", torch.uint8, dev, 2)
+    _require(q_off, "q_off", torch.int32, dev, 1)
+    n_tpl, D = des_tpl.shape
+    F = q_off.numel() - 1
+    idx = torch.empty((F, n_tpl, 2), dtype=torch.int32, device=dev)
+    dist = torch.empty((F, n_tpl, 2), dtype=torch.float32, device=dev)
+    L = _lib.load()
+    _lib.check(L.kcmc_knn2_l2u8(_ctx(dev).handle, _ptr(des_tpl), n_tpl, D, _ptr(des_q), _ptr(q_off), F, int(max_nq),
+                                _ptr(idx), _ptr(dist), _stream(dev)))
+    return idx, dist
+
+
+def match_frames(
+    des_tpl: torch.Tensor,
+    kp_tpl: torch.Tensor,
+    des_q: torch.Tensor,
+    kp_q: torch.Tensor,
+    q_off: torch.Tensor,
+    q_off_host: np.ndarray,
+    ratio: float = 0.75,
+    d_lo: float = 0.5,
+    d_hi: float = 2.0,
+) -> MatchResult:
+    """VA:194-214 for every frame: knn k=2 + reorder + ratio + median filters."""
+    dev = _device_of(des_tpl)
+    _require(des_tpl, "des_tpl", torch.uint8, dev, 2)
+    _require(kp_tpl, "kp_tpl", torch.float64, dev, 2)
+    _require(des_q, "des_q", torch.uint8, dev, 2)
+    _require(kp_q, "kp_q", torch.float64, dev, 2)
+    _require(q_off, "q_off", torch.int32, dev, 1)
+    n_tpl, D = des_tpl.shape
+    F = q_off.numel() - 1
+    q_off_host = np.asarray(q_off_host)
+    _check_offsets(q_off_host, F)
+    nq = np.diff(q_off_host)
+    if F and n_tpl and nq.min() < 2:
+        bad = int(np.argmin(nq))
+        raise ValueError(f"frame {bad} has {int(nq[bad])} keypoints; knnMatch(k=2) needs >= 2 (VA:203)")
+    if kp_tpl.shape != (n_tpl, 2) or kp_q.shape[0] != des_q.shape[0] or int(q_off_host[-1]) > des_q.shape[0]:
+        raise ValueError("keypoint/descriptor shapes disagree")
+    words = (n_tpl + 31) // 32
+    res = MatchResult(
+        idx=torch.empty((F, n_tpl, 2), dtype=torch.int32, device=dev),
+        dist=torch.empty((F, n_tpl, 2), dtype=torch.float32, device=dev),
+        kp_ordered=torch.empty((F, n_tpl, 2), dtype=torch.float64, device=dev),
+        keep_bits=torch.empty((F, words), dtype=torch.int32, device=dev),
+        counts=torch.empty((F, 4), dtype=torch.int32, device=dev),
+    )
+    L = _lib.load()
+    _lib.check(L.kcmc_match_frames(
+        _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F,
+        int(nq.max()) if F else 0, float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist),
+        _ptr(res.kp_ordered), _ptr(res.keep_bits), _ptr(res.counts), _stream(dev)))
+    return res
+
+
+# ------------------------------------------------------------------ consensus
+@dataclass
+class Consensus:
+    order: np.ndarray    # [n] i32 template indices in Counter.most_common order
+    votes: np.ndarray    # [n] i32 vote counts
+    pt_off: np.ndarray   # [F+1] i32 CSR offsets of per-frame RANSAC point lists
+    pt_idx: np.ndarray   # [P] i32 template indices in CPython set-iteration order (VA:274)
+
+
+def consensus(keep_bits: np.ndarray, n_tpl: int, n_kp_global: int, n_min: int) -> Consensus:
+    """VA:224-286 in native code with CPython set/Counter ordering."""
+    kb = np.ascontiguousarray(keep_bits).view(np.uint32)
+    F = kb.shape[0]
+    if kb.shape != (F, (n_tpl + 31) // 32):
+        raise ValueError("keep_bits must be [F, ceil(n_tpl/32)]")
+    n_kp_global = int(n_kp_global)
+    cons = np.zeros(max(n_kp_global, 1), np.int32)
+    votes = np.zeros(max(n_kp_global, 1), np.int32)
+    n_c = ctypes.c_int(0)
+    pt_off = np.zeros(F + 1, np.int32)
+    pt_idx = np.zeros(max(F * max(n_kp_global, 0), 1), np.int32)
+    L = _lib.load()
+    _lib.check(L.kcmc_consensus(_np_ptr(kb), F, int(n_tpl), n_kp_global, int(n_min), _np_ptr(cons), _np_ptr(votes),
+                                ctypes.byref(n_c), _np_ptr(pt_off), _np_ptr(pt_idx)))
+    n = n_c.value
+    return Consensus(cons[:n].copy(), votes[:n].copy(), pt_off, pt_idx[: pt_off[-1]].copy())
+
+
+def hypothesis_table(n: int, trials: int = 1000, seed: int = 42, min_samples: int = 2) -> np.ndarray:
+    """The per-trial samples skimage 0.18.3's ransac draws (legacy MT19937)."""
+    out = np.empty((trials, min_samples), np.int32)
+    _lib.check(_lib.load().kcmc_hypothesis_table(int(n), int(trials), int(seed) & 0xFFFFFFFF, int(min_samples),
+                                                 _np_ptr(out)))
+    return out
+
+
+# ----------------------------------------------------------------------- K2
+@dataclass
+class RansacResult:
+    params: torch.Tensor       # [F, 2, 3] f64 (NaN where the reference returns NaN)
+    inliers: torch.Tensor      # [P] u8 inlier mask of the best hypothesis (CSR like the points)
+    n_inliers: torch.Tensor    # [F] i32
+    best_trial: torch.Tensor   # [F] i32 (-1: none)
+
+
+def ransac_rigid(
+    src: torch.Tensor,
+    dst: torch.Tensor,
+    pt_off: torch.Tensor,
+    pt_off_host: np.ndarray,
+    pt_idx: Optional[torch.Tensor] = None,
+    src_frame_stride: int = 0,
+    trials: int = 1000,
+    residual_threshold: float = 2.0,
+    spatial_rate: float = 1.0,
+    n_skip: int = 3,
+    seed: int = 42,
+    min_samples: int = 2,
+) -> RansacResult:
+    """skimage ransac(EuclideanTransform) per frame (VA:288-323), all frames in one launch.
+
+    With ``pt_idx``: point k of frame f is src[f*src_frame_stride + pt_idx[k]] /
+    dst[pt_idx[k]] (src = kp_ordered [F*n_tpl, 2], dst = template keypoints).
+    """
+    dev = _device_of(src)
+    _require(src, "src", torch.float64, dev, 2)
+    _require(dst, "dst", torch.float64, dev, 2)
+    _require(pt_off, "pt_off", torch.int32, dev, 1)
+    if pt_idx is not None:
+        _require(pt_idx, "pt_idx", torch.int32, dev, 1)
+    if min_samples != 2:
+        raise ValueError("rigid RANSAC uses min_samples=2 (EuclideanTransform, VA:312)")
+    F = pt_off.numel() - 1
+    pt_off_host = np.asarray(pt_off_host)
+    _check_offsets(pt_off_host, F)
+    ns = np.diff(pt_off_host)
+    # skimage raises when a frame is not skipped but has N <= min_samples (fit.py:798-799)
+    bad = (ns >= n_skip) & (ns <= min_samples)
+    if bad.any():
+        raise ValueError("`min_samples` must be in range (0, <number-of-samples>)")
+    max_n = int(ns.max()) if F else 0
+    P = int(pt_off_host[-1]) if F else 0
+    res = RansacResult(
+        params=torch.empty((F, 2, 3), dtype=torch.float64, device=dev),
+        inliers=torch.empty((max(P, 0),), dtype=torch.uint8, device=dev),
+        n_inliers=torch.empty((F,), dtype=torch.int32, device=dev),
+        best_trial=torch.empty((F,), dtype=torch.int32, device=dev),
+    )
+    if F == 0:
+        return res
+    ctx = _ctx(dev)
+    L = _lib.load()
+    n_run = np.unique(ns[ns >= max(int(n_skip), 3)]).astype(np.int32)
+    _lib.check(L.kcmc_ransac_prepare(ctx.handle, _np_ptr(n_run), int(n_run.size), int(trials),
+                                     int(seed) & 0xFFFFFFFF))
+    _lib.check(L.kcmc_ransac_rigid(
+        ctx.handle, _ptr(src), _ptr(dst), _ptr(pt_idx), _ptr(pt_off), int(src_frame_stride), F, max_n, int(trials),
+        float(residual_threshold), float(spatial_rate), int(n_skip), _ptr(res.params), _ptr(res.inliers),
+        _ptr(res.n_inliers), _ptr(res.best_trial), _stream(dev)))
+    return res
+
+
+# ----------------------------------------------------------------------- K3
+def warp_affine_u16(frames: torch.Tensor, affines: torch.Tensor, out: Optional[torch.Tensor] = None,
+                    inverse_map: bool = False) -> torch.Tensor:
+    """cv2.warpAffine(frame, M, (W, H), INTER_LINEAR) for every frame (VA:458).
+
+    frames [F, H, W] or [F, H, W, C] uint16 on the device; affines [F, 2, 3] f64.
+    """
+    dev = _device_of(frames)
+    if frames.dtype != torch.uint16:
+        raise TypeError(f"frames: expected torch.uint16, got {frames.dtype}")
+    if frames.dim() not in (3, 4):
+        raise ValueError("frames must be [F, H, W] or [F, H, W, C]")
+    _require(frames, "frames", torch.uint16, dev)
+    _require(affines, "affines", torch.float64, dev, 3)
+    F, H, W = frames.shape[:3]
+    C = 1 if frames.dim() == 3 else frames.shape[3]
+    if affines.shape != (F, 2, 3):
+        raise ValueError(f"affines must be [{F}, 2, 3], got {tuple(affines.shape)}")
+    if out is None:
+        out = torch.empty_like(frames)
+    else:
+        _require(out, "out", torch.uint16, dev)
+        if out.shape != frames.shape:
+            raise ValueError("out must have the shape of frames")
+    L = _lib.load()
+    _lib.check(L.kcmc_warp_affine_u16(_ctx(dev).handle, _ptr(frames), _ptr(out), _ptr(affines), F, H, W, C,
+                                      int(bool(inverse_map)), _stream(dev)))
+    return out

@@ -1,0 +1,368 @@
+"""VideoAligner with the reference's public surface, running the hot path on MI355X.
+
+Mirror of /root/reference/VideoAligner.py (VA:15-510): same class names, class
+constants, ``align_images`` signature/returns and per-frame static helpers.  The
+per-frame joblib stages (VA:117-123, 137-142, 150) are replaced by one batched HIP
+launch each (``pipeline.align_slab``); the helpers that the reference runs per frame
+(``_get_frame_keypoints``, ``_compute_euclidean_affine``, ``_apply_affine``) run the
+same kernels on a batch of one, so code written against the reference keeps working.
+
+Differences, all deliberate:
+  * Keypoint detection still needs an OpenCV-compatible detector object
+    (``detectAndCompute(img, mask) -> (keypoints with .pt, uint8 descriptors)``).
+    OpenCV is not part of this image; ``DETECTOR_CONSTRUCTOR_DICT`` uses cv2 when it is
+    importable and accepts any registered factory.  ``align_keypoints`` is the hot-path
+    entry for precomputed keypoints/descriptors.
+  * numpy >= 1.24 made the reference crash on ragged per-frame point lists (VA:284-285);
+    ``_lookup_consensus_kps`` returns numpy<1.24-style object arrays instead.
+  * Constants are read from the instance's class, so subclass overrides take effect
+    everywhere (the reference's static methods read ``VideoAligner.X``; defaults equal).
+"""
+from __future__ import annotations
+
+import time
+from collections import Counter
+from logging import LoggerAdapter, getLogger
+from multiprocessing import cpu_count
+from typing import Callable, List, Optional, Sequence, Set, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import affines as _aff
+from . import pipeline as _pl
+from . import stages
+from .affines import AlignmentError
+
+
+def _cv2_factory(name: str) -> Callable:
+    def make():
+        try:
+            import cv2  # type: ignore
+        except ImportError as e:  # pragma: no cover - cv2 absent in this image
+            raise RuntimeError(
+                f"OpenCV is not installed, so '{name}' is unavailable: register a detector factory in "
+                "VideoAligner.DETECTOR_CONSTRUCTOR_DICT or call align_keypoints() with precomputed keypoints"
+            ) from e
+        return getattr(cv2, name)()
+
+    make.__name__ = name
+    return make
+
+
+def _as_numpy(x) -> np.ndarray:
+    return x.cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
+
+
+class VideoAligner:
+    AlignmentError = AlignmentError
+
+    FRAME_SAMPLE_RATE = 100  # Hz
+    SPATIAL_DOWNSAMPLE_RATE = 1
+    N_JOBS_PARALLEL = cpu_count()
+    DETECTOR_CONSTRUCTOR_DICT = {
+        "akaze": _cv2_factory("AKAZE_create"),
+        "brisk": _cv2_factory("BRISK_create"),
+    }
+    N_KP_GLOBAL_MIN = 5
+    N_KP_FRAME_SKIP = 3
+    TEMPLATE_FRAME_LOC = 0.5
+    MAX_FRAC_INTERPOLATED = 0.2
+    DESCRIPTOR_DISTANCE_RATIO_THRESH = 0.75
+    MEDIAN_KEYPOINT_INLIER_DISTANCE_RANGE = (0.5, 2.0)
+    IMAGE_NORM_MAX_PERCENTILE = 99.99
+    MAX_PIXEL_UINT8 = 255
+    RANSAC_MIN_SAMPLES = 2
+    RANSAC_RESIDUAL_THRESH = 2
+    RANSAC_MAX_TRIALS = 1000
+    RANDOM_SEED = 42
+    # New: which GPU runs the hot path (None = torch's current device).
+    DEVICE: Optional[int] = None
+
+    def __init__(self, logger: LoggerAdapter = None):
+        self.logger = logger
+        if self.logger is None:
+            self.logger = getLogger(self.__class__.__name__)
+        self.affines = None
+        self.aligned_imgs = None
+        self.interpolated_idxs = None
+        self._kp_template = None
+        self._des_template = None
+
+    # ------------------------------------------------------------------ helpers
+    @classmethod
+    def _device(cls) -> torch.device:
+        if not torch.cuda.is_available():
+            from ._lib import KcmcLibraryError
+
+            raise KcmcLibraryError("no GPU visible: the kcmc hot path runs on MI355X only (no CPU fallback)")
+        idx = cls.DEVICE if cls.DEVICE is not None else torch.cuda.current_device()
+        return torch.device("cuda", idx)
+
+    def _config(self, n_kp_global: int, frame_downsample_rate: int = 1) -> _pl.AlignConfig:
+        cls = type(self)
+        d_lo, d_hi = (0.5, 2)  # hard-coded at VA:209 (MEDIAN_KEYPOINT_INLIER_DISTANCE_RANGE is unused there)
+        return _pl.AlignConfig(
+            n_kp_global=int(n_kp_global), n_kp_global_min=cls.N_KP_GLOBAL_MIN, n_kp_frame_skip=cls.N_KP_FRAME_SKIP,
+            ratio=cls.DESCRIPTOR_DISTANCE_RATIO_THRESH, d_lo=d_lo, d_hi=d_hi, ransac_trials=cls.RANSAC_MAX_TRIALS,
+            ransac_threshold=float(cls.RANSAC_RESIDUAL_THRESH), ransac_min_samples=cls.RANSAC_MIN_SAMPLES,
+            seed=cls.RANDOM_SEED, spatial_rate=cls.SPATIAL_DOWNSAMPLE_RATE,
+            frame_downsample_rate=int(frame_downsample_rate))
+
+    # ------------------------------------------------------------- public API
+    def align_images(
+        self,
+        images: np.ndarray,
+        n_kp_global: int,
+        detector_algorithm: str,
+        frame_rate: int,
+        masked_template: Optional[np.ndarray] = None,
+        patch: Optional[Tuple[float, float, float, float]] = None,
+    ) -> Tuple[np.ndarray, np.ndarray, List[int]]:
+        """Register a uint16 stack [frames, x, y] to a template frame (VA:57-158).
+
+        Returns (aligned_imgs, euclidean_transforms [n, 3] = (tx, ty, rotation),
+        skipped_idxs).  A device tensor input yields a device tensor output.
+        """
+        self.logger.info(f"aligning {len(images)} frames with n_kp_global: {n_kp_global} and {detector_algorithm}")
+        if not 0 <= self.TEMPLATE_FRAME_LOC <= 1:
+            raise ValueError("`template_frame_loc` must be between 0 and 1")
+        images_np = _as_numpy(images)
+        if masked_template is not None:
+            template = _as_numpy(masked_template)
+        else:
+            template_idx = int(len(images_np) * self.TEMPLATE_FRAME_LOC)
+            template = images_np[template_idx]
+            self.logger.info(f"no masked template provided. Using frame {template_idx} as template")
+
+        self.logger.info("normalizing frames...")
+        t_start = time.time()
+        brightest_px = self._get_brightest_px(images_np)
+        images_i8, template_i8 = self._max_scale_images(images_np, template, brightest_px, np.uint8)
+        assert images_np.dtype == np.uint16 and images_i8.dtype == np.uint8
+        frame_downsample_rate = max(1, frame_rate // self.FRAME_SAMPLE_RATE)
+        images_sample, template = self._downsample(images_i8, template_i8, frame_downsample_rate,
+                                                   self.SPATIAL_DOWNSAMPLE_RATE)
+        self.logger.info(f"normalized frames in: {round(time.time() - t_start)} s")
+
+        self.logger.info("identifying keypoints...")
+        t_start = time.time()
+        detector = self.DETECTOR_CONSTRUCTOR_DICT[detector_algorithm]()
+        kp_t, des_t = detector.detectAndCompute(template, None)
+        self._kp_template = np.array([p.pt for p in kp_t])
+        self._des_template = des_t
+        kp_list, des_list = [], []
+        for img in images_sample:
+            kq, dq = detector.detectAndCompute(img, None)
+            kp_list.append(np.array([p.pt for p in kq], dtype=np.float64).reshape(-1, 2))
+            des_list.append(np.asarray(dq, dtype=np.uint8).reshape(len(kq), -1))
+        self.logger.info(f"identified keypoints in: {round(time.time() - t_start)} s")
+        return self._align_detected(images, self._kp_template, self._des_template, kp_list, des_list, n_kp_global,
+                                    frame_downsample_rate, patch)
+
+    def align_keypoints(
+        self,
+        images,
+        kp_template: np.ndarray,
+        des_template: np.ndarray,
+        kp_query: Sequence[np.ndarray],
+        des_query: Sequence[np.ndarray],
+        n_kp_global: int,
+        frame_rate: int = 30,
+        patch: Optional[Tuple[float, float, float, float]] = None,
+    ):
+        """The hot path with precomputed keypoints: per SAMPLE frame
+        (images[::max(1, frame_rate // FRAME_SAMPLE_RATE)]) keypoint coordinates [n, 2]
+        and uint8 descriptors [n, D]; template keypoints/descriptors likewise."""
+        self._kp_template = np.asarray(kp_template, dtype=np.float64).reshape(-1, 2)
+        self._des_template = np.asarray(des_template, dtype=np.uint8)
+        rate = max(1, frame_rate // self.FRAME_SAMPLE_RATE)
+        return self._align_detected(images, self._kp_template, self._des_template, list(kp_query), list(des_query),
+                                    n_kp_global, rate, patch)
+
+    def _align_detected(self, images, kp_template, des_template, kp_list, des_list, n_kp_global, rate, patch):
+        dev = self._device()
+        to_host = not isinstance(images, torch.Tensor)
+        frames = torch.from_numpy(np.ascontiguousarray(images)).to(dev) if to_host else images.contiguous()
+        q_off = np.zeros(len(kp_list) + 1, np.int32)
+        q_off[1:] = np.cumsum([len(k) for k in kp_list])
+        D = des_template.shape[1]
+        kp_flat = np.concatenate(kp_list).astype(np.float64) if q_off[-1] else np.zeros((0, 2))
+        des_flat = np.concatenate(des_list).astype(np.uint8) if q_off[-1] else np.zeros((0, D), np.uint8)
+        inp = _pl.SlabInputs(
+            frames=frames,
+            des_tpl=torch.from_numpy(np.ascontiguousarray(des_template, np.uint8)).to(dev),
+            kp_tpl=torch.from_numpy(np.ascontiguousarray(kp_template, np.float64)).to(dev),
+            des_q=torch.from_numpy(np.ascontiguousarray(des_flat)).to(dev),
+            kp_q=torch.from_numpy(np.ascontiguousarray(kp_flat).reshape(-1, 2)).to(dev),
+            q_off=torch.from_numpy(q_off).to(dev),
+            q_off_host=q_off,
+        )
+        cfg = self._config(n_kp_global, rate)
+        self.logger.info("generating keypoint consensus...")
+        t_start = time.time()
+        res = _pl.align_slab(inp, cfg, logger=self.logger)
+        self.interpolated_idxs = res.interpolated
+        self.logger.info(f"aligned frames in: {round(time.time() - t_start)} s")
+        aligned = res.aligned
+        if patch is not None:
+            x_start, y_start, width, height = patch
+            x_end = x_start + width
+            y_end = y_start + height
+            aligned = aligned[:, x_start:x_end, y_start:y_end]
+        if to_host:
+            aligned = aligned.cpu().numpy()
+        return aligned, res.euclidean, res.skipped
+
+    # ------------------------------------------------ per-frame helpers (VA:160-458)
+    @classmethod
+    def _get_frame_keypoints(cls, i: int, image: np.ndarray, kp_template: np.ndarray, des_template: np.ndarray,
+                             detector_algorithm: str) -> Tuple[Set[int], np.ndarray, str]:
+        """VA:160-222 for one frame (detection on the host, matching on the GPU)."""
+        detector = cls.DETECTOR_CONSTRUCTOR_DICT[detector_algorithm]()
+        kq, dq = detector.detectAndCompute(image, None)
+        kp_query = np.array([p.pt for p in kq], dtype=np.float64).reshape(-1, 2)
+        return cls._match_frame(i, kp_query, np.asarray(dq, np.uint8), kp_template, des_template)
+
+    @classmethod
+    def _match_frame(cls, i, kp_query, des_query, kp_template, des_template):
+        dev = cls._device()
+        q_off = np.array([0, len(kp_query)], np.int32)
+        m = stages.match_frames(
+            torch.from_numpy(np.ascontiguousarray(des_template, np.uint8)).to(dev),
+            torch.from_numpy(np.ascontiguousarray(kp_template, np.float64)).to(dev),
+            torch.from_numpy(np.ascontiguousarray(des_query, np.uint8)).to(dev),
+            torch.from_numpy(np.ascontiguousarray(kp_query, np.float64)).to(dev),
+            torch.from_numpy(q_off).to(dev), q_off, ratio=cls.DESCRIPTOR_DISTANCE_RATIO_THRESH)
+        n_tpl = len(kp_template)
+        bits = m.keep_bits.cpu().numpy().view(np.uint32)[0]
+        kept = [k for k in range(n_tpl) if (bits[k >> 5] >> (k & 31)) & 1]
+        c = m.counts.cpu().numpy()[0]
+        log_str = (
+            f"frame {i}:\n"
+            f"\t{int(c[0])} unfiltered features identified\n"
+            f"\t{int(c[1])} matches identified between frame and template\n"
+            f"\t{int(c[2])} matches after feature-space ratio filter\n"
+            f"\t{int(c[3])} matches after distance-based outlier rejection"
+        )
+        return set(kept), m.kp_ordered.cpu().numpy()[0], log_str
+
+    def _get_consensus_kps(self, kp_idxs_list: List[set], n_frames: int, n_kp_global: int) -> Set[int]:
+        """VA:224-249: the n_kp_global most frequently matched template keypoints."""
+        counts = Counter([x for s in kp_idxs_list for x in s])
+        votes = [x for x in counts.most_common(n_kp_global)]
+        if len(votes) < self.N_KP_GLOBAL_MIN:
+            raise VideoAligner.AlignmentError(
+                "Too few keypoints found. Try a higher quality video, or decrease `VideoAligner.N_KP_GLOBAL_MIN`")
+        consensus_idxs, vote_match_rates = zip(*votes)
+        vote_match_rates = np.array(vote_match_rates) / n_frames
+        self.logger.info(f"top n keypoints match rates: {vote_match_rates}")
+        return set(consensus_idxs)
+
+    def _lookup_consensus_kps(self, consensus_idxs: Set[int], kp_idxs_list: List[Set[int]],
+                              kp_query_list: List[np.ndarray]) -> Tuple[np.ndarray, np.ndarray]:
+        """VA:251-286 (object arrays for ragged frames, as numpy < 1.24 produced)."""
+        tk, qk = [], []
+        for i in range(len(kp_query_list)):
+            idx = list(consensus_idxs.intersection(kp_idxs_list[i]))
+            tk.append(self._kp_template[idx])
+            qk.append(np.asarray(kp_query_list[i])[idx])
+            if len(qk[-1]) < self.N_KP_FRAME_SKIP:
+                self.logger.info(
+                    f"transform for frame {i} not estimated due to low keypoint count: "
+                    f"({len(qk[-1])}). Will be interpolated based on other frames instead")
+
+        def arr(lst):
+            try:
+                return np.array(lst)
+            except ValueError:
+                out = np.empty(len(lst), dtype=object)
+                for k, v in enumerate(lst):
+                    out[k] = v
+                return out
+
+        return arr(tk), arr(qk)
+
+    @classmethod
+    def _compute_euclidean_affine(cls, kp_template: np.ndarray, kp_query: np.ndarray,
+                                  spatial_downsample_rate: Union[float, int]) -> Optional[np.ndarray]:
+        """VA:288-323 for one frame: seeded rigid RANSAC on the GPU (NaN on failure)."""
+        kp_query = np.asarray(kp_query, dtype=np.float64).reshape(-1, 2)
+        kp_template = np.asarray(kp_template, dtype=np.float64).reshape(-1, 2)
+        if len(kp_query) < cls.N_KP_FRAME_SKIP:
+            return np.full((2, 3), np.nan)
+        dev = cls._device()
+        off = np.array([0, len(kp_query)], np.int32)
+        r = stages.ransac_rigid(
+            torch.from_numpy(np.ascontiguousarray(kp_query)).to(dev),
+            torch.from_numpy(np.ascontiguousarray(kp_template)).to(dev),
+            torch.from_numpy(off).to(dev), off, trials=cls.RANSAC_MAX_TRIALS,
+            residual_threshold=float(cls.RANSAC_RESIDUAL_THRESH), spatial_rate=spatial_downsample_rate,
+            n_skip=cls.N_KP_FRAME_SKIP, seed=cls.RANDOM_SEED, min_samples=cls.RANSAC_MIN_SAMPLES)
+        return r.params.cpu().numpy()[0]
+
+    _process_affines = staticmethod(_aff.process_affines)
+    _interpolate_affines = staticmethod(_aff.interpolate_affines)
+    _get_euclidean_transforms = staticmethod(_aff.euclidean_transforms)
+
+    @staticmethod
+    def _interpolate_affines_frame_range(base_affines: np.ndarray, failed_idx_range: range) -> List[np.ndarray]:
+        """VA:409-437."""
+        xs = np.arange(failed_idx_range[0], failed_idx_range[-1] + 1)
+        out = _aff._lerp_gap(base_affines[0], base_affines[1], failed_idx_range[0] - 1, failed_idx_range[-1] + 1, xs)
+        return [a for a in out]
+
+    @classmethod
+    def _apply_affine(cls, image: np.ndarray, affine: np.ndarray) -> np.ndarray:
+        """VA:455-458: cv2.warpAffine(image, affine, (W, H), INTER_LINEAR) on the GPU."""
+        dev = cls._device()
+        img = torch.from_numpy(np.ascontiguousarray(image, np.uint16)[None]).to(dev)
+        a = torch.from_numpy(np.ascontiguousarray(affine, np.float64).reshape(1, 2, 3)).to(dev)
+        return stages.warp_affine_u16(img, a).cpu().numpy()[0]
+
+    def _parallelize(self, func: Callable, *sequences: Sequence, **kwargs) -> List:
+        """VA:460-465 kept for API compatibility (ordered map; the hot path is batched)."""
+        return [func(*[x[i] for x in sequences], **kwargs) for i in range(len(sequences[0]))]
+
+    def _parallelize_i(self, func: Callable, *sequences: Sequence, **kwargs) -> List:
+        r = range(len(sequences[0]))
+        return self._parallelize(func, r, *sequences, **kwargs)
+
+    @staticmethod
+    def _convert_to_array(*args: Sequence):
+        return tuple(np.array(arg) for arg in args)
+
+    @classmethod
+    def _get_brightest_px(cls, images: np.ndarray) -> Union[float, int]:
+        """VA:479-482 (host numpy; a GPU histogram version is a listed next step)."""
+        return np.percentile(images, cls.IMAGE_NORM_MAX_PERCENTILE)
+
+    @classmethod
+    def _max_scale_images(cls, images: np.ndarray, template: np.ndarray, brightest_px: float,
+                          output_dtype: type) -> Tuple[np.ndarray, np.ndarray]:
+        """VA:484-492."""
+        max_px = cls.MAX_PIXEL_UINT8
+        images = np.clip(images / brightest_px * max_px, a_min=0, a_max=max_px).astype(output_dtype)
+        template = np.clip(template / brightest_px * max_px, a_min=0, a_max=max_px).astype(output_dtype)
+        return images, template
+
+    @staticmethod
+    def _downsample(images: np.ndarray, template: np.ndarray, frame_downsample_rate: int,
+                    spatial_downsample_rate: Union[float, int]) -> Tuple[np.ndarray, np.ndarray]:
+        """VA:494-506 (OpenCV pyrDown when frame_downsample_rate != 1)."""
+        images_sample = images[::frame_downsample_rate]
+        dst_size = tuple(np.array(images_sample[0].shape) // spatial_downsample_rate)
+        if frame_downsample_rate != 1:
+            try:
+                import cv2  # type: ignore
+            except ImportError as e:
+                raise RuntimeError("frame_rate >= 2*FRAME_SAMPLE_RATE needs cv2.pyrDown (OpenCV absent)") from e
+            images_sample = [cv2.pyrDown(frame, dstsize=dst_size) for frame in images_sample]
+            template = cv2.pyrDown(template, dstsize=dst_size)
+            images_sample = np.stack(images_sample).astype(np.uint8)
+            template = template.astype(np.uint8)
+        return images_sample, template
+
+
+class LoResVideoAligner(VideoAligner):
+    SPATIAL_DOWNSAMPLE_RATE = 2

@@ -1,0 +1,54 @@
+"""The C-ABI library loads on the CPU and exports exactly what include/kcmc.h declares."""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+from kcmc_amd import _lib
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "kcmc.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"\b(kcmc_\w+)\s*\(", src))
+
+
+def test_header_declarations_match_binding_table():
+    assert _declared() == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.load()
+    for name in _declared():
+        assert hasattr(L, name), name
+    # dynamic symbol table of the shared object itself
+    out = os.popen(f"nm -D --defined-only {_lib.lib_path()}").read()
+    for name in _declared():
+        assert re.search(rf"\bT {name}\b", out), name
+
+
+def test_abi_version_and_error_reporting():
+    L = _lib.load()
+    assert L.kcmc_abi_version() == _lib.ABI_VERSION
+    out = np.zeros(4, np.int32)
+    rc = L.kcmc_hypothesis_table(0, 2, 42, 2, out.ctypes.data_as(ctypes.c_void_p))
+    assert rc == _lib.KCMC_EINVAL
+    assert b"min_samples" in L.kcmc_last_error()
+    h = ctypes.c_void_p()
+    assert L.kcmc_create(-1, ctypes.byref(h)) != _lib.KCMC_OK  # no GPU here, or a bad ordinal there
+    assert L.kcmc_last_error()
+
+
+def test_launch_entry_points_validate_before_touching_the_gpu():
+    L = _lib.load()
+    P = ctypes.c_void_p
+    assert L.kcmc_knn2_l2u8(None, None, 1, 32, None, None, 1, 2, None, None, None) == _lib.KCMC_EINVAL
+    assert L.kcmc_warp_affine_u16(None, None, None, None, 1, 4, 4, 1, 0, None) == _lib.KCMC_EINVAL
+    assert L.kcmc_ransac_rigid(None, None, None, None, None, 0, 1, 10, 1000, 2.0, 1.0, 3, None, None, None, None,
+                               None) == _lib.KCMC_EINVAL
+    assert L.kcmc_ransac_prepare(None, None, 1, 1000, 42) == _lib.KCMC_EINVAL
+    assert L.kcmc_consensus(None, -1, 0, 0, 0, None, None, None, None, None) == _lib.KCMC_EINVAL
+    del P

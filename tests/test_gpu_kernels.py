@@ -1,0 +1,247 @@
+"""Parity of the HIP kernels (called through the C ABI) with the CPU oracle and the
+reference goldens.  Integer/index results must be bit-exact; RANSAC parameters
+within 1e-4 relative (north_star; we observe ~1e-12); warped pixels bit-exact to the
+oracle (north_star tolerance: 1 LSB)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import load_golden
+from kcmc_amd import stages, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _csr(lists):
+    off = np.zeros(len(lists) + 1, np.int32)
+    off[1:] = np.cumsum([len(x) for x in lists])
+    return off
+
+
+# ------------------------------------------------------------------------ K1
+@pytest.mark.parametrize("D", [1, 7, 31, 32, 33, 61, 64])
+def test_knn2_matches_oracle(dev, D):
+    rng = np.random.default_rng(D)
+    n_tpl = 300
+    tpl = rng.integers(0, 256, (n_tpl, D), dtype=np.uint8)
+    frames = []
+    for f in range(5):
+        n_q = int(rng.integers(2, 700))
+        q = rng.integers(0, 256, (n_q, D), dtype=np.uint8)
+        q[: n_q // 3] = tpl[rng.integers(0, n_tpl, n_q // 3)]  # exact matches -> ties
+        if n_q > 10:
+            q[7] = q[3]
+            q[9] = q[3]
+        frames.append(q)
+    off = _csr(frames)
+    idx, dist = stages.knn2_l2u8(_t(tpl, dev), _t(np.concatenate(frames), dev), _t(off, dev), int(np.diff(off).max()))
+    idx, dist = idx.cpu().numpy(), dist.cpu().numpy()
+    for f, q in enumerate(frames):
+        ri, rd = oracle.knn2_l2u8(tpl, q)
+        assert np.array_equal(idx[f], ri), f
+        assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), f
+
+
+def test_knn2_wide_keys_and_edge_counts(dev):
+    # n_q > 1024 with D = 64 does not fit 32-bit packed keys -> 64-bit key path
+    rng = np.random.default_rng(11)
+    D, n_tpl = 64, 97
+    tpl = rng.integers(0, 256, (n_tpl, D), dtype=np.uint8)
+    frames = [rng.integers(0, 256, (n, D), dtype=np.uint8) for n in (1500, 2, 1, 0, 33)]
+    frames[0][1400] = tpl[5]
+    off = _csr(frames)
+    idx, dist = stages.knn2_l2u8(_t(tpl, dev), _t(np.concatenate(frames), dev), _t(off, dev), 1500)
+    idx, dist = idx.cpu().numpy(), dist.cpu().numpy()
+    for f, q in enumerate(frames):
+        ri, rd = oracle.knn2_l2u8(tpl, q)
+        assert np.array_equal(idx[f], ri), f
+        assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), f
+
+
+def test_knn2_template_larger_than_a_workgroup(dev):
+    rng = np.random.default_rng(12)
+    tpl = rng.integers(0, 256, (1100, 32), dtype=np.uint8)
+    q = rng.integers(0, 256, (600, 32), dtype=np.uint8)
+    off = np.array([0, 600], np.int32)
+    idx, dist = stages.knn2_l2u8(_t(tpl, dev), _t(q, dev), _t(off, dev), 600)
+    ri, rd = oracle.knn2_l2u8(tpl, q)
+    assert np.array_equal(idx.cpu().numpy()[0], ri)
+    assert np.array_equal(dist.cpu().numpy()[0], rd)
+
+
+def _match_all(g, dev):
+    qo = g["q_offsets"].astype(np.int32)
+    return stages.match_frames(_t(g["des_template"], dev), _t(g["kp_template"], dev), _t(g["des_query"], dev),
+                               _t(g["kp_query"], dev), _t(qo, dev), qo)
+
+
+@pytest.mark.parametrize("name", ["match_golden_akaze.npz", "match_golden_orb.npz"])
+def test_match_frames_vs_reference_golden(dev, name):
+    g = load_golden(name)
+    m = _match_all(g, dev)
+    bits = m.keep_bits.cpu().numpy().view(np.uint32)
+    kq = m.kp_ordered.cpu().numpy()
+    counts = m.counts.cpu().numpy()
+    so = g["kp_idxs_offsets"]
+    n_tpl = g["kp_template"].shape[0]
+    for f in range(len(so) - 1):
+        kept = [i for i in range(n_tpl) if (bits[f, i >> 5] >> (i & 31)) & 1]
+        assert kept == g["kp_idxs"][so[f]:so[f + 1]].tolist(), f
+        assert list(set(kept)) == g["kp_idxs_setorder"][so[f]:so[f + 1]].tolist()
+        assert np.array_equal(kq[f], g["kp_query_ordered"][f]), f
+        assert counts[f].tolist() == g["log_counts"][f].tolist(), f
+
+
+def test_match_frames_vs_oracle_at_config2_size(dev):
+    """1080p ORB-like: n_tpl 500, D 32, ~550 keypoints per frame."""
+    ks = synthetic.make_keypoints(24, 500, 32, (1080, 1920), seed=5)
+    m = stages.match_frames(_t(ks.des_tpl, dev), _t(ks.kp_tpl, dev), _t(ks.des_q, dev), _t(ks.kp_q, dev),
+                            _t(ks.q_off, dev), ks.q_off)
+    bits = m.keep_bits.cpu().numpy().view(np.uint32)
+    kqo = m.kp_ordered.cpu().numpy()
+    for f in range(24):
+        a, b = ks.q_off[f], ks.q_off[f + 1]
+        idx, dist = oracle.knn2_l2u8(ks.des_tpl, ks.des_q[a:b])
+        s, kq, cnt = oracle.filter_matches(idx, dist, ks.kp_tpl, ks.kp_q[a:b])
+        kept = [i for i in range(500) if (bits[f, i >> 5] >> (i & 31)) & 1]
+        assert kept == sorted(s)
+        assert np.array_equal(kqo[f], kq)
+        assert len(kept) > 200  # the synthetic data matches well
+
+
+def test_match_frames_rejects_frames_with_fewer_than_two_keypoints(dev):
+    tpl = np.zeros((4, 8), np.uint8)
+    off = np.array([0, 3, 4], np.int32)
+    with pytest.raises(ValueError):
+        stages.match_frames(_t(tpl, dev), _t(np.zeros((4, 2)), dev), _t(np.zeros((4, 8), np.uint8), dev),
+                            _t(np.zeros((4, 2)), dev), _t(off, dev), off)
+
+
+# ------------------------------------------------------------------------ K2
+def _ransac(dev, tpls, qs, rate=1.0, trials=1000):
+    off = _csr(qs)
+    r = stages.ransac_rigid(_t(np.concatenate(qs).reshape(-1, 2), dev), _t(np.concatenate(tpls).reshape(-1, 2), dev),
+                            _t(off, dev), off, trials=trials, spatial_rate=rate)
+    return off, r.params.cpu().numpy(), r.inliers.cpu().numpy().astype(bool), r.n_inliers.cpu().numpy(), \
+        r.best_trial.cpu().numpy()
+
+
+def test_ransac_vs_reference_golden(dev):
+    g = load_golden("ransac_golden.npz")
+    off = g["offsets"]
+    F = len(off) - 1
+    tpls = [g["kp_template"][off[f]:off[f + 1]] for f in range(F)]
+    qs = [g["kp_query"][off[f]:off[f + 1]] for f in range(F)]
+    for rate in (1, 2):
+        sel = [f for f in range(F) if g["spatial_rate"][f] == rate]
+        _, params, inl, nin, _ = _ransac(dev, [tpls[f] for f in sel], [qs[f] for f in sel], rate=rate)
+        o2 = _csr([qs[f] for f in sel])
+        for k, f in enumerate(sel):
+            ref = g["affine"][f]
+            if np.isnan(ref).any():
+                assert np.isnan(params[k]).all(), f
+                continue
+            np.testing.assert_allclose(params[k], ref, rtol=1e-4, atol=1e-6)
+            np.testing.assert_allclose(params[k], ref, rtol=1e-9, atol=1e-9)
+            assert np.array_equal(inl[o2[k]:o2[k + 1]], g["inliers"][off[f]:off[f + 1]]), f
+            assert nin[k] == g["n_inliers"][f]
+
+
+def test_ransac_bit_exact_selection_vs_oracle(dev):
+    """Same hypotheses, same residual arithmetic -> identical inliers and winning trial,
+    including N > 128 (numpy's recursive pairwise order)."""
+    rng = np.random.default_rng(21)
+    tpls, qs = [], []
+    for N in [3, 4, 5, 8, 9, 50, 100, 127, 128, 129, 136, 200, 255, 256, 257, 300, 500, 777, 1024, 2000]:
+        tpl = rng.uniform(0, 1000, (N, 2))
+        A = synthetic.rigid(rng.normal(0, 0.02), rng.normal(0, 5), rng.normal(0, 5))
+        q = (tpl - A[:, 2]) @ A[:, :2] + rng.normal(0, rng.uniform(0.1, 1.5), (N, 2))
+        out = rng.random(N) < rng.uniform(0, 0.6)
+        q[out] = rng.uniform(0, 1000, (int(out.sum()), 2))
+        tpls.append(tpl.astype(np.float32).astype(np.float64))
+        qs.append(q.astype(np.float32).astype(np.float64))
+    off, params, inl, nin, best = _ransac(dev, tpls, qs)
+    for f in range(len(qs)):
+        p, i_ref, bt, ni = oracle.ransac_rigid(qs[f], tpls[f])
+        assert best[f] == bt, f
+        assert nin[f] == ni, f
+        assert np.array_equal(inl[off[f]:off[f + 1]], i_ref), f
+        np.testing.assert_allclose(params[f], p, rtol=1e-10, atol=1e-10)
+
+
+def test_ransac_degenerate_and_skipped_frames(dev):
+    rng = np.random.default_rng(22)
+    tpl = rng.uniform(0, 100, (10, 2))
+    same = np.repeat(tpl[:1], 10, 0)  # all frame points identical -> every hypothesis degenerate
+    off, params, inl, nin, best = _ransac(dev, [tpl, tpl[:2], tpl[:0], tpl], [same, tpl[:2] + 1, tpl[:0], tpl + 3])
+    assert np.isnan(params[0]).all() and nin[0] == 0 and best[0] == -1
+    assert np.isnan(params[1]).all() and np.isnan(params[2]).all()  # N < N_KP_FRAME_SKIP
+    np.testing.assert_allclose(params[3], [[1, 0, -3], [0, 1, -3]], atol=1e-9)
+
+
+def test_ransac_exact_data_early_exit(dev):
+    # integer points + integer translation: every residual is exactly 0 -> S == 0 at trial 0
+    tpl = np.array([[x, y] for x in range(0, 50, 7) for y in range(0, 40, 9)], np.float64)
+    q = tpl - np.array([4.0, -2.0])
+    off, params, inl, nin, best = _ransac(dev, [tpl], [q])
+    _, _, bt, ni = oracle.ransac_rigid(q, tpl)
+    assert best[0] == bt == 0 and nin[0] == ni == len(tpl)
+    np.testing.assert_allclose(params[0], [[1, 0, 4], [0, 1, -2]], atol=1e-12)
+
+
+def test_ransac_gather_mode_matches_contiguous(dev):
+    rng = np.random.default_rng(23)
+    n_tpl, F = 60, 7
+    kp_tpl = rng.uniform(0, 500, (n_tpl, 2))
+    kp_ord = kp_tpl[None] + rng.normal(0, 0.5, (F, n_tpl, 2)) + 2.0
+    lists = [rng.permutation(n_tpl)[: int(rng.integers(0, 40))].astype(np.int32) for _ in range(F)]
+    off = _csr(lists)
+    r = stages.ransac_rigid(_t(kp_ord.reshape(-1, 2), dev), _t(kp_tpl, dev), _t(off, dev), off,
+                            pt_idx=_t(np.concatenate(lists), dev), src_frame_stride=n_tpl)
+    _, p2, _, _, _ = _ransac(dev, [kp_tpl[L] for L in lists], [kp_ord[f][L] for f, L in enumerate(lists)])
+    np.testing.assert_array_equal(r.params.cpu().numpy(), p2)
+
+
+# ------------------------------------------------------------------------ K3
+@pytest.mark.parametrize("shape", [(1, 5, 7), (3, 64, 128), (2, 67, 131), (2, 130, 257), (1, 1080, 1920)])
+def test_warp_matches_oracle(dev, shape):
+    F, H, W = shape
+    rng = np.random.default_rng(H * W)
+    imgs = rng.integers(0, 65536, shape).astype(np.uint16)
+    Ms = []
+    for f in range(F):
+        A = synthetic.rigid(rng.normal(0, 0.03), rng.normal(0, 6), rng.normal(0, 6))
+        if f % 3 == 1:
+            A[:, :2] *= 1.05
+        Ms.append(A)
+    Ms = np.stack(Ms)
+    out = stages.warp_affine_u16(_t(imgs, dev), _t(Ms, dev)).cpu().numpy()
+    for f in range(F):
+        assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], Ms[f])), f
+
+
+def test_warp_identity_inverse_map_and_extreme_maps(dev):
+    rng = np.random.default_rng(31)
+    imgs = rng.integers(0, 65536, (4, 33, 45)).astype(np.uint16)
+    Ms = np.stack([np.array([[1.0, 0, 0], [0, 1, 0]]), np.array([[0.0, -1, 40], [1, 0, -3]]),
+                   np.array([[3.0, 0.2, -50], [0.1, 0.2, 7]]), np.array([[1.0, 0, 1000], [0, 1, -1000]])])
+    for inv in (False, True):
+        out = stages.warp_affine_u16(_t(imgs, dev), _t(Ms, dev), inverse_map=inv).cpu().numpy()
+        for f in range(4):
+            assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], Ms[f], inverse_map=inv)), (f, inv)
+    assert np.array_equal(out[0], imgs[0])
+
+
+@pytest.mark.parametrize("C", [3, 4])
+def test_warp_multichannel(dev, C):
+    rng = np.random.default_rng(C)
+    imgs = rng.integers(0, 65536, (2, 50, 70, C)).astype(np.uint16)
+    Ms = np.stack([synthetic.rigid(0.02, 1.5, -2.25), synthetic.rigid(-0.01, -3.3, 0.7)])
+    out = stages.warp_affine_u16(_t(imgs, dev), _t(Ms, dev)).cpu().numpy()
+    for f in range(2):
+        assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], Ms[f]))

@@ -1,0 +1,128 @@
+"""End-to-end parity of the batched hot path and of the reference-shaped API."""
+import logging
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import load_golden
+from kcmc_amd import VideoAligner, pipeline, stages, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _split(flat, off):
+    return [flat[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+
+
+class _KP:
+    def __init__(self, x, y):
+        self.pt = (float(x), float(y))
+
+
+class _RegistryDetector:
+    """Test stand-in for cv2.AKAZE: returns the golden keypoints registered for an image."""
+
+    registry = {}
+
+    def detectAndCompute(self, image, mask):
+        kp, des = self.registry[np.ascontiguousarray(image).tobytes()]
+        return [_KP(x, y) for x, y in kp], des
+
+
+def test_align_keypoints_vs_reference_pipeline_golden():
+    g = load_golden("pipeline_golden.npz")
+    qo = g["q_offsets"]
+    va = VideoAligner()
+    aligned, eu, skipped = va.align_keypoints(g["images"], g["kp_template"], g["des_template"],
+                                              _split(g["kp_query"], qo), _split(g["des_query"], qo),
+                                              int(g["n_kp_global"]), frame_rate=30)
+    assert skipped == g["skipped"].tolist()
+    assert va.interpolated_idxs == g["interpolated"].tolist()
+    np.testing.assert_allclose(eu, g["euclidean"], rtol=1e-4, atol=1e-6)
+    assert np.array_equal(aligned, g["aligned"])
+
+
+def test_align_images_with_registered_detector_vs_golden(monkeypatch):
+    g = load_golden("pipeline_golden.npz")
+    imgs = g["images"]
+    F = len(imgs)
+    b = VideoAligner._get_brightest_px(imgs)
+    t_idx = int(F * VideoAligner.TEMPLATE_FRAME_LOC)
+    i8, t8 = VideoAligner._max_scale_images(imgs, imgs[t_idx], b, np.uint8)
+    qo = g["q_offsets"]
+    kq, dq = _split(g["kp_query"], qo), _split(g["des_query"], qo)
+    reg = {t8.tobytes(): (g["kp_template"], g["des_template"])}
+    for f in range(F):
+        reg[np.ascontiguousarray(i8[f]).tobytes()] = (kq[f], dq[f])
+    _RegistryDetector.registry = reg
+    monkeypatch.setitem(VideoAligner.DETECTOR_CONSTRUCTOR_DICT, "akaze", _RegistryDetector)
+    aligned, eu, skipped = VideoAligner().align_images(imgs, n_kp_global=int(g["n_kp_global"]),
+                                                       detector_algorithm="akaze", frame_rate=30)
+    assert skipped == g["skipped"].tolist()
+    np.testing.assert_allclose(eu, g["euclidean"], rtol=1e-4, atol=1e-6)
+    assert np.array_equal(aligned, g["aligned"])
+    # patch crop semantics (VA:153-157): axis 1 by x, axis 2 by y
+    a2, _, _ = VideoAligner().align_images(imgs, int(g["n_kp_global"]), "akaze", 30, patch=(3, 5, 10, 20))
+    assert np.array_equal(a2, g["aligned"][:, 3:13, 5:25])
+
+
+def test_per_frame_helpers_match_reference_golden(monkeypatch):
+    g = load_golden("ransac_golden.npz")
+    off = g["offsets"]
+    for f in range(0, len(off) - 1, 5):
+        tpl, q = g["kp_template"][off[f]:off[f + 1]], g["kp_query"][off[f]:off[f + 1]]
+        a = VideoAligner._compute_euclidean_affine(tpl, q, int(g["spatial_rate"][f]))
+        ref = g["affine"][f]
+        if np.isnan(ref).any():
+            assert np.isnan(a).all()
+        else:
+            np.testing.assert_allclose(a, ref, rtol=1e-4, atol=1e-6)
+    m = load_golden("match_golden_akaze.npz")
+    qo, so = m["q_offsets"], m["kp_idxs_offsets"]
+    reg = {}
+    for f in range(4):
+        img = np.full((4, 4), f, np.uint8)
+        reg[img.tobytes()] = (m["kp_query"][qo[f]:qo[f + 1]], m["des_query"][qo[f]:qo[f + 1]])
+    _RegistryDetector.registry = reg
+    monkeypatch.setitem(VideoAligner.DETECTOR_CONSTRUCTOR_DICT, "akaze", _RegistryDetector)
+    for f in range(4):
+        s, kq, log = VideoAligner._get_frame_keypoints(f, np.full((4, 4), f, np.uint8), m["kp_template"],
+                                                       m["des_template"], "akaze")
+        assert list(s) == m["kp_idxs_setorder"][so[f]:so[f + 1]].tolist()
+        assert np.array_equal(kq, m["kp_query_ordered"][f])
+        assert [int(l.split()[0]) for l in log.split("\n")[1:]] == m["log_counts"][f].tolist()
+    img = np.random.default_rng(0).integers(0, 65536, (40, 50)).astype(np.uint16)
+    M = synthetic.rigid(0.05, 2.5, -1.25)
+    assert np.array_equal(VideoAligner._apply_affine(img, M), oracle.warp_affine_u16(img, M))
+
+
+def test_config2_slab_end_to_end(dev):
+    """A 1080p slab shaped like BASELINE config 2 (ORB-like D=32, n_tpl=500, rigid):
+    the recovered frame->template maps match the ground truth and every stage agrees
+    with the oracle on sampled frames."""
+    F, H, W = 48, 1080, 1920
+    ks = synthetic.make_keypoints(F, 500, 32, (H, W), seed=7)
+    base = synthetic.make_texture((H, W), seed=0)
+    frames = torch.from_numpy(np.broadcast_to(base, (F, H, W)).copy()).to(dev)
+    inp = pipeline.SlabInputs(frames, torch.from_numpy(ks.des_tpl).to(dev), torch.from_numpy(ks.kp_tpl).to(dev),
+                              torch.from_numpy(ks.des_q).to(dev), torch.from_numpy(ks.kp_q).to(dev),
+                              torch.from_numpy(ks.q_off).to(dev), ks.q_off)
+    cfg = pipeline.AlignConfig(n_kp_global=100)
+    res = pipeline.align_slab(inp, cfg, logger=logging.getLogger("test"), keep_intermediates=True)
+    assert res.skipped == [] and res.interpolated == []
+    np.testing.assert_allclose(res.affines[:, :, :2], ks.gt[:, :, :2], atol=2e-3)
+    np.testing.assert_allclose(res.affines[:, :, 2], ks.gt[:, :, 2], atol=0.5)
+    # RANSAC parity on the device-gathered point lists
+    kq = res.match.kp_ordered.cpu().numpy()
+    inl = res.ransac.inliers.cpu().numpy().astype(bool)
+    po, pi = res.consensus.pt_off, res.consensus.pt_idx
+    for f in range(0, F, 7):
+        L = pi[po[f]:po[f + 1]]
+        p, i_ref, _, _ = oracle.ransac_rigid(kq[f][L], ks.kp_tpl[L])
+        assert np.array_equal(inl[po[f]:po[f + 1]], i_ref)
+        np.testing.assert_allclose(res.affines[f], p, rtol=1e-4, atol=1e-6)
+    out = res.aligned.cpu().numpy()
+    for f in (0, F - 1):
+        assert np.array_equal(out[f], oracle.warp_affine_u16(base, res.affines[f]))

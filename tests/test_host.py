@@ -1,0 +1,177 @@
+"""Host-side parts of the product that run without a GPU: the native hypothesis-table
+generator, the native CPython-set consensus, the affine post-processing and the
+VideoAligner host helpers -- each against the oracle and the reference goldens."""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import load_golden
+from kcmc_amd import VideoAligner, affines, stages
+
+
+# ------------------------------------------------------------ hypothesis tables
+@pytest.mark.parametrize("n", list(range(3, 40)) + [64, 100, 127, 128, 129, 255, 500, 1000, 4096])
+def test_native_hypothesis_table_matches_numpy(n):
+    assert np.array_equal(stages.hypothesis_table(n, 1000, 42), oracle.hypothesis_table(n, 1000, 42))
+
+
+def test_native_hypothesis_table_other_seeds_and_sizes():
+    for seed in (0, 1, 2**32 - 1):
+        rs = np.random.RandomState(seed)
+        exp = np.array([rs.choice(50, 3, replace=False) for _ in range(20)])
+        assert np.array_equal(stages.hypothesis_table(50, 20, seed, 3), exp)
+
+
+# ------------------------------------------------------------ consensus
+def _bits(sets, n_tpl):
+    words = (n_tpl + 31) // 32
+    kb = np.zeros((len(sets), words), np.uint32)
+    for f, s in enumerate(sets):
+        for i in s:
+            kb[f, i >> 5] |= np.uint32(1 << (i & 31))
+    return kb
+
+
+def _check_consensus(sets, n_tpl, n_kp_global, n_min=5):
+    try:
+        cons_set, order, votes = oracle.consensus(sets, n_kp_global, n_min)
+    except RuntimeError:
+        with pytest.raises(VideoAligner.AlignmentError):
+            stages.consensus(_bits(sets, n_tpl), n_tpl, n_kp_global, n_min)
+        return
+    c = stages.consensus(_bits(sets, n_tpl), n_tpl, n_kp_global, n_min)
+    assert c.order.tolist() == list(order)
+    assert c.votes.tolist() == list(votes)
+    lists = oracle.lookup(cons_set, sets)
+    for f, L in enumerate(lists):
+        assert c.pt_idx[c.pt_off[f]:c.pt_off[f + 1]].tolist() == L
+
+
+def test_native_consensus_matches_cpython_random():
+    rng = np.random.default_rng(7)
+    for case in range(60):
+        n_tpl = int(rng.choice([8, 33, 100, 500, 1000, 4096, 9000]))
+        F = int(rng.integers(1, 50))
+        p = rng.uniform(0.0, 0.9, n_tpl) * rng.uniform(0.1, 1.0)
+        # sets built from ascending lists, exactly like VA:214
+        sets = [set(np.flatnonzero(rng.random(n_tpl) < p).tolist()) for _ in range(F)]
+        n_kp_global = int(rng.choice([1, 5, 10, 50, 100, 200, 500, 5000]))
+        _check_consensus(sets, n_tpl, n_kp_global)
+
+
+def test_native_consensus_many_ties():
+    # all counts equal -> most_common order is first-occurrence (set iteration) order
+    sets = [set(range(0, 300, 3)), set(range(0, 300, 3))]
+    _check_consensus(sets, 300, 17)
+    _check_consensus([set(range(1000))], 1000, 1000)
+    _check_consensus([set([999, 64, 65, 3, 1029 % 1000])], 1000, 5)
+
+
+def test_native_consensus_too_few_raises():
+    with pytest.raises(VideoAligner.AlignmentError):
+        stages.consensus(_bits([{1, 2}, {2, 3}], 10), 10, 10, 5)
+
+
+def test_native_consensus_vs_reference_golden():
+    g = load_golden("consensus_golden.npz")
+    for c in range(int(g["n_cases"])):
+        n_tpl = int(g[f"c{c}_n_tpl"])
+        fo, fl = g[f"c{c}_frames_off"], g[f"c{c}_frames"]
+        sets = [set(fl[fo[i]:fo[i + 1]].tolist()) for i in range(len(fo) - 1)]
+        res = stages.consensus(_bits(sets, n_tpl), n_tpl, int(g[f"c{c}_n_kp_global"]), 5)
+        assert sorted(res.order.tolist()) == sorted(g[f"c{c}_consensus_setorder"].tolist())
+        lo, ll = g[f"c{c}_lookup_off"], g[f"c{c}_lookup"]
+        assert np.array_equal(res.pt_off, lo)
+        assert np.array_equal(res.pt_idx, ll)
+
+
+# ------------------------------------------------------------ affine post-processing
+def test_affines_vs_reference_golden():
+    g = load_golden("affines_golden.npz")
+    names = sorted({k.rsplit("_r", 1)[0] for k in g.files if k.endswith("_in")})
+    for name in names:
+        for rate in (1, 3):
+            p = f"{name}_r{rate}"
+            exp, skipped = affines.process_affines(list(g[p + "_in"]), rate)
+            np.testing.assert_array_equal(exp, g[p + "_expanded"])
+            assert skipped == g[p + "_skipped"].tolist()
+            itp, idx = affines.interpolate_affines(exp)
+            # arccos/arcsin/cos/sin differ by ~1 ulp between numpy builds (the golden was
+            # made with numpy 1.26); everything else is exact
+            np.testing.assert_allclose(itp, g[p + "_interp"], rtol=1e-13, atol=1e-15)
+            assert idx == g[p + "_interp_idx"].tolist()
+            np.testing.assert_allclose(affines.euclidean_transforms(itp), g[p + "_euclid"], rtol=1e-13, atol=1e-15)
+    with pytest.raises(VideoAligner.AlignmentError):
+        affines.interpolate_affines(np.full((4, 2, 3), np.nan))
+
+
+def test_gap_lerp_matches_scipy_interp1d():
+    from scipy.interpolate import interp1d
+
+    rng = np.random.default_rng(9)
+    for _ in range(50):
+        lo = int(rng.integers(0, 20))
+        hi = lo + int(rng.integers(2, 9))
+        base = np.stack([np.array([[np.cos(t), -np.sin(t), rng.normal()], [np.sin(t), np.cos(t), rng.normal()]])
+                         for t in rng.normal(0, 0.05, 2)])
+        b = base.copy()
+        b[:, 0, 0] = np.arccos(b[:, 0, 0])
+        b[:, 0, 1] = np.arcsin(b[:, 0, 1])
+        b[:, 1, 0] = np.arcsin(b[:, 1, 0])
+        b[:, 1, 1] = np.arccos(b[:, 1, 1])
+        it = interp1d([lo, hi], b, axis=0)
+        xs = np.arange(lo + 1, hi)
+        got = affines._lerp_gap(base[0], base[1], lo, hi, xs)
+        for k, j in enumerate(xs):
+            a = it(j)
+            a[0, 0], a[0, 1], a[1, 0], a[1, 1] = np.cos(a[0, 0]), np.sin(a[0, 1]), np.sin(a[1, 0]), np.cos(a[1, 1])
+            np.testing.assert_array_equal(got[k], a)
+
+
+# ------------------------------------------------------------ VideoAligner host helpers
+def test_preprocessing_vs_reference_golden():
+    g = load_golden("preprocess_golden.npz")
+    for k in range(int(g["n_cases"])):
+        imgs = g[f"p{k}_images"]
+        b = VideoAligner._get_brightest_px(imgs)
+        assert b == g[f"p{k}_brightest"]
+        i8, t8 = VideoAligner._max_scale_images(imgs, imgs[len(imgs) // 2], b, np.uint8)
+        np.testing.assert_array_equal(i8, g[f"p{k}_u8"])
+        np.testing.assert_array_equal(t8, g[f"p{k}_tpl_u8"])
+
+
+def test_consensus_helpers_vs_reference_golden():
+    g = load_golden("consensus_golden.npz")
+    va = VideoAligner()
+    for c in range(int(g["n_cases"])):
+        n_tpl = int(g[f"c{c}_n_tpl"])
+        fo, fl = g[f"c{c}_frames_off"], g[f"c{c}_frames"]
+        sets = [set(fl[fo[i]:fo[i + 1]].tolist()) for i in range(len(fo) - 1)]
+        cons = va._get_consensus_kps(sets, len(sets), int(g[f"c{c}_n_kp_global"]))
+        assert list(cons) == g[f"c{c}_consensus_setorder"].tolist()
+        va._kp_template = np.arange(n_tpl, dtype=np.float64).reshape(-1, 1) * np.array([[1.0, -1.0]])
+        tk, _ = va._lookup_consensus_kps(cons, sets, [np.zeros((n_tpl, 2))] * len(sets))
+        lo, ll = g[f"c{c}_lookup_off"], g[f"c{c}_lookup"]
+        for i in range(len(sets)):
+            got = np.asarray(tk[i]).reshape(-1, 2)[:, 0].astype(np.int64).tolist()
+            assert got == ll[lo[i]:lo[i + 1]].tolist()
+    with pytest.raises(VideoAligner.AlignmentError):
+        va._get_consensus_kps([{1, 2}, {2, 3}], 2, 10)
+
+
+def test_api_surface_matches_reference():
+    import kcmc_amd
+
+    for name in ("FRAME_SAMPLE_RATE", "SPATIAL_DOWNSAMPLE_RATE", "N_JOBS_PARALLEL", "DETECTOR_CONSTRUCTOR_DICT",
+                 "N_KP_GLOBAL_MIN", "N_KP_FRAME_SKIP", "TEMPLATE_FRAME_LOC", "MAX_FRAC_INTERPOLATED",
+                 "DESCRIPTOR_DISTANCE_RATIO_THRESH", "MEDIAN_KEYPOINT_INLIER_DISTANCE_RANGE",
+                 "IMAGE_NORM_MAX_PERCENTILE", "MAX_PIXEL_UINT8", "RANSAC_MIN_SAMPLES", "RANSAC_RESIDUAL_THRESH",
+                 "RANSAC_MAX_TRIALS", "RANDOM_SEED", "align_images", "_get_frame_keypoints", "_get_consensus_kps",
+                 "_lookup_consensus_kps", "_compute_euclidean_affine", "_process_affines", "_interpolate_affines",
+                 "_interpolate_affines_frame_range", "_get_euclidean_transforms", "_apply_affine", "_parallelize",
+                 "_parallelize_i", "_convert_to_array", "_get_brightest_px", "_max_scale_images", "_downsample"):
+        assert hasattr(VideoAligner, name), name
+    assert set(VideoAligner.DETECTOR_CONSTRUCTOR_DICT) == {"akaze", "brisk"}
+    assert issubclass(VideoAligner.AlignmentError, BaseException)
+    assert kcmc_amd.LoResVideoAligner.SPATIAL_DOWNSAMPLE_RATE == 2
+    assert (VideoAligner.RANSAC_MAX_TRIALS, VideoAligner.RANDOM_SEED, VideoAligner.N_KP_FRAME_SKIP) == (1000, 42, 3)
