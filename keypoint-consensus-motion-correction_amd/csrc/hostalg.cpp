@@ -191,21 +191,6 @@ class PySet {
   size_t mask_, fill_, used_;
 };
 
-// set.intersection(other) for two sets (Objects/setobject.c set_intersection):
-// iterate the smaller one (`so` keeps the larger when len(other) > len(so)),
-// inserting hits into a fresh set; return that set's iteration order.
-void intersection_order(const PySet& so_in, const PySet& other_in, std::vector<int32_t>& out) {
-  const PySet* so = &so_in;
-  const PySet* other = &other_in;
-  if (other->size() > so->size()) std::swap(so, other);
-  PySet result;
-  other->for_each([&](int64_t k) {
-    if (so->contains(k)) result.add(k);
-  });
-  out.clear();
-  result.for_each([&](int64_t k) { out.push_back((int32_t)k); });
-}
-
 template <class F>
 void parallel_for(int n, F&& f) {
   unsigned hw = std::thread::hardware_concurrency();
@@ -239,25 +224,47 @@ extern "C" int kcmc_consensus(const uint32_t* keep_bits, int n_frames, int n_tpl
       !out_n_consensus || !out_pt_off)
     return fail(KCMC_EINVAL, "kcmc_consensus: bad arguments");
   const int words = (n_tpl + 31) / 32;
-  // kp_idxs = set([m.queryIdx for m in distance_matches]) -- ascending insertions (VA:214)
-  std::vector<PySet> frame_sets((size_t)n_frames);
-  parallel_for(n_frames, [&](int f) {
-    const uint32_t* w = keep_bits + (size_t)f * words;
-    for (int i = 0; i < n_tpl; ++i)
-      if ((w[i >> 5] >> (i & 31)) & 1u) frame_sets[(size_t)f].add(i);
-  });
-  // Counter([x for s in kp_idxs_list for x in s]) (VA:239): counts + first-occurrence rank.
+  auto frame_bits = [&](int f) { return keep_bits + (size_t)f * words; };
+  // kp_idxs = set([m.queryIdx for m in distance_matches]) (VA:214): insertions in
+  // ascending template order.  Only needed where its iteration order is observable.
+  auto frame_set = [&](int f) {
+    PySet s;
+    const uint32_t* w = frame_bits(f);
+    for (int k = 0; k < words; ++k)
+      for (uint32_t b = w[k]; b; b &= b - 1) s.add(32 * k + __builtin_ctz(b));
+    return s;
+  };
+  // Counter([x for s in kp_idxs_list for x in s]) (VA:239): vote counts, and the
+  // first-occurrence order (dict insertion order) -- a frame's set iteration order only
+  // matters for the elements it contributes first, so only those frames are replayed.
   std::vector<int32_t> count((size_t)n_tpl, 0);
-  std::vector<int32_t> first((size_t)n_tpl, -1);
+  std::vector<uint32_t> seen((size_t)words, 0u), any((size_t)words, 0u);
+  for (int f = 0; f < n_frames; ++f) {
+    const uint32_t* w = frame_bits(f);
+    for (int k = 0; k < words; ++k) {
+      any[(size_t)k] |= w[k];
+      for (uint32_t b = w[k]; b; b &= b - 1) ++count[(size_t)(32 * k + __builtin_ctz(b))];
+    }
+  }
+  size_t remaining = 0;
+  for (int k = 0; k < words; ++k) remaining += (size_t)__builtin_popcount(any[(size_t)k]);
   std::vector<int32_t> order;
-  for (int f = 0; f < n_frames; ++f)
-    frame_sets[(size_t)f].for_each([&](int64_t k) {
-      if (first[(size_t)k] < 0) {
-        first[(size_t)k] = (int32_t)order.size();
-        order.push_back((int32_t)k);
+  order.reserve(remaining);
+  for (int f = 0; f < n_frames && remaining; ++f) {
+    const uint32_t* w = frame_bits(f);
+    bool fresh = false;
+    for (int k = 0; k < words && !fresh; ++k) fresh = (w[k] & ~seen[(size_t)k]) != 0;
+    if (!fresh) continue;
+    frame_set(f).for_each([&](int64_t key) {
+      uint32_t& sw = seen[(size_t)(key >> 5)];
+      const uint32_t bit = 1u << (key & 31);
+      if (!(sw & bit)) {
+        sw |= bit;
+        order.push_back((int32_t)key);
+        --remaining;
       }
-      ++count[(size_t)k];
     });
+  }
   // most_common(n) == stable sort by count desc over first-occurrence order (heapq.nlargest).
   std::stable_sort(order.begin(), order.end(),
                    [&](int32_t a, int32_t b) { return count[(size_t)a] > count[(size_t)b]; });
@@ -271,12 +278,35 @@ extern "C" int kcmc_consensus(const uint32_t* keep_bits, int n_frames, int n_tpl
     return fail(KCMC_EALIGN,
                 "Too few keypoints found. Try a higher quality video, or decrease "
                 "`VideoAligner.N_KP_GLOBAL_MIN`");
-  // consensus_idxs = set(consensus_idxs) (VA:248), then per frame
-  // list(consensus_idxs.intersection(kp_idxs_list[i])) (VA:274).
+  // consensus_idxs = set(consensus_idxs) (VA:248)
   PySet cons;
   for (int k = 0; k < nc; ++k) cons.add(order[(size_t)k]);
+  std::vector<int32_t> cons_iter;
+  cons_iter.reserve((size_t)nc);
+  cons.for_each([&](int64_t key) { cons_iter.push_back((int32_t)key); });
+  std::vector<uint32_t> cons_bits((size_t)words, 0u);
+  for (int32_t key : cons_iter) cons_bits[(size_t)(key >> 5)] |= 1u << (key & 31);
+  // list(consensus_idxs.intersection(kp_idxs_list[i])) (VA:274): set_intersection
+  // iterates the smaller set (the frame's when len(frame) <= len(consensus)) and
+  // inserts the hits into a fresh set, whose iteration order is the result.
   std::vector<std::vector<int32_t>> lists((size_t)n_frames);
-  parallel_for(n_frames, [&](int f) { intersection_order(cons, frame_sets[(size_t)f], lists[(size_t)f]); });
+  parallel_for(n_frames, [&](int f) {
+    const uint32_t* w = frame_bits(f);
+    size_t len = 0;
+    for (int k = 0; k < words; ++k) len += (size_t)__builtin_popcount(w[k]);
+    PySet result;
+    if (len > (size_t)nc) {
+      for (int32_t key : cons_iter)
+        if ((w[key >> 5] >> (key & 31)) & 1u) result.add(key);
+    } else {
+      frame_set(f).for_each([&](int64_t key) {
+        if ((cons_bits[(size_t)(key >> 5)] >> (key & 31)) & 1u) result.add(key);
+      });
+    }
+    auto& L = lists[(size_t)f];
+    L.reserve(result.size());
+    result.for_each([&](int64_t key) { L.push_back((int32_t)key); });
+  });
   out_pt_off[0] = 0;
   for (int f = 0; f < n_frames; ++f) {
     const auto& L = lists[(size_t)f];

@@ -12,18 +12,26 @@
 // operation by operation.
 //
 // Layout: frames [F, H, W, C] u16 contiguous in HBM.  One workgroup covers a
-// 128-column x 64-row output strip of one frame: the per-column deltas and per-row
-// origins are computed once into LDS (the only double-precision work), then each
-// thread produces 4 consecutive output pixels per row with integer coordinate
-// arithmetic, gathers the taps through L1/L2 and writes one 8-byte store.
+// 128-column x 32-row output tile of one frame.  The per-column deltas and per-row
+// origins are computed once into LDS (the only double-precision work).  Because the
+// fixed-point source coordinate is separable (X = X0[y] + adelta[x]), the exact source
+// bounding box of the tile follows from four min/max reductions; the box is staged
+// into LDS with coalesced 16-byte loads (zero outside the image, which is exactly
+// BORDER_CONSTANT), and every output pixel gathers its four taps from LDS.  Each
+// thread writes pixel pairs as 4-byte stores (a wave writes 256 contiguous bytes).
+// Tiles whose box exceeds the 16 KB staging budget (strong zoom-out or rotation)
+// gather from global memory instead; tiles whose box misses the image store zeros.
+#include <climits>
+
 #include "kcmc_internal.h"
 
 namespace kcmc {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kTileW = 128;  // output columns per workgroup (32 threads x 4 px)
-constexpr int kTileH = 64;   // output rows per workgroup (8 row-groups x 8 passes)
+constexpr int kTileW = 128;    // output columns per workgroup (32 threads x 2 pairs of pixels)
+constexpr int kTileH = 32;     // output rows per workgroup (8 row groups x 4 passes)
+constexpr int kLdsElems = 8192;  // 16 KB of uint16 source staging per workgroup
 
 __device__ __forceinline__ int cv_round(double v) { return (int)__builtin_rint(v); }
 
@@ -72,70 +80,177 @@ __device__ __forceinline__ void bilinear_px(const uint16_t* __restrict__ S, int 
   }
 }
 
+// Bilinear blend of four taps exactly as remapBilinear<Cast<float, ushort>> does it:
+// float weights tab[fy] x tab[fx] (exact), separately rounded products, left-to-right sum.
+__device__ __forceinline__ uint16_t blend(float v00, float v01, float v10, float v11, int fx, int fy) {
+  const float wx0 = (float)(32 - fx) * 0.03125f, wx1 = (float)fx * 0.03125f;
+  const float wy0 = (float)(32 - fy) * 0.03125f, wy1 = (float)fy * 0.03125f;
+  return sat_u16(v00 * (wy0 * wx0) + v01 * (wy0 * wx1) + v10 * (wy1 * wx0) + v11 * (wy1 * wx1));
+}
+
 template <int C>
 __global__ __launch_bounds__(kThreads) void warp_affine_u16_kernel(const uint16_t* __restrict__ src,
                                                                    uint16_t* __restrict__ dst,
                                                                    const double* __restrict__ Mall, int H, int W,
                                                                    int inverse_map) {
+  __shared__ __attribute__((aligned(16))) uint16_t stile[kLdsElems];
   __shared__ int s_adelta[kTileW], s_bdelta[kTileW], s_X0[kTileH], s_Y0[kTileH];
+  __shared__ int s_box[5];  // mode, ax0 (first staged column), sy0 (first staged row), pitch, rows
   const int f = blockIdx.z;
   const int xb = blockIdx.x * kTileW, yb = blockIdx.y * kTileH;
-  const int tid = threadIdx.x;
-  double M[6];
-  if (inverse_map) {
-    for (int k = 0; k < 6; ++k) M[k] = Mall[6 * (size_t)f + k];
-  } else {
-    invert_affine(Mall + 6 * (size_t)f, M);
-  }
-  // per-column deltas (threads 0..127: a, 128..255: b) and per-row origins
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint16_t* S = src + (size_t)f * H * W * C;
+  uint16_t* Dst = dst + (size_t)f * H * W * C;
+
+  // ---- fixed-point coordinate tables (WarpAffineInvoker)
   {
-    const int x = xb + (tid & (kTileW - 1));
+    double M[6];
+    if (inverse_map) {
+      for (int k = 0; k < 6; ++k) M[k] = Mall[6 * (size_t)f + k];
+    } else {
+      invert_affine(Mall + 6 * (size_t)f, M);
+    }
+    const int xi = tid & (kTileW - 1);
+    const int x = xb + xi;
     if (tid < kTileW)
-      s_adelta[tid] = cv_round(M[0] * x * 1024);
+      s_adelta[xi] = cv_round(M[0] * x * 1024);
     else
-      s_bdelta[tid - kTileW] = cv_round(M[3] * x * 1024);
+      s_bdelta[xi] = cv_round(M[3] * x * 1024);
     if (tid < 2 * kTileH) {
-      const int y = yb + (tid & (kTileH - 1));
+      const int yi = tid & (kTileH - 1);
+      const int y = yb + yi;
       if (tid < kTileH)
-        s_X0[tid] = cv_round((M[1] * y + M[2]) * 1024) + 16;
+        s_X0[yi] = cv_round((M[1] * y + M[2]) * 1024) + 16;
       else
-        s_Y0[tid - kTileH] = cv_round((M[4] * y + M[5]) * 1024) + 16;
+        s_Y0[yi] = cv_round((M[4] * y + M[5]) * 1024) + 16;
     }
   }
   __syncthreads();
-  const uint16_t* S = src + (size_t)f * H * W * C;
-  uint16_t* Dst = dst + (size_t)f * H * W * C;
-  const int tx = tid & 31, ty = tid >> 5;
-  const int xl = tx * 4;
-  const int x = xb + xl;
-  int ad[4], bd[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    ad[p] = s_adelta[xl + p];
-    bd[p] = s_bdelta[xl + p];
+  // ---- exact source bounding box of the tile's valid pixels (wave 0)
+  if (tid < 64) {
+    int amin = INT_MAX, amax = INT_MIN, bmin = INT_MAX, bmax = INT_MIN;
+    int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
+    for (int i = lane; i < kTileW; i += 64)
+      if (xb + i < W) {
+        amin = min(amin, s_adelta[i]);
+        amax = max(amax, s_adelta[i]);
+        bmin = min(bmin, s_bdelta[i]);
+        bmax = max(bmax, s_bdelta[i]);
+      }
+    for (int i = lane; i < kTileH; i += 64)
+      if (yb + i < H) {
+        xmin = min(xmin, s_X0[i]);
+        xmax = max(xmax, s_X0[i]);
+        ymin = min(ymin, s_Y0[i]);
+        ymax = max(ymax, s_Y0[i]);
+      }
+    for (int o = 32; o > 0; o >>= 1) {
+      amin = min(amin, __shfl_xor(amin, o));
+      amax = max(amax, __shfl_xor(amax, o));
+      bmin = min(bmin, __shfl_xor(bmin, o));
+      bmax = max(bmax, __shfl_xor(bmax, o));
+      xmin = min(xmin, __shfl_xor(xmin, o));
+      xmax = max(xmax, __shfl_xor(xmax, o));
+      ymin = min(ymin, __shfl_xor(ymin, o));
+      ymax = max(ymax, __shfl_xor(ymax, o));
+    }
+    if (lane == 0) {
+      // sx = (X0 + adelta) >> 10; the second tap is sx + 1 (64-bit: no overflow here)
+      const long long sx0 = ((long long)xmin + amin) >> 10, sx1 = (((long long)xmax + amax) >> 10) + 1;
+      const long long sy0 = ((long long)ymin + bmin) >> 10, sy1 = (((long long)ymax + bmax) >> 10) + 1;
+      int mode = 2;  // 0: staged in LDS, 1: all taps outside the image, 2: direct gather
+      const long long lim = 30000;
+      const bool small = sx0 > -lim && sx1 < lim && sy0 > -lim && sy1 < lim;
+      if (small && (sx1 < 0 || sx0 > W - 1 || sy1 < 0 || sy0 > H - 1)) mode = 1;
+      const long long ax0 = (sx0 >> 3) << 3;
+      const long long pitch = ((sx1 - ax0 + 1) + 7) & ~7ll;
+      const long long rows = sy1 - sy0 + 1;
+      if (small && mode != 1 && pitch * rows * C <= kLdsElems) mode = 0;
+      s_box[0] = mode;
+      s_box[1] = (int)ax0;
+      s_box[2] = (int)sy0;
+      s_box[3] = (int)pitch;
+      s_box[4] = (int)rows;
+    }
   }
+  __syncthreads();
+  const int mode = s_box[0];
+  const int ax0 = s_box[1], sy0 = s_box[2], pitch = s_box[3], rows = s_box[4];
+
+  if (mode == 0) {
+    // ---- stage the box (zeros outside the image)
+    if (C == 1 && (W & 7) == 0) {
+      const int cpr = pitch >> 3;  // 16-byte chunks per staged row
+      for (int q = tid; q < rows * cpr; q += kThreads) {
+        const int r = q / cpr, c = q - r * cpr;
+        const int gy = sy0 + r, gx = ax0 + 8 * c;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if ((unsigned)gy < (unsigned)H) {
+          const uint16_t* row = S + (size_t)gy * W;
+          if (gx >= 0 && gx + 8 <= W) {
+            v = *reinterpret_cast<const uint4*>(row + gx);
+          } else {
+            uint16_t e[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) e[k] = ((unsigned)(gx + k) < (unsigned)W) ? row[gx + k] : (uint16_t)0;
+            v = make_uint4(e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16), e[4] | ((uint32_t)e[5] << 16),
+                           e[6] | ((uint32_t)e[7] << 16));
+          }
+        }
+        *reinterpret_cast<uint4*>(&stile[r * pitch + 8 * c]) = v;
+      }
+    } else {
+      for (int q = tid; q < rows * pitch * C; q += kThreads) {
+        const int r = q / (pitch * C), e = q - r * pitch * C;
+        const int gy = sy0 + r, gx = ax0 + e / C, k = e % C;
+        stile[q] = ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W) ? S[((size_t)gy * W + gx) * C + k]
+                                                                              : (uint16_t)0;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- output: thread (tx, ty) makes pixel pairs x = xb + 2*tx + 64*pp (+0, +1)
+  const int tx = tid & 31, ty = tid >> 5;
   for (int rr = ty; rr < kTileH; rr += kThreads / 32) {
     const int y = yb + rr;
     if (y >= H) break;
     const int X0 = s_X0[rr], Y0 = s_Y0[rr];
-    uint16_t o[4 * C];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int X = (X0 + ad[p]) >> 5, Y = (Y0 + bd[p]) >> 5;
-      bilinear_px<C>(S, H, W, X, Y, o + p * C);
-    }
-    uint16_t* drow = Dst + ((size_t)y * W + x) * C;
-    if (C == 1 && x + 4 <= W && (W & 3) == 0) {
-      uint2 v;
-      v.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-      v.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-      *reinterpret_cast<uint2*>(drow) = v;
-    } else {
+    for (int pp = 0; pp < 2; ++pp) {
+      const int xl = 2 * tx + 64 * pp;
+      const int x = xb + xl;
+      uint16_t o[2 * C];
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
-        if (x + p < W)
+      for (int q = 0; q < 2; ++q) {
+        const int X = (X0 + s_adelta[xl + q]) >> 5, Y = (Y0 + s_bdelta[xl + q]) >> 5;
+        if (x + q >= W) {  // outside the frame: nothing to compute or store
 #pragma unroll
-          for (int k = 0; k < C; ++k) drow[p * C + k] = o[p * C + k];
+          for (int k = 0; k < C; ++k) o[q * C + k] = 0;
+        } else if (mode == 0) {
+          const int sx = X >> 5, sy = Y >> 5, fx = X & 31, fy = Y & 31;
+          const int li = ((sy - sy0) * pitch + (sx - ax0)) * C;
+#pragma unroll
+          for (int k = 0; k < C; ++k)
+            o[q * C + k] = blend((float)stile[li + k], (float)stile[li + C + k], (float)stile[li + pitch * C + k],
+                                 (float)stile[li + pitch * C + C + k], fx, fy);
+        } else if (mode == 1) {
+#pragma unroll
+          for (int k = 0; k < C; ++k) o[q * C + k] = 0;
+        } else {
+          bilinear_px<C>(S, H, W, X, Y, o + q * C);
+        }
+      }
+      uint16_t* drow = Dst + ((size_t)y * W + x) * C;
+      if (C == 1 && x + 2 <= W && (W & 1) == 0) {
+        *reinterpret_cast<uint32_t*>(drow) = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          if (x + q < W)
+#pragma unroll
+            for (int k = 0; k < C; ++k) drow[q * C + k] = o[q * C + k];
+      }
     }
   }
 }
