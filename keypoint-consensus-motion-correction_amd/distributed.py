@@ -67,10 +67,9 @@ def _all_gather_rows(t: torch.Tensor, counts: List[int], group=None) -> torch.Te
     fmax = max(counts)
     pad = torch.zeros((fmax,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     pad[: t.shape[0]] = t
-    out = torch.empty((world * fmax,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, pad, group=group)
-    parts = [out[r * fmax : r * fmax + counts[r]] for r in range(world)]
-    return torch.cat(parts, 0)
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad, group=group)
+    return torch.cat([outs[r][: counts[r]] for r in range(world)], 0)
 
 
 def broadcast_template(des_tpl: torch.Tensor, kp_tpl: torch.Tensor, group=None, src: int = 0):
@@ -82,9 +81,9 @@ def broadcast_template(des_tpl: torch.Tensor, kp_tpl: torch.Tensor, group=None, 
 def frame_counts(n_local: int, device: torch.device, group=None) -> List[int]:
     world = dist.get_world_size(group)
     t = torch.tensor([n_local], dtype=torch.int64, device=device)
-    out = torch.empty(world, dtype=torch.int64, device=device)
-    dist.all_gather_into_tensor(out, t, group=group)
-    return [int(x) for x in out.cpu().tolist()]
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t, group=group)
+    return [int(o.item()) for o in outs]
 
 
 def align_sharded(inp: _pl.SlabInputs, cfg: _pl.AlignConfig, group=None, impl: SlabStages = HIP_STAGES,

@@ -245,3 +245,18 @@ def test_warp_multichannel(dev, C):
     out = stages.warp_affine_u16(_t(imgs, dev), _t(Ms, dev)).cpu().numpy()
     for f in range(2):
         assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], Ms[f]))
+
+
+def test_warp_all_tile_paths_at_1080p(dev):
+    """Rotations/zooms that put tiles on every path: LDS-staged boxes, boxes too large
+    for LDS (direct gather), and boxes entirely outside the frame (zeros)."""
+    rng = np.random.default_rng(41)
+    H, W = 1080, 1920
+    img = rng.integers(0, 65536, (H, W)).astype(np.uint16)
+    Ms = [synthetic.rigid(np.deg2rad(6.0), 10.5, -7.25), synthetic.rigid(np.deg2rad(-30.0), 300, 100),
+          np.array([[0.6, 0.01, 5.0], [-0.01, 0.6, 3.0]]), np.array([[1.8, 0.0, -400.0], [0.0, 1.8, -300.0]]),
+          synthetic.rigid(0.0, 1500.0, 0.0)]
+    imgs = np.broadcast_to(img, (len(Ms), H, W)).copy()
+    out = stages.warp_affine_u16(_t(imgs, dev), _t(np.stack(Ms), dev)).cpu().numpy()
+    for f, M in enumerate(Ms):
+        assert np.array_equal(out[f], oracle.warp_affine_u16(img, M)), f

@@ -10,14 +10,15 @@ import sys
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name)  # drop the argument list
-    name = name.replace("kcmc::(anonymous namespace)::", "kcmc::")
     return name[:110]
 
 
 def rows_from_db(path):
     c = sqlite3.connect(path)
-    return [(r[0], int(r[1]), float(r[2]), float(r[3]), float(r[4]))
+    # the top_kernels view reports microseconds; normalise to nanoseconds like the CSV
+    return [(r[0], int(r[1]), 1e3 * float(r[2]), 1e3 * float(r[3]), float(r[4]))
             for r in c.execute("select name, total_calls, total_duration, average, percentage from top_kernels")]
 
 
