@@ -190,7 +190,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--frames", type=int, default=2000, help="frames per GPU (config[1]: 2000)")
-    ap.add_argument("--cpu-sample", type=int, default=24, help="frames in the CPU-baseline sample (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=240, help="frames in the CPU-baseline sample (0: skip)")
     args = ap.parse_args()
 
     rank, world, local = kdist.init_from_env("nccl")

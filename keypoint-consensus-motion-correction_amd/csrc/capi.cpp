@@ -52,16 +52,47 @@ extern "C" int kcmc_create(int device, kcmc_ctx** out) {
 
 extern "C" int kcmc_destroy(kcmc_ctx* ctx) {
   if (!ctx) return KCMC_OK;
-  if (ctx->hyp || ctx->hyp_off) {
+  if (ctx->hyp || ctx->hyp_off || ctx->ws_pool) {
     int prev = 0;
     hipGetDevice(&prev);
     hipSetDevice(ctx->device);
     free_tables(ctx);
+    if (ctx->ws_pool) {
+      hipDeviceSynchronize();  // pending stream-ordered frees return to the pool first
+      hipMemPoolDestroy(ctx->ws_pool);
+    }
     hipSetDevice(prev);
   }
   delete ctx;
   return KCMC_OK;
 }
+
+namespace kcmc {
+
+int workspace_alloc(kcmc_ctx* ctx, void** p, size_t bytes, hipStream_t s) {
+  if (!ctx->ws_pool) {
+    hipMemPoolProps props = {};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = ctx->device;
+    KCMC_TRY(hip_check(hipMemPoolCreate(&ctx->ws_pool, &props), "hipMemPoolCreate"));
+    uint64_t keep = UINT64_MAX;  // never trim: the same sizes come back every call
+    KCMC_TRY(hip_check(hipMemPoolSetAttribute(ctx->ws_pool, hipMemPoolAttrReleaseThreshold, &keep),
+                       "hipMemPoolSetAttribute"));
+  }
+  if (hipMallocFromPoolAsync(p, bytes, ctx->ws_pool, s) != hipSuccess) {
+    hipGetLastError();
+    return fail(KCMC_ENOMEM, "workspace: device out of memory (" + std::to_string(bytes) + " bytes)");
+  }
+  return KCMC_OK;
+}
+
+int workspace_free(kcmc_ctx* ctx, void* p, hipStream_t s) {
+  (void)ctx;
+  return hip_check(hipFreeAsync(p, s), "hipFreeAsync");
+}
+
+}  // namespace kcmc
 
 static void free_tables(kcmc_ctx* ctx) {
   if (ctx->hyp) hipFree(ctx->hyp);

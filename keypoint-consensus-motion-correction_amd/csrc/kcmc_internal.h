@@ -21,6 +21,9 @@ struct kcmc_ctx {
   int hyp_off_len = 0;
   int hyp_trials = 0;
   uint32_t hyp_seed = 0;
+  // Stream-ordered scratch (per-call workspaces, e.g. the warp's tile plans): a private
+  // memory pool that keeps its pages between calls.
+  hipMemPool_t ws_pool = nullptr;
 };
 
 namespace kcmc {
@@ -32,6 +35,11 @@ int hip_check(hipError_t e, const char* what);
 int launch_check(const char* what);
 
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+// Stream-ordered workspace from the context's pool (valid for work enqueued on `s`
+// until workspace_free, which is itself stream-ordered).
+int workspace_alloc(kcmc_ctx* ctx, void** p, size_t bytes, hipStream_t s);
+int workspace_free(kcmc_ctx* ctx, void* p, hipStream_t s);
 
 }  // namespace kcmc
 

@@ -11,16 +11,22 @@
 // This file is compiled with -ffp-contract=off so that arithmetic is reproduced
 // operation by operation.
 //
-// Layout: frames [F, H, W, C] u16 contiguous in HBM.  One workgroup covers a
-// 128-column x 32-row output tile of one frame.  The per-column deltas and per-row
-// origins are computed once into LDS (the only double-precision work).  Because the
-// fixed-point source coordinate is separable (X = X0[y] + adelta[x]), the exact source
-// bounding box of the tile follows from four min/max reductions; the box is staged
-// into LDS with coalesced 16-byte loads (zero outside the image, which is exactly
-// BORDER_CONSTANT), and every output pixel gathers its four taps from LDS.  Each
-// thread writes pixel pairs as 4-byte stores (a wave writes 256 contiguous bytes).
-// Tiles whose box exceeds the 16 KB staging budget (strong zoom-out or rotation)
-// gather from global memory instead; tiles whose box misses the image store zeros.
+// Layout: frames [F, H, W, C] u16 contiguous in HBM, processed in 128 x 56 output
+// tiles.  Because the fixed-point source coordinate is separable (X = X0[y] + adelta[x])
+// and monotone, the exact source bounding box of a tile follows from its corner values;
+// the box is staged into LDS with coalesced 16-byte loads (zero outside the image,
+// which is exactly BORDER_CONSTANT) and every output pixel gathers its four taps from
+// LDS with aligned 16-bit reads.  A wave makes one 128-pixel output row at a time
+// (lane l: pixels 2l, 2l+1, one 4-byte store), so its tap reads cover consecutive LDS
+// words without bank conflicts and its row-level state is wave-uniform.  Tiles whose box exceeds the staging budget (strong
+// zoom-out or rotation) gather from global memory instead; tiles whose box misses the
+// image store zeros.
+//
+// Two launches: warp_plan_kernel (one thread per tile) inverts the map in fp64 and
+// derives each tile's source box, so that the tile kernel starts with scalar loads of
+// its plan and issues its staging loads immediately; warp_affine_u16_kernel then makes
+// one tile per workgroup, latency hidden by the other resident workgroups (a persistent
+// double-buffered variant measured 25% slower).
 #include <climits>
 
 #include "kcmc_internal.h"
@@ -29,11 +35,16 @@ namespace kcmc {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kTileW = 128;      // output columns per workgroup (32 threads x 2 pairs of pixels)
-constexpr int kTileH = 64;       // output rows per workgroup (8 row groups x 8 passes)
-constexpr int kLdsElems = 12288; // 24 KB of uint16 source staging per workgroup
-constexpr int kMaxPitch = 256;   // staged row length limit (32 x 16-byte chunks)
-constexpr int kRowPasses = 10;   // staging passes of 8 rows x 32 chunks: box rows <= 80
+constexpr int kTileW = 128;     // output columns per tile (64 lanes x 2 pixels)
+constexpr int kMaxPitch = 256;  // staged row length limit (32 x 16-byte chunks)
+
+template <int TILE_H, int LDS_ELEMS, int ROW_PASSES>
+struct WarpCfg {
+  static constexpr int kTileH = TILE_H;          // output rows per tile (4 waves x kTileH/4)
+  static constexpr int kLdsElems = LDS_ELEMS;    // uint16 staging budget per box
+  static constexpr int kRowPasses = ROW_PASSES;  // staging passes of 8 rows x 32 chunks
+};
+using BlockCfg = WarpCfg<56, 10240, 9>;  // 20 KB box, box rows <= 72 (7 workgroups per CU)
 
 __device__ __forceinline__ int cv_round(double v) { return (int)__builtin_rint(v); }
 
@@ -60,17 +71,27 @@ __device__ __forceinline__ void invert_affine(const double* Min, double* M) {
   M[5] = b2;
 }
 
-typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void load_map(const double* __restrict__ Mall, int f, int inverse_map, double* M) {
+  if (inverse_map) {
+    for (int k = 0; k < 6; ++k) M[k] = Mall[6 * (size_t)f + k];
+  } else {
+    invert_affine(Mall + 6 * (size_t)f, M);
+  }
+}
 
-// Bilinear blend of four taps exactly as remapBilinear<Cast<float, ushort>> does it:
-// float weights tab[fy] x tab[fx] (each (32-f)/32 or f/32, products exact), separately
-// rounded tap products, left-to-right sum.  Weight pairs use packed f32 math.
-__device__ __forceinline__ uint16_t blend(float v00, float v01, float v10, float v11, int fx, int fy) {
-  const f2 wx = __builtin_elementwise_fma(f2{(float)fx, (float)fx}, f2{-0.03125f, 0.03125f}, f2{1.f, 0.f});
-  const f2 wy = __builtin_elementwise_fma(f2{(float)fy, (float)fy}, f2{-0.03125f, 0.03125f}, f2{1.f, 0.f});
-  const f2 p01 = f2{v00, v01} * (wy.x * wx);
-  const f2 p23 = f2{v10, v11} * (wy.y * wx);
-  return sat_u16(((p01.x + p01.y) + p23.x) + p23.y);
+// remapBilinear<Cast<float, ushort>>'s blend in exact integer/float steps that are cheap
+// on the VALU: w_k = K_k / 1024 with K_k = (32-fy|fy) * (32-fx|fx) an integer, and
+// fl(v * K/1024) = fl(v*K) * 2^-10 (power-of-two scaling commutes with rounding), where
+// fl(v*K) = cvt_f32_u32(v*K) because the integer product is exact and the conversion
+// rounds to nearest-even like the multiply.  The left-to-right sum scales the same way.
+__device__ __forceinline__ uint16_t blend_int(uint32_t v00, uint32_t v01, uint32_t v10, uint32_t v11, int fx,
+                                              int fy) {
+  const uint32_t ax = 32 - fx, ay = 32 - fy;
+  const float q0 = (float)__umul24(v00, __umul24(ay, ax));
+  const float q1 = (float)__umul24(v01, __umul24(ay, (uint32_t)fx));
+  const float q2 = (float)__umul24(v10, __umul24((uint32_t)fy, ax));
+  const float q3 = (float)__umul24(v11, __umul24((uint32_t)fy, (uint32_t)fx));
+  return sat_u16((((q0 + q1) + q2) + q3) * 0.0009765625f);
 }
 
 // Direct-gather path (tiles whose source box does not fit the LDS budget): taps are
@@ -88,10 +109,10 @@ __device__ __forceinline__ void bilinear_px(const uint16_t* __restrict__ S, int 
   const size_t r0 = (size_t)cy0 * W, r1 = (size_t)cy1 * W;
 #pragma unroll
   for (int k = 0; k < C; ++k) {
-    const uint16_t t00 = S[(r0 + cx0) * C + k], t01 = S[(r0 + cx1) * C + k];
-    const uint16_t t10 = S[(r1 + cx0) * C + k], t11 = S[(r1 + cx1) * C + k];
-    out[k] = blend((x0 && y0) ? (float)t00 : 0.f, (x1 && y0) ? (float)t01 : 0.f, (x0 && y1) ? (float)t10 : 0.f,
-                   (x1 && y1) ? (float)t11 : 0.f, fx, fy);
+    const uint32_t t00 = S[(r0 + cx0) * C + k], t01 = S[(r0 + cx1) * C + k];
+    const uint32_t t10 = S[(r1 + cx0) * C + k], t11 = S[(r1 + cx1) * C + k];
+    out[k] = blend_int((x0 && y0) ? t00 : 0u, (x1 && y0) ? t01 : 0u, (x0 && y1) ? t10 : 0u, (x1 && y1) ? t11 : 0u,
+                       fx, fy);
   }
 }
 
@@ -107,9 +128,9 @@ struct Box {
 // X0[y] = cvRound((M1*y + M2)*1024) + 16 are monotone in x and y (monotone products,
 // sums and rounding), so their extremes sit at the tile's first/last valid column/row
 // and sx = (X0[y] + adelta[x]) >> 10 spans [min, max] exactly; the second tap adds 1.
-template <int C>
+template <class Cfg, int C>
 __device__ __forceinline__ Box source_box(const double* M, int xb, int yb, int H, int W) {
-  const int xl = min(xb + kTileW, W) - 1, yl = min(yb + kTileH, H) - 1;
+  const int xl = min(xb + kTileW, W) - 1, yl = min(yb + Cfg::kTileH, H) - 1;
   const long long a0 = cv_round(M[0] * xb * 1024), a1 = cv_round(M[0] * xl * 1024);
   const long long b0 = cv_round(M[3] * xb * 1024), b1 = cv_round(M[3] * xl * 1024);
   const long long x0 = cv_round((M[1] * yb + M[2]) * 1024) + 16, x1 = cv_round((M[1] * yl + M[2]) * 1024) + 16;
@@ -125,7 +146,7 @@ __device__ __forceinline__ Box source_box(const double* M, int xb, int yb, int H
   b.mode = 2;
   if (small && (sx1 < 0 || sx0 > W - 1 || sy1 < 0 || sy0 > H - 1))
     b.mode = 1;
-  else if (small && pitch <= kMaxPitch && rows <= 8 * kRowPasses && pitch * rows * C <= kLdsElems)
+  else if (small && pitch <= kMaxPitch && rows <= 8 * Cfg::kRowPasses && pitch * rows * C <= Cfg::kLdsElems)
     b.mode = 0;
   b.ax0 = (int)ax0;
   b.sy0 = (int)sy0;
@@ -134,176 +155,279 @@ __device__ __forceinline__ Box source_box(const double* M, int xb, int yb, int H
   return b;
 }
 
-
-
-// LDS tap read.  ALIGNED16 keeps every read a naturally aligned ds_read_u16 (the
-// compiler otherwise fuses the two horizontal taps into one 4-byte read at a 2-byte
-// aligned address).
-template <bool ALIGNED16>
-__device__ __forceinline__ float tap(const uint16_t* stile, int i) {
-  if (ALIGNED16)
-    return (float)__hip_atomic_load(const_cast<uint16_t*>(stile) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return (float)stile[i];
-}
-
-// Output rows of one tile on one path (0: LDS-staged box, 1: zeros, 2: direct gather).
-template <int C, int MODE, bool ALIGNED16 = false>
-__device__ __forceinline__ void output_rows(const uint16_t* stile, const Box& box, const uint16_t* __restrict__ S,
-                                            uint16_t* __restrict__ Dst, int H, int W, int xb, int yb, int tx, int ty,
-                                            const int (&ad)[4], const int (&bd)[4], const int* s_X0,
-                                            const int* s_Y0) {
-  for (int rr = ty; rr < kTileH; rr += kThreads / 32) {
-    const int y = yb + rr;
-    if (y >= H) break;
-    const int X0 = s_X0[rr], Y0 = s_Y0[rr];
-    uint16_t o[4 * C];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int X = (X0 + ad[p]) >> 5, Y = (Y0 + bd[p]) >> 5;
-      if (MODE == 0) {
-        const int sx = X >> 5, sy = Y >> 5, fx = X & 31, fy = Y & 31;
-        const int li = ((sy - box.sy0) * box.pitch + (sx - box.ax0)) * C;
-#pragma unroll
-        for (int k = 0; k < C; ++k) {
-          const int i00 = li + k, i10 = li + box.pitch * C + k;
-          o[p * C + k] = blend(tap<ALIGNED16>(stile, i00), tap<ALIGNED16>(stile, i00 + C), tap<ALIGNED16>(stile, i10),
-                               tap<ALIGNED16>(stile, i10 + C), fx, fy);
-        }
-      } else if (MODE == 1) {
-#pragma unroll
-        for (int k = 0; k < C; ++k) o[p * C + k] = 0;
-      } else {
-        bilinear_px<C>(S, H, W, X, Y, o + p * C);
-      }
-    }
-#pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-      const int x = xb + 2 * tx + 64 * pp;
-      uint16_t* drow = Dst + ((size_t)y * W + x) * C;
-      if (C == 1 && x + 2 <= W && (W & 1) == 0) {
-        *reinterpret_cast<uint32_t*>(drow) = (uint32_t)o[2 * pp] | ((uint32_t)o[2 * pp + 1] << 16);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-          if (x + q < W)
-#pragma unroll
-            for (int k = 0; k < C; ++k) drow[q * C + k] = o[(2 * pp + q) * C + k];
-      }
-    }
-  }
-}
-
-// VARIANT != 0 builds are ablations for tools/warp_lab.hip only (1: skip the per-pixel
-// work, 2: skip the staging loads, 3: stores only, 4: aligned 16-bit tap reads); the
-// library launches VARIANT 0.
-template <int C, int VARIANT = 0>
-__global__ __launch_bounds__(kThreads) void warp_affine_u16_kernel(const uint16_t* __restrict__ src,
-                                                                   uint16_t* __restrict__ dst,
-                                                                   const double* __restrict__ Mall, int H, int W,
-                                                                   int inverse_map) {
-  __shared__ __attribute__((aligned(16))) uint16_t stile[kLdsElems];
-  __shared__ int s_adelta[kTileW], s_bdelta[kTileW], s_X0[kTileH], s_Y0[kTileH];
-  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so give each
-  // XCD a contiguous run of tiles (neighbouring tiles share halo rows in that XCD's L2).
-  const int ntx = gridDim.x, nty = gridDim.y;
-  const int nwg = ntx * nty * gridDim.z;
-  const int bid = blockIdx.x + ntx * (blockIdx.y + nty * blockIdx.z);
-  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
-  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int f = tile / (ntx * nty);
-  const int t2 = tile - f * ntx * nty;
-  const int xb = (t2 % ntx) * kTileW, yb = (t2 / ntx) * kTileH;
-  const int tid = threadIdx.x;
-  const uint16_t* S = src + (size_t)f * H * W * C;
-  uint16_t* Dst = dst + (size_t)f * H * W * C;
-
-  double M[6];
-  if (inverse_map) {
-    for (int k = 0; k < 6; ++k) M[k] = Mall[6 * (size_t)f + k];
-  } else {
-    invert_affine(Mall + 6 * (size_t)f, M);
-  }
-  const Box box = source_box<C>(M, xb, yb, H, W);
-  const bool vec_stage = (C == 1) && ((W & 7) == 0);
-
-  // ---- 1. issue the staging loads first (16-byte chunks; with W % 8 == 0 a chunk
-  //         is either entirely inside the image or entirely outside -> zeros).
-  //         Thread = (chunk c = tid & 31, row r = tid >> 5 + 8k): no integer division.
-  uint4 chunk[kRowPasses];
+// Staging of a box.  With C == 1 and W % 8 == 0 every 16-byte chunk is entirely inside
+// or entirely outside the image (zeros).  Thread = (chunk c = tid & 31, row r = tid>>5 + 8k).
+template <class Cfg>
+__device__ __forceinline__ void stage_issue(const uint16_t* __restrict__ S, const Box& box, int H, int W, int tid,
+                                            uint4 (&chunk)[Cfg::kRowPasses]) {
   const int cpr = box.pitch >> 3;
   const int sc = tid & 31, sr = tid >> 5;
   const int gx = box.ax0 + 8 * sc;
   const bool col_ok = sc < cpr && gx >= 0 && gx < W;
-  if (box.mode == 0 && vec_stage && VARIANT != 2 && VARIANT != 3) {
 #pragma unroll
-    for (int k = 0; k < kRowPasses; ++k) {
-      const int r = sr + 8 * k;
-      const int gy = box.sy0 + r;
-      chunk[k] = make_uint4(0u, 0u, 0u, 0u);
-      if (r < box.rows && col_ok && (unsigned)gy < (unsigned)H)
-        chunk[k] = *reinterpret_cast<const uint4*>(S + (size_t)gy * W + gx);
-    }
+  for (int k = 0; k < Cfg::kRowPasses; ++k) {
+    const int r = sr + 8 * k;
+    const int gy = box.sy0 + r;
+    chunk[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (r < box.rows && col_ok && (unsigned)gy < (unsigned)H)
+      chunk[k] = *reinterpret_cast<const uint4*>(S + (size_t)gy * W + gx);
   }
-  // ---- 2. fixed-point coordinate tables (WarpAffineInvoker), overlapping the loads
-  {
-    const int xi = tid & (kTileW - 1);
-    const int x = xb + xi;
-    if (tid < kTileW)
-      s_adelta[xi] = cv_round(M[0] * x * 1024);
-    else
-      s_bdelta[xi] = cv_round(M[3] * x * 1024);
-    if (tid < 2 * kTileH) {
-      const int yi = tid & (kTileH - 1);
-      const int y = yb + yi;
-      if (tid < kTileH)
-        s_X0[yi] = cv_round((M[1] * y + M[2]) * 1024) + 16;
-      else
-        s_Y0[yi] = cv_round((M[4] * y + M[5]) * 1024) + 16;
-    }
-  }
-  // ---- 3. land the staged box in LDS
-  if (box.mode == 0) {
-    if (vec_stage) {
+}
+
+template <class Cfg>
+__device__ __forceinline__ void stage_land(uint16_t* stile, const Box& box, int tid,
+                                           const uint4 (&chunk)[Cfg::kRowPasses]) {
+  const int cpr = box.pitch >> 3;
+  const int sc = tid & 31, sr = tid >> 5;
 #pragma unroll
-      for (int k = 0; k < kRowPasses; ++k) {
-        const int r = sr + 8 * k;
-        if (r < box.rows && sc < cpr) *reinterpret_cast<uint4*>(&stile[r * box.pitch + 8 * sc]) = chunk[k];
+  for (int k = 0; k < Cfg::kRowPasses; ++k) {
+    const int r = sr + 8 * k;
+    if (r < box.rows && sc < cpr) *reinterpret_cast<uint4*>(&stile[r * box.pitch + 8 * sc]) = chunk[k];
+  }
+}
+
+// Element-wise staging (C > 1 or W % 8 != 0).
+template <int C>
+__device__ __forceinline__ void stage_scalar(const uint16_t* __restrict__ S, uint16_t* stile, const Box& box, int H,
+                                             int W, int tid) {
+  for (int q = tid; q < box.rows * box.pitch * C; q += kThreads) {
+    const int r = q / (box.pitch * C), e = q - r * box.pitch * C;
+    const int gy = box.sy0 + r, gx = box.ax0 + e / C, k = e % C;
+    stile[q] = ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W) ? S[((size_t)gy * W + gx) * C + k]
+                                                                          : (uint16_t)0;
+  }
+}
+
+// rint(S / 1024) (round half to even) for an integer S < 2^24, as the low 16 bits of
+// fl(S * 2^-10 + 1.5 * 2^23): float(S) and the scaling are exact, the fused add rounds
+// once to an integer (ulp 1 at that magnitude) in round-to-nearest-even.
+__device__ __forceinline__ uint16_t round_q10(uint32_t S) {
+  return (uint16_t)__float_as_uint(__builtin_fmaf((float)S, 0x1p-10f, 12582912.0f));
+}
+
+__device__ __forceinline__ uint32_t tap(const uint16_t* stile, int i) { return stile[i]; }
+
+// Per-tile plan made by warp_plan_kernel.
+struct TilePlan {
+  int mode, ax0, sy0;
+  int pitch_rows;  // pitch | rows << 16
+};
+
+__device__ __forceinline__ Box unpack(const TilePlan& t) {
+  Box b;
+  b.mode = t.mode;
+  b.ax0 = t.ax0;
+  b.sy0 = t.sy0;
+  b.pitch = t.pitch_rows & 0xffff;
+  b.rows = t.pitch_rows >> 16;
+  return b;
+}
+
+// Per-thread coordinates of one tile (WarpAffineInvoker): adelta/bdelta of the lane's two
+// columns, and in lane i < kTileH/4 the row origins X0/Y0 of the wave's i-th row.  For a
+// staged tile the box origin (ox, oy) is folded into the row origins (a multiple of 1024
+// in fixed point, so the fractional bits are unchanged): coordinates are box-relative.
+// Columns past the frame edge reuse the last valid column's coordinates so that their
+// (never stored) taps stay inside the box.
+template <class Cfg>
+__device__ __forceinline__ void lane_coords(const double* __restrict__ M, int xb, int yb, int W, int wave, int lane,
+                                            int ox, int oy, int (&ad)[2], int (&bd)[2], int& X0v, int& Y0v) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int x = min(xb + 2 * lane + q, W - 1);
+    ad[q] = cv_round(M[0] * x * 1024);
+    bd[q] = cv_round(M[3] * x * 1024);
+  }
+  const int y = yb + wave + 4 * min(lane, Cfg::kTileH / 4 - 1);
+  X0v = cv_round((M[1] * y + M[2]) * 1024) + 16 - ox * 1024;
+  Y0v = cv_round((M[4] * y + M[5]) * 1024) + 16 - oy * 1024;
+}
+
+// Output rows of one tile on one path (0: LDS-staged box, 1: zeros, 2: direct gather).
+// Wave w makes rows w, w + 4, ...; lane l pixels x = xb + 2l, xb + 2l + 1.
+template <class Cfg, int C, int MODE>
+__device__ __forceinline__ void output_rows(const uint16_t* stile, const Box& box, const uint16_t* __restrict__ S,
+                                            uint16_t* __restrict__ Dst, int H, int W, int xb, int yb, int wave,
+                                            int lane, const int (&ad)[2], const int (&bd)[2], int X0v, int Y0v) {
+  const int x = xb + 2 * lane;
+  const bool pair_store = C == 1 && (W & 1) == 0 && x + 2 <= W;
+#pragma unroll
+  for (int i = 0; i < Cfg::kTileH / 4; ++i) {
+    const int y = yb + wave + 4 * i;  // wave-uniform
+    if (y >= H) break;
+    const int X0 = __builtin_amdgcn_readlane(X0v, i), Y0 = __builtin_amdgcn_readlane(Y0v, i);
+    uint16_t o[2 * C];
+    if (MODE == 0) {
+      // Box-relative taps.  The blend is first evaluated exactly in integers,
+      // S = ay*(v00*ax + v01*fx) + fy*(v10*ax + v11*fx) = sum v_k*K_k: while S < 2^24
+      // every product and partial sum of OpenCV's float evaluation is an integer below
+      // 2^24 as well, hence exact, and its result is rint(S/1024).  Only pixels with
+      // S >= 2^24 (bright: taps beyond 14 bits) take the float-faithful blend.
+      uint32_t Sx[2 * C], hi = 0, fx[2], fy[2], li[2], v[2][C][4];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int tX = X0 + ad[p], tY = Y0 + bd[p];
+        fx[p] = (tX >> 5) & 31;
+        fy[p] = (tY >> 5) & 31;
+        li[p] = __umul24((uint32_t)(tY >> 10), (uint32_t)box.pitch) + (uint32_t)(tX >> 10);
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+          const int i00 = li[p] * C + k, i10 = i00 + box.pitch * C;
+          v[p][k][0] = tap(stile, i00);
+          v[p][k][1] = tap(stile, i00 + C);
+          v[p][k][2] = tap(stile, i10);
+          v[p][k][3] = tap(stile, i10 + C);
+        }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const uint32_t ax = 32 - fx[p], ay = 32 - fy[p];
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+          uint32_t h0 = __umul24(v[p][k][0], ax) + __umul24(v[p][k][1], fx[p]);
+          uint32_t h1 = __umul24(v[p][k][2], ax) + __umul24(v[p][k][3], fx[p]);
+          // keep the separable form (the compiler would otherwise expand it into the
+          // four weight products, three more multiplies)
+          asm volatile("" : "+v"(h0), "+v"(h1));
+          const uint32_t Sv = __umul24(h0, ay) + __umul24(h1, fy[p]);
+          Sx[p * C + k] = Sv;
+          hi |= Sv;
+          o[p * C + k] = round_q10(Sv);
+        }
+      }
+      if (hi >> 24) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int k = 0; k < C; ++k)
+            if (Sx[p * C + k] >> 24)
+              o[p * C + k] = blend_int(v[p][k][0], v[p][k][1], v[p][k][2], v[p][k][3], fx[p], fy[p]);
       }
     } else {
-      for (int q = tid; q < box.rows * box.pitch * C; q += kThreads) {
-        const int r = q / (box.pitch * C), e = q - r * box.pitch * C;
-        const int gy = box.sy0 + r, gx = box.ax0 + e / C, k = e % C;
-        stile[q] = ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W) ? S[((size_t)gy * W + gx) * C + k]
-                                                                              : (uint16_t)0;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int X = (X0 + ad[p]) >> 5, Y = (Y0 + bd[p]) >> 5;
+        if (MODE == 1) {
+#pragma unroll
+          for (int k = 0; k < C; ++k) o[p * C + k] = 0;
+        } else {
+          bilinear_px<C>(S, H, W, X, Y, o + p * C);
+        }
       }
+    }
+    uint16_t* drow = Dst + ((size_t)y * W + x) * C;
+    if (pair_store) {
+      *reinterpret_cast<uint32_t*>(drow) = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (x + q < W)
+#pragma unroll
+          for (int k = 0; k < C; ++k) drow[q * C + k] = o[q * C + k];
+    }
+  }
+}
+
+// One row loop per path (a path-uniform branch inside the loop makes the compiler drain
+// the previous rows' stores with s_waitcnt vmcnt(0) every row).
+template <class Cfg, int C>
+__device__ __forceinline__ void output_tile(int mode, const uint16_t* stile, const Box& box,
+                                            const uint16_t* __restrict__ S, uint16_t* __restrict__ Dst, int H, int W,
+                                            int xb, int yb, int wave, int lane, const int (&ad)[2], const int (&bd)[2],
+                                            int X0v, int Y0v) {
+  if (mode == 0)
+    output_rows<Cfg, C, 0>(stile, box, S, Dst, H, W, xb, yb, wave, lane, ad, bd, X0v, Y0v);
+  else if (mode == 1)
+    output_rows<Cfg, C, 1>(stile, box, S, Dst, H, W, xb, yb, wave, lane, ad, bd, X0v, Y0v);
+  else
+    output_rows<Cfg, C, 2>(stile, box, S, Dst, H, W, xb, yb, wave, lane, ad, bd, X0v, Y0v);
+}
+
+// XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so give each XCD a
+// contiguous run of ids (bijective also when n % 8 != 0).
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
+  const int q8 = n >> 3, r8 = n & 7, xcd = bid & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+// ------------------------------------------------------------------------- plan
+// One thread per tile (tile id = (f * nty + ty) * ntx + tx): the fp64 map inversion
+// (written once per frame to minv) and the tile's source box.
+template <int C, class Cfg>
+__global__ __launch_bounds__(256) void warp_plan_kernel(const double* __restrict__ Mall, int n_frames, int H, int W,
+                                                        int inverse_map, int ntx, int nty,
+                                                        TilePlan* __restrict__ plan, double* __restrict__ minv) {
+  const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (t >= (long long)ntx * nty * n_frames) return;
+  const int f = (int)(t / (ntx * nty)), t2 = (int)(t - (long long)f * ntx * nty);
+  const int xb = (t2 % ntx) * kTileW, yb = (t2 / ntx) * Cfg::kTileH;
+  double M[6];
+  load_map(Mall, f, inverse_map, M);
+  if (t2 == 0)
+    for (int k = 0; k < 6; ++k) minv[6 * (size_t)f + k] = M[k];
+  const Box b = source_box<Cfg, C>(M, xb, yb, H, W);
+  plan[t] = TilePlan{b.mode, b.ax0, b.sy0, b.pitch | (b.rows << 16)};
+}
+
+// ------------------------------------------------------------ one tile per workgroup
+// VARIANT != 0 builds are ablations for tools/warp_lab.hip only (1: zeros instead of the
+// per-pixel work, 2: skip the staging loads); the library launches VARIANT 0.
+// no-unaligned-access-mode: keeps the two adjacent 16-bit tap reads from being fused
+// into one 4-byte LDS read at a 2-byte-aligned address, which the LDS replays (1.75x
+// slower kernel, measured in tools/warp_lab).
+template <int C, class Cfg = BlockCfg, int VARIANT = 0>
+__global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-access-mode"))) void warp_affine_u16_kernel(
+    const uint16_t* __restrict__ src, uint16_t* __restrict__ dst, const TilePlan* __restrict__ plan,
+    const double* __restrict__ minv, int H, int W) {
+  __shared__ __attribute__((aligned(16))) uint16_t stile[Cfg::kLdsElems];
+  const int ntx = gridDim.x, nty = gridDim.y;
+  const int tile = xcd_remap(blockIdx.x + ntx * (blockIdx.y + nty * blockIdx.z), ntx * nty * gridDim.z);
+  const int f = tile / (ntx * nty);
+  const int t2 = tile - f * ntx * nty;
+  const int xb = (t2 % ntx) * kTileW, yb = (t2 / ntx) * Cfg::kTileH;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const uint16_t* S = src + (size_t)f * H * W * C;
+  uint16_t* Dst = dst + (size_t)f * H * W * C;
+
+  const Box box = unpack(plan[tile]);
+  const bool vec_stage = (C == 1) && ((W & 7) == 0);
+  uint4 chunk[Cfg::kRowPasses];
+  if (box.mode == 0 && vec_stage && VARIANT != 2) stage_issue<Cfg>(S, box, H, W, tid, chunk);  // loads first
+  int ad[2], bd[2], X0v, Y0v;  // overlaps the loads
+  lane_coords<Cfg>(minv + 6 * (size_t)f, xb, yb, W, wave, lane, box.mode == 0 ? box.ax0 : 0,
+                   box.mode == 0 ? box.sy0 : 0, ad, bd, X0v, Y0v);
+  if (box.mode == 0) {
+    if (vec_stage) {
+      if (VARIANT != 2) stage_land<Cfg>(stile, box, tid, chunk);
+    } else {
+      stage_scalar<C>(S, stile, box, H, W, tid);
     }
   }
   __syncthreads();
+  output_tile<Cfg, C>(VARIANT == 1 ? 1 : box.mode, stile, box, S, Dst, H, W, xb, yb, wave, lane, ad, bd, X0v, Y0v);
+}
 
-  // ---- 4. output: thread (tx, ty) makes pixel pairs x = xb + 2*tx + 64*pp (+0, +1)
-  const int tx = tid & 31, ty = tid >> 5;
-  // columns past the frame edge reuse the last valid column's coordinates so that
-  // their (never stored) taps stay inside the staged box
-  const int xlast = min(kTileW, W - xb) - 1;
-  int ad[4], bd[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int xl = min(2 * tx + 64 * (p >> 1) + (p & 1), xlast);
-    ad[p] = s_adelta[xl];
-    bd[p] = s_bdelta[xl];
-  }
-  // one row loop per path (a path-uniform branch inside the loop would make the
-  // compiler drain the previous rows' stores with s_waitcnt vmcnt(0) every row)
-  if (VARIANT == 1 || VARIANT == 3)
-    output_rows<C, 1>(stile, box, S, Dst, H, W, xb, yb, tx, ty, ad, bd, s_X0, s_Y0);
-  else if (box.mode == 0 && VARIANT == 4)
-    output_rows<C, 0, true>(stile, box, S, Dst, H, W, xb, yb, tx, ty, ad, bd, s_X0, s_Y0);
-  else if (box.mode == 0)
-    output_rows<C, 0>(stile, box, S, Dst, H, W, xb, yb, tx, ty, ad, bd, s_X0, s_Y0);
-  else if (box.mode == 1)
-    output_rows<C, 1>(stile, box, S, Dst, H, W, xb, yb, tx, ty, ad, bd, s_X0, s_Y0);
-  else
-    output_rows<C, 2>(stile, box, S, Dst, H, W, xb, yb, tx, ty, ad, bd, s_X0, s_Y0);
+template <class Cfg>
+size_t warp_workspace_bytes(int n_frames, int H, int W) {
+  const size_t tiles = (size_t)ceil_div(W, kTileW) * ceil_div(H, Cfg::kTileH) * n_frames;
+  return tiles * sizeof(TilePlan) + (size_t)n_frames * 6 * sizeof(double);
+}
+
+// Plan + tile launches on `s`; ws holds warp_workspace_bytes<Cfg>(n_frames, H, W) bytes.
+template <int C, class Cfg = BlockCfg, int VARIANT = 0>
+void launch_warp(const uint16_t* src, uint16_t* dst, const double* M, int n_frames, int H, int W, int inverse_map,
+                 void* ws, hipStream_t s) {
+  const int ntx = ceil_div(W, kTileW), nty = ceil_div(H, Cfg::kTileH);
+  const long long tiles = (long long)ntx * nty * n_frames;
+  double* minv = static_cast<double*>(ws);
+  TilePlan* plan = reinterpret_cast<TilePlan*>(minv + 6 * (size_t)n_frames);
+  hipLaunchKernelGGL((warp_plan_kernel<C, Cfg>), dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, s, M, n_frames,
+                     H, W, inverse_map, ntx, nty, plan, minv);
+  hipLaunchKernelGGL((warp_affine_u16_kernel<C, Cfg, VARIANT>), dim3(ntx, nty, n_frames), dim3(kThreads), 0, s, src,
+                     dst, plan, minv, H, W);
 }
 
 }  // namespace
@@ -319,23 +443,25 @@ extern "C" int kcmc_warp_affine_u16(kcmc_ctx* ctx, const uint16_t* src, uint16_t
   if (!src || !dst || !M) return fail(KCMC_EINVAL, "kcmc_warp_affine_u16: NULL pointer");
   if (H > 32767 || W > 32767) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: H, W must be < 32768");
   if (n_frames > 65535) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: at most 65535 frames per call");
+  if (C != 1 && C != 3 && C != 4) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: C must be 1, 3 or 4");
   if (src == dst) return fail(KCMC_EINVAL, "kcmc_warp_affine_u16: in-place warp is not supported");
-  dim3 grid(ceil_div(W, kTileW), ceil_div(H, kTileH), n_frames);
-  if ((long long)grid.x * grid.y * grid.z >= (1ll << 31))
+  if ((long long)ceil_div(W, kTileW) * ceil_div(H, BlockCfg::kTileH) * n_frames >= (1ll << 31))
     return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: too many tiles in one call");
   hipStream_t s = (hipStream_t)stream;
+  void* ws = nullptr;
+  KCMC_TRY(workspace_alloc(ctx, &ws, warp_workspace_bytes<BlockCfg>(n_frames, H, W), s));
   switch (C) {
     case 1:
-      hipLaunchKernelGGL((warp_affine_u16_kernel<1>), grid, dim3(kThreads), 0, s, src, dst, M, H, W, inverse_map);
+      launch_warp<1>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
       break;
     case 3:
-      hipLaunchKernelGGL((warp_affine_u16_kernel<3>), grid, dim3(kThreads), 0, s, src, dst, M, H, W, inverse_map);
-      break;
-    case 4:
-      hipLaunchKernelGGL((warp_affine_u16_kernel<4>), grid, dim3(kThreads), 0, s, src, dst, M, H, W, inverse_map);
+      launch_warp<3>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
       break;
     default:
-      return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: C must be 1, 3 or 4");
+      launch_warp<4>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
+      break;
   }
-  return launch_check("warp_affine_u16_kernel");
+  const int rc = launch_check("warp_affine_u16_kernel");
+  KCMC_TRY(workspace_free(ctx, ws, s));
+  return rc;
 }

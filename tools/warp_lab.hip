@@ -11,6 +11,8 @@ void set_error(const std::string& m) { fprintf(stderr, "%s\n", m.c_str()); }
 int fail(int c, const std::string& m) { set_error(m); return c; }
 int hip_check(hipError_t e, const char* w) { if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", w, hipGetErrorString(e)); return KCMC_EHIP; } return 0; }
 int launch_check(const char* w) { return hip_check(hipGetLastError(), w); }
+int workspace_alloc(kcmc_ctx*, void**, size_t, hipStream_t) { return KCMC_EUNSUPPORTED; }
+int workspace_free(kcmc_ctx*, void*, hipStream_t) { return KCMC_EUNSUPPORTED; }
 }  // namespace kcmc
 #include "../keypoint-consensus-motion-correction_amd/csrc/warp.hip"
 
@@ -18,18 +20,35 @@ __global__ void copy_kernel(const uint4* __restrict__ a, uint4* __restrict__ b, 
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) b[i] = a[i];
 }
 
+__global__ void fill_kernel(uint16_t* a, size_t n, uint32_t dist) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    uint32_t v = h >> 16;
+    if (dist == 0) v &= 0x3fff;
+    if (dist == 1) v = (h & 1023) == 0 ? 60000 : (v & 0x1fff);
+    a[i] = (uint16_t)v;
+  }
+}
+
+__global__ void diff_kernel(const uint16_t* a, const uint16_t* b, size_t n, unsigned long long* cnt) {
+  unsigned long long c = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    c += a[i] != b[i];
+  if (c) atomicAdd(cnt, c);
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
-template <int V>
-float run(const uint16_t* src, uint16_t* dst, const double* M, int F, int H, int W, int reps) {
-  dim3 grid(kcmc::ceil_div(W, kTileW), kcmc::ceil_div(H, kTileH), F);
+template <class L>
+float timeit(L launch, int reps) {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  hipLaunchKernelGGL((warp_affine_u16_kernel<1, V>), grid, dim3(kThreads), 0, 0, src, dst, M, H, W, 0);
+  launch();
   hipEventRecord(a);
-  for (int r = 0; r < reps; ++r)
-    hipLaunchKernelGGL((warp_affine_u16_kernel<1, V>), grid, dim3(kThreads), 0, 0, src, dst, M, H, W, 0);
+  for (int r = 0; r < reps; ++r) launch();
   hipEventRecord(b);
   hipEventSynchronize(b);
   float ms;
@@ -40,11 +59,13 @@ float run(const uint16_t* src, uint16_t* dst, const double* M, int F, int H, int
 int main(int argc, char** argv) {
   const int F = argc > 1 ? atoi(argv[1]) : 2000, H = 1080, W = 1920, reps = 5;
   const size_t n = (size_t)F * H * W;
-  uint16_t *src, *dst;
+  uint16_t *src, *dst, *dst2;
   double* M;
+  unsigned long long* cnt;
   CK(hipMalloc(&src, n * 2));
   CK(hipMalloc(&dst, n * 2));
-  CK(hipMemset(src, 0x5a, n * 2));
+  CK(hipMalloc(&dst2, n * 2));
+  CK(hipMalloc(&cnt, 8));
   std::vector<double> hm((size_t)F * 6);
   for (int f = 0; f < F; ++f) {
     double th = 0.008 * std::sin(f * 0.7), c = std::cos(th), s = std::sin(th);
@@ -54,24 +75,45 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&M, hm.size() * 8));
   CK(hipMemcpy(M, hm.data(), hm.size() * 8, hipMemcpyHostToDevice));
   const double gb = 2.0 * n * 2 / 1e9;
-  const char* names[] = {"full", "no-compute(zeros after staging)", "no-staging-loads", "stores-only",
-                         "aligned-u16-taps"};
-  float t[5] = {run<0>(src, dst, M, F, H, W, reps), run<1>(src, dst, M, F, H, W, reps),
-                run<2>(src, dst, M, F, H, W, reps), run<3>(src, dst, M, F, H, W, reps),
-                run<4>(src, dst, M, F, H, W, reps)};
-  for (int v = 0; v < 5; ++v) printf("%-34s %8.3f ms  %7.1f GB/s (algorithmic r+w)\n", names[v], t[v], gb / (t[v] * 1e-3));
-  // plain copy of the same bytes: the HBM reference point on this box
-  hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
-  hipLaunchKernelGGL(copy_kernel, dim3(8192), dim3(256), 0, 0, (const uint4*)src, (uint4*)dst, n / 8);
-  hipEventRecord(a);
-  for (int r = 0; r < reps; ++r)
-    hipLaunchKernelGGL(copy_kernel, dim3(8192), dim3(256), 0, 0, (const uint4*)src, (uint4*)dst, n / 8);
-  hipEventRecord(b);
-  hipEventSynchronize(b);
-  float ms;
-  hipEventElapsedTime(&ms, a, b);
-  printf("%-34s %8.3f ms  %7.1f GB/s\n", "uint4 copy", ms / reps, gb / (ms / reps * 1e-3));
+  auto report = [&](const char* name, float ms) {
+    printf("%-44s %8.3f ms  %7.1f GB/s (algorithmic r+w)\n", name, ms, gb / (ms * 1e-3));
+  };
+  auto check = [&]() -> unsigned long long {
+    (void)hipMemset(cnt, 0, 8);
+    hipLaunchKernelGGL(diff_kernel, dim3(4096), dim3(256), 0, 0, dst, dst2, n, cnt);
+    unsigned long long h = 0;
+    (void)hipMemcpy(&h, cnt, 8, hipMemcpyDeviceToHost);
+    return h;
+  };
+  void* ws;
+  CK(hipMalloc(&ws, warp_workspace_bytes<WarpCfg<32, 8192, 6>>(F, H, W)));  // the most tiles
+  using C32 = WarpCfg<32, 8192, 6>;
+  using C40 = WarpCfg<40, 8192, 7>;
+  using C48 = WarpCfg<48, 9216, 8>;
+  using C56 = WarpCfg<56, 10240, 9>;
+  using C64 = WarpCfg<64, 12288, 10>;
+  // source values: 14-bit (exact integer blend everywhere), 13-bit with 0.1% hot pixels
+  // (sparse float-faithful fallback, like the bench texture), full 16-bit (fallback in
+  // nearly every row)
+  for (int dist = 0; dist < 3; ++dist) {
+    static const char* dn[] = {"14-bit", "13-bit + 0.1% hot pixels", "16-bit"};
+    printf("-- source values: %s\n", dn[dist]);
+    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0, src, n, (uint32_t)dist);
+    report("128x64 (box 24 KB)", timeit([&] { launch_warp<1, C64, 0>(src, dst, M, F, H, W, 0, ws, 0); }, reps));
+    report("128x64: no-compute (zeros)", timeit([&] { launch_warp<1, C64, 1>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+    report("128x64: no staging loads", timeit([&] { launch_warp<1, C64, 2>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+    report("128x32 (box 16 KB)", timeit([&] { launch_warp<1, C32, 0>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+    printf("    mismatches vs 128x64: %llu\n", check());
+    report("128x40 (box 16 KB)", timeit([&] { launch_warp<1, C40, 0>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+    printf("    mismatches vs 128x64: %llu\n", check());
+    report("128x48 (box 18 KB)", timeit([&] { launch_warp<1, C48, 0>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+    printf("    mismatches vs 128x64: %llu\n", check());
+    report("128x48: no staging loads", timeit([&] { launch_warp<1, C48, 2>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+    report("128x56 (box 20 KB)", timeit([&] { launch_warp<1, C56, 0>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+    printf("    mismatches vs 128x64: %llu\n", check());
+  }
+  report("uint4 copy", timeit([&] {
+    hipLaunchKernelGGL(copy_kernel, dim3(8192), dim3(256), 0, 0, (const uint4*)src, (uint4*)dst2, n / 8); }, reps));
+  CK(hipDeviceSynchronize());
   return 0;
 }
