@@ -21,7 +21,7 @@ class AlignmentError(BaseException):
 
 def process_affines(affines_sample: Sequence[np.ndarray], frame_downsample_rate: int) -> Tuple[np.ndarray, List[int]]:
     """VA:326-345: stack, record NaN sample frames, NaN-pad the temporally skipped frames."""
-    a = np.stack(affines_sample)
+    a = affines_sample if isinstance(affines_sample, np.ndarray) else np.stack(affines_sample)
     rate = int(frame_downsample_rate)
     skipped = [int(i) * rate for i in np.flatnonzero(np.isnan(a).reshape(len(a), -1).any(axis=1))]
     out = np.full((len(a) * rate,) + a.shape[1:], np.nan, dtype=np.result_type(a.dtype, np.float64))
@@ -65,12 +65,12 @@ def interpolate_affines(affines: np.ndarray) -> Tuple[np.ndarray, List[int]]:
     if first > 0:  # extrapolate leading frames (VA:383-387)
         aff[:first] = aff[first]
         interpolated += list(range(first))
-    for lo, hi in zip(present[:-1], present[1:]):  # interior gaps (VA:389-395)
-        lo, hi = int(lo), int(hi)
-        if hi - lo > 1:
-            xs = np.arange(lo + 1, hi)
-            aff[lo + 1 : hi] = _lerp_gap(aff[lo], aff[hi], lo, hi, xs)
-            interpolated += list(range(lo + 1, hi))
+    gaps = np.flatnonzero(np.diff(present) > 1)
+    for g in gaps:  # interior gaps (VA:389-395)
+        lo, hi = int(present[g]), int(present[g + 1])
+        xs = np.arange(lo + 1, hi)
+        aff[lo + 1 : hi] = _lerp_gap(aff[lo], aff[hi], lo, hi, xs)
+        interpolated += list(range(lo + 1, hi))
     last = int(present[-1])
     if last < n - 1:  # extrapolate trailing frames (VA:397-400: reported range is empty)
         aff[last + 1 :] = aff[last]

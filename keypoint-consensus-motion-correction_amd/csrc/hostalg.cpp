@@ -6,6 +6,7 @@
 //     iteration order of CPython `set` objects (VA:214, VA:248, VA:274) and whose
 //     selection is Counter.most_common (stable by first occurrence).
 #include <algorithm>
+#include <array>
 #include <cstdint>
 #include <cstring>
 #include <numeric>
@@ -98,6 +99,26 @@ class PySet {
   PySet() : table_(8, kEmpty), mask_(7), fill_(0), used_(0) {}
 
   size_t size() const { return used_; }
+
+  // Table sizes after m = 0..max_m insertions of distinct keys into an empty set (no
+  // deletions): the same fill/resize rule as store().
+  static std::vector<size_t> table_sizes(size_t max_m) {
+    std::vector<size_t> out(max_m + 1);
+    size_t mask = 7, fill = 0;
+    out[0] = 8;
+    for (size_t used = 1; used <= max_m; ++used) {
+      ++fill;
+      if (fill * 5 >= mask * 3) {
+        const size_t minused = used > 50000 ? used * 2 : used * 4;
+        size_t newsize = 8;
+        while (newsize <= minused) newsize <<= 1;
+        mask = newsize - 1;
+        fill = used;
+      }
+      out[used] = mask + 1;
+    }
+    return out;
+  }
 
   void add(int64_t key) {
     size_t mask = mask_;
@@ -237,15 +258,37 @@ extern "C" int kcmc_consensus(const uint32_t* keep_bits, int n_frames, int n_tpl
   // Counter([x for s in kp_idxs_list for x in s]) (VA:239): vote counts, and the
   // first-occurrence order (dict insertion order) -- a frame's set iteration order only
   // matters for the elements it contributes first, so only those frames are replayed.
-  std::vector<int32_t> count((size_t)n_tpl, 0);
+  // Vertical counting in byte lanes: spread[byte] holds the byte's 8 bits as 8 bytes of
+  // 0/1, so one 64-bit add counts 8 template indices; flushed every 255 frames.
+  static const std::array<uint64_t, 256> spread = [] {
+    std::array<uint64_t, 256> t{};
+    for (int v = 0; v < 256; ++v)
+      for (int b = 0; b < 8; ++b) t[(size_t)v] |= (uint64_t)((v >> b) & 1) << (8 * b);
+    return t;
+  }();
+  std::vector<int32_t> count((size_t)words * 32, 0);
   std::vector<uint32_t> seen((size_t)words, 0u), any((size_t)words, 0u);
+  std::vector<uint64_t> acc((size_t)words * 4, 0);
+  auto flush = [&] {
+    for (size_t q = 0; q < acc.size(); ++q) {
+      for (int b = 0; b < 8; ++b) count[8 * q + (size_t)b] += (int32_t)((acc[q] >> (8 * b)) & 0xff);
+      acc[q] = 0;
+    }
+  };
   for (int f = 0; f < n_frames; ++f) {
     const uint32_t* w = frame_bits(f);
     for (int k = 0; k < words; ++k) {
-      any[(size_t)k] |= w[k];
-      for (uint32_t b = w[k]; b; b &= b - 1) ++count[(size_t)(32 * k + __builtin_ctz(b))];
+      const uint32_t wk = w[k];
+      any[(size_t)k] |= wk;
+      uint64_t* a = acc.data() + 4 * (size_t)k;
+      a[0] += spread[wk & 0xff];
+      a[1] += spread[(wk >> 8) & 0xff];
+      a[2] += spread[(wk >> 16) & 0xff];
+      a[3] += spread[wk >> 24];
     }
+    if (f % 255 == 254) flush();
   }
+  flush();
   size_t remaining = 0;
   for (int k = 0; k < words; ++k) remaining += (size_t)__builtin_popcount(any[(size_t)k]);
   std::vector<int32_t> order;
@@ -289,8 +332,35 @@ extern "C" int kcmc_consensus(const uint32_t* keep_bits, int n_frames, int n_tpl
   // list(consensus_idxs.intersection(kp_idxs_list[i])) (VA:274): set_intersection
   // iterates the smaller set (the frame's when len(frame) <= len(consensus)) and
   // inserts the hits into a fresh set, whose iteration order is the result.
+  //
+  // Shortcut: without deletions a set's table size after m insertions depends on m
+  // only (table_size_after), and when every key is below that size each key sits in
+  // its own home slot (hash(i) = i), so the iteration order is ascending whatever the
+  // insertion and resize history.  Only frames whose result keeps a key >= its final
+  // table size replay the insertions.
+  const std::vector<size_t> tsize = PySet::table_sizes((size_t)nc);
   std::vector<std::vector<int32_t>> lists((size_t)n_frames);
-  parallel_for(n_frames, [&](int f) {
+  std::vector<int> replay;
+  for (int f = 0; f < n_frames; ++f) {
+    const uint32_t* w = frame_bits(f);
+    size_t m = 0;
+    int top = -1;
+    for (int k = 0; k < words; ++k) {
+      const uint32_t hit = w[k] & cons_bits[(size_t)k];
+      m += (size_t)__builtin_popcount(hit);
+      if (hit) top = 32 * k + 31 - __builtin_clz(hit);
+    }
+    if (top >= 0 && (size_t)top >= tsize[m]) {
+      replay.push_back(f);
+      continue;
+    }
+    auto& L = lists[(size_t)f];
+    L.reserve(m);
+    for (int k = 0; k < words; ++k)
+      for (uint32_t b = w[k] & cons_bits[(size_t)k]; b; b &= b - 1) L.push_back(32 * k + __builtin_ctz(b));
+  }
+  parallel_for((int)replay.size(), [&](int r) {
+    const int f = replay[(size_t)r];
     const uint32_t* w = frame_bits(f);
     size_t len = 0;
     for (int k = 0; k < words; ++k) len += (size_t)__builtin_popcount(w[k]);

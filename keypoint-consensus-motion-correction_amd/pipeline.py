@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import logging
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import Callable, List, Optional
 
 import numpy as np
 import torch
@@ -114,7 +114,7 @@ def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.C
 
 def postprocess_affines(params_host: np.ndarray, cfg: AlignConfig):
     """VA:143-145 on the host: NaN-pad, interpolate, Euclidean summary."""
-    affines, skipped = _aff.process_affines(list(params_host), cfg.frame_downsample_rate)
+    affines, skipped = _aff.process_affines(np.asarray(params_host), cfg.frame_downsample_rate)
     affines, interpolated = _aff.interpolate_affines(affines)
     return affines, skipped, interpolated, _aff.euclidean_transforms(affines)
 
@@ -144,3 +144,89 @@ def align_slab(inp: SlabInputs, cfg: AlignConfig, logger: Optional[logging.Logge
     return SlabResult(aligned, affines, eu, skipped, interpolated,
                       match if keep_intermediates else None, cons if keep_intermediates else None,
                       rr if keep_intermediates else None, counts)
+
+
+class OverlappedSlabs:
+    """Streams slabs through the hot path with the warp of slab k overlapping the rest
+    of slab k+1.
+
+    Match, consensus and RANSAC run on an analysis stream, the warp on a warp stream;
+    the host waits only for the analysis stream (survivor bitmasks, affines), so the
+    host steps (consensus, affine post-processing) and the small GPU stages of the next
+    slab proceed while the previous slab's frames are being warped.  Every slab still
+    runs every stage and its results equal ``align_slab``'s.
+
+    With ``counts`` (frames per rank) the slabs are one rank's share of a frame-sharded
+    job (distributed.align_sharded's exchanges on the analysis stream).
+
+        ov = OverlappedSlabs(device, cfg)
+        for inp in slabs:
+            res, done = ov.submit(inp)     # done: event on the warp stream
+        ov.synchronize()
+    """
+
+    def __init__(self, device, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
+                 counts: Optional[List[int]] = None, group=None):
+        self.dev = torch.device(device)
+        self.cfg = cfg
+        self.logger = logger
+        self.counts = counts
+        self.group = group
+        self.analysis = torch.cuda.Stream(self.dev)
+        self.warp = torch.cuda.Stream(self.dev)
+
+    def submit(self, inp: SlabInputs, out: Optional[torch.Tensor] = None,
+               mark: Optional[Callable[[str], None]] = None):
+        mark = mark or (lambda name: None)
+        cfg = self.cfg
+        cur = torch.cuda.current_stream(self.dev)
+        self.analysis.wait_stream(cur)
+        self.warp.wait_stream(cur)
+        n_tpl = inp.des_tpl.shape[0]
+        n_local = inp.q_off.numel() - 1
+        with torch.cuda.stream(self.analysis):
+            mark("m0")
+            match = match_stage(inp, cfg)
+            mark("m1")
+            if self.counts is not None and len(self.counts) > 1:
+                from .distributed import _all_gather_rows
+                import torch.distributed as dist
+
+                rank = dist.get_rank(self.group)
+                keep = _all_gather_rows(match.keep_bits, self.counts, self.group).cpu().numpy()
+                cons = consensus_stage(keep, n_tpl, sum(self.counts), cfg, self.logger if rank == 0 else None)
+                f0 = sum(self.counts[:rank])
+                po = cons.pt_off
+                lo, hi = int(po[f0]), int(po[f0 + n_local])
+                local = stages.Consensus(cons.order, cons.votes, (po[f0:f0 + n_local + 1] - lo).astype(np.int32),
+                                         cons.pt_idx[lo:hi])
+                mark("r0")
+                rr = ransac_stage(match, inp.kp_tpl, local, cfg)
+                mark("r1")
+                params = _all_gather_rows(rr.params, self.counts, self.group).cpu().numpy()
+            else:
+                f0 = 0
+                keep = match.keep_bits.cpu().numpy()
+                cons = consensus_stage(keep, n_tpl, n_local, cfg, self.logger)
+                mark("r0")
+                rr = ransac_stage(match, inp.kp_tpl, cons, cfg)
+                mark("r1")
+                params = rr.params.cpu().numpy()
+        affines, skipped, interpolated, eu = postprocess_affines(params, cfg)
+        with torch.cuda.stream(self.warp):
+            if out is not None:
+                out.record_stream(self.warp)
+            inp.frames.record_stream(self.warp)
+            # pinned + non_blocking: a pageable copy could wait for the warp stream to drain
+            a = torch.from_numpy(np.ascontiguousarray(affines[f0:f0 + inp.frames.shape[0]], dtype=np.float64))
+            a = a.pin_memory().to(self.dev, non_blocking=True)
+            mark("w0")
+            aligned = stages.warp_affine_u16(inp.frames, a, out=out)
+            mark("w1")
+            done = torch.cuda.Event()
+            done.record(self.warp)
+        return SlabResult(aligned, affines, eu, skipped, interpolated, consensus=cons, ransac=rr), done
+
+    def synchronize(self) -> None:
+        self.analysis.synchronize()
+        self.warp.synchronize()
