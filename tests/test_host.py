@@ -67,6 +67,24 @@ def test_native_consensus_many_ties():
     _check_consensus([set([999, 64, 65, 3, 1029 % 1000])], 1000, 5)
 
 
+def test_native_consensus_sorted_order_shortcut_boundaries():
+    # per-frame results whose final set table is / is not larger than their largest key
+    # (the native code lists the former in ascending order and replays the latter):
+    # intersection sizes around the 128 -> 512 table growth (76 / 77 elements), small
+    # sets of small keys, and sets with keys just above / below the table size
+    rng = np.random.default_rng(3)
+    n_tpl = 600
+    common = list(range(0, 600, 4))  # 150 keys seen in every frame -> the consensus
+    sets = [set(common)]
+    for m in (1, 2, 5, 19, 20, 76, 77, 78, 120, 150):
+        # built from ascending lists, like VA:214
+        sets.append(set(sorted(rng.choice(common, m, replace=False).tolist())))
+    sets += [set([0, 4, 8]), set([4, 28]), set([0, 32]), set([124, 128]), set([508, 512, 516])]
+    sets += [set(common[:76]), set(common[-76:]), set(common[:77]), set(common[-77:])]
+    _check_consensus(sets, n_tpl, 150)
+    _check_consensus(sets, n_tpl, 40)
+
+
 def test_native_consensus_too_few_raises():
     with pytest.raises(VideoAligner.AlignmentError):
         stages.consensus(_bits([{1, 2}, {2, 3}], 10), 10, 10, 5)
