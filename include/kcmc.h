@@ -144,6 +144,36 @@ int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src_dev, const double* dst_de
                       uint8_t* out_inliers_dev, int32_t* out_n_inliers_dev,
                       int32_t* out_best_trial_dev, kcmc_stream_t stream);
 
+/* ------------------------------------------------- K2 extension: affine / projective
+ * The reference only fits EuclideanTransform (VA:311).  BASELINE configs 3-5 need the
+ * other scikit-image 0.18.3 models through the same ransac call (fit.py:621-881):
+ *   KCMC_MODEL_AFFINE      ransac(..., AffineTransform,     min_samples=3, ...)
+ *   KCMC_MODEL_PROJECTIVE  ransac(..., ProjectiveTransform, min_samples=4, ...)
+ * with the same seeded sample stream (RandomState(seed).choice(N, min_samples, False)
+ * per trial) and skimage's total-least-squares refit on the inliers
+ * (_geometric.py:596-703). */
+enum { KCMC_MODEL_EUCLIDEAN = 0, KCMC_MODEL_AFFINE = 1, KCMC_MODEL_PROJECTIVE = 2 };
+
+/* kcmc_ransac_prepare for min_samples in {2, 3, 4} (2 is kcmc_ransac_prepare itself).
+ * Every point count must exceed min_samples (skimage raises otherwise, fit.py:798). */
+int kcmc_ransac_prepare_samples(kcmc_ctx* ctx, int min_samples, const int32_t* n_values_host, int count,
+                                int trials, uint32_t seed);
+
+/* Batched affine / projective RANSAC (model = KCMC_MODEL_AFFINE or _PROJECTIVE); points,
+ * pt_idx/pt_off/src_frame_stride, outputs and NaN conventions as kcmc_ransac_rigid,
+ * except:
+ *   out_params_dev [n_frames, 3, 3] f64  model.params (affine: last row 0 0 1), scaled for
+ *                                         spatial downsampling as S H S^-1, S = diag(r, r, 1)
+ *                                         (affine: translation * r, like VA:320)
+ * Frames with N_f < max(n_skip, min_samples + 1) get NaN.  Tables for every other N_f
+ * must have been prepared with kcmc_ransac_prepare_samples(ctx, min_samples, ...). */
+int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src_dev, const double* dst_dev,
+                      const int32_t* pt_idx_dev, const int32_t* pt_off_dev, int src_frame_stride,
+                      int n_frames, int max_n, int trials, double residual_threshold,
+                      double spatial_rate, int n_skip, double* out_params_dev,
+                      uint8_t* out_inliers_dev, int32_t* out_n_inliers_dev,
+                      int32_t* out_best_trial_dev, kcmc_stream_t stream);
+
 /* ------------------------------------------------------------------ K3: warp
  * cv2.warpAffine(frame, M_f, (W, H), flags=INTER_LINEAR [| WARP_INVERSE_MAP]) for
  * every frame: src_dev/dst_dev [n_frames, H, W, C] u16 (C interleaved, C=1 for the
@@ -154,6 +184,16 @@ int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src_dev, const double* dst_de
 int kcmc_warp_affine_u16(kcmc_ctx* ctx, const uint16_t* src_dev, uint16_t* dst_dev,
                          const double* M_dev, int n_frames, int H, int W, int C, int inverse_map,
                          kcmc_stream_t stream);
+
+/* cv2.warpPerspective(frame, M_f, (W, H), flags=INTER_LINEAR [| WARP_INVERSE_MAP]) for
+ * every frame -- the warp of the homography extension (BASELINE config 5; the
+ * reference's own warp is warpAffine, VA:458).  M_dev [n_frames, 3, 3] f64 forward maps,
+ * inverted like cv::invert (closed-form 3x3) unless inverse_map != 0; classic
+ * WarpPerspectiveInvoker fixed-point coordinates (per-block double evaluation, 1/32 px)
+ * and the remapBilinear blend of kcmc_warp_affine_u16; out-of-image taps read 0. */
+int kcmc_warp_perspective_u16(kcmc_ctx* ctx, const uint16_t* src_dev, uint16_t* dst_dev,
+                              const double* M_dev, int n_frames, int H, int W, int C, int inverse_map,
+                              kcmc_stream_t stream);
 
 #ifdef __cplusplus
 }

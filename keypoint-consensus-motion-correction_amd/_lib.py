@@ -32,8 +32,17 @@ EXPORTED_SYMBOLS = (
     "kcmc_hypothesis_table",
     "kcmc_ransac_prepare",
     "kcmc_ransac_rigid",
+    "kcmc_ransac_prepare_samples",
+    "kcmc_ransac_model",
     "kcmc_warp_affine_u16",
+    "kcmc_warp_perspective_u16",
 )
+
+KCMC_MODEL_EUCLIDEAN = 0
+KCMC_MODEL_AFFINE = 1
+KCMC_MODEL_PROJECTIVE = 2
+MODEL_IDS = {"euclidean": KCMC_MODEL_EUCLIDEAN, "affine": KCMC_MODEL_AFFINE, "projective": KCMC_MODEL_PROJECTIVE}
+MODEL_MIN_SAMPLES = {"euclidean": 2, "affine": 3, "projective": 4}
 
 
 class KcmcLibraryError(RuntimeError):
@@ -66,7 +75,10 @@ _SIGNATURES = {
     "kcmc_hypothesis_table": ([I, I, U32, I, P], I),
     "kcmc_ransac_prepare": ([P, P, I, I, U32], I),
     "kcmc_ransac_rigid": ([P, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, P], I),
+    "kcmc_ransac_prepare_samples": ([P, I, P, I, I, U32], I),
+    "kcmc_ransac_model": ([P, I, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, P], I),
     "kcmc_warp_affine_u16": ([P, P, P, P, I, I, I, I, I, P], I),
+    "kcmc_warp_perspective_u16": ([P, P, P, P, I, I, I, I, I, P], I),
 }
 
 

@@ -17,8 +17,8 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 REPO = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libkcmc.so")
 OFFLOAD_ARCH = os.environ.get("KCMC_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["capi.cpp", "hostalg.cpp", "match.hip", "ransac.hip", "warp.hip"]
-HEADERS = ["kcmc_internal.h", os.path.join("..", "..", "include", "kcmc.h")]
+SOURCES = ["capi.cpp", "hostalg.cpp", "match.hip", "ransac.hip", "ransac_model.hip", "warp.hip"]
+HEADERS = ["kcmc_internal.h", "ransac_common.h", os.path.join("..", "..", "include", "kcmc.h")]
 
 COMMON_FLAGS = [
     f"--offload-arch={OFFLOAD_ARCH}",

@@ -50,13 +50,24 @@ extern "C" int kcmc_create(int device, kcmc_ctx** out) {
   return KCMC_OK;
 }
 
+static void free_model_tables(HypTables& t) {
+  if (t.dev) hipFree(t.dev);
+  if (t.off) hipFree(t.off);
+  t.dev = nullptr;
+  t.off = nullptr;
+  t.off_len = 0;
+}
+
 extern "C" int kcmc_destroy(kcmc_ctx* ctx) {
   if (!ctx) return KCMC_OK;
-  if (ctx->hyp || ctx->hyp_off || ctx->ws_pool) {
+  bool any_model = false;
+  for (const auto& t : ctx->mhyp) any_model = any_model || t.dev || t.off;
+  if (ctx->hyp || ctx->hyp_off || ctx->ws_pool || any_model) {
     int prev = 0;
     hipGetDevice(&prev);
     hipSetDevice(ctx->device);
     free_tables(ctx);
+    for (auto& t : ctx->mhyp) free_model_tables(t);
     if (ctx->ws_pool) {
       hipDeviceSynchronize();  // pending stream-ordered frees return to the pool first
       hipMemPoolDestroy(ctx->ws_pool);
@@ -154,5 +165,72 @@ extern "C" int kcmc_ransac_prepare(kcmc_ctx* ctx, const int32_t* n_values, int c
     return rc;
   }
   ctx->hyp_off_len = off_len;
+  return KCMC_OK;
+}
+
+extern "C" int kcmc_ransac_prepare_samples(kcmc_ctx* ctx, int min_samples, const int32_t* n_values, int count,
+                                           int trials, uint32_t seed) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_ransac_prepare_samples: ctx is NULL");
+  if (min_samples == 2) return kcmc_ransac_prepare(ctx, n_values, count, trials, seed);
+  if (min_samples != 3 && min_samples != 4)
+    return fail(KCMC_EINVAL, "kcmc_ransac_prepare_samples: min_samples must be 2, 3 or 4");
+  if (count < 0 || (count > 0 && !n_values) || trials < 1)
+    return fail(KCMC_EINVAL, "kcmc_ransac_prepare_samples: bad arguments");
+  HypTables& T = ctx->mhyp[min_samples];
+  if (T.trials != trials || T.seed != seed) {
+    T.host.clear();
+    T.trials = trials;
+    T.seed = seed;
+  }
+  bool changed = T.dev == nullptr;
+  std::vector<int32_t> tab((size_t)trials * min_samples);
+  for (int k = 0; k < count; ++k) {
+    const int n = n_values[k];
+    if (n <= min_samples || n > 65535)
+      return fail(KCMC_EINVAL, "kcmc_ransac_prepare_samples: point counts must be in [min_samples + 1, 65535]");
+    if (T.host.count(n)) continue;
+    KCMC_TRY(hypothesis_table_impl(n, trials, seed, min_samples, tab.data()));
+    std::vector<uint64_t> packed((size_t)trials);
+    for (int t = 0; t < trials; ++t) {
+      uint64_t w = ~0ull;
+      for (int s = 0; s < min_samples; ++s) {
+        w &= ~(0xffffull << (16 * s));
+        w |= (uint64_t)(uint32_t)tab[(size_t)t * min_samples + s] << (16 * s);
+      }
+      packed[(size_t)t] = w;
+    }
+    T.host.emplace(n, std::move(packed));
+    changed = true;
+  }
+  if (!changed) return KCMC_OK;
+  const int off_len = T.host.empty() ? 1 : T.host.rbegin()->first + 1;
+  std::vector<int32_t> off((size_t)off_len, -1);
+  std::vector<uint64_t> all;
+  all.reserve(T.host.size() * (size_t)trials);
+  for (const auto& kv : T.host) {
+    off[(size_t)kv.first] = (int32_t)all.size();
+    all.insert(all.end(), kv.second.begin(), kv.second.end());
+  }
+  if (all.size() > (size_t)INT32_MAX) return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_prepare_samples: tables too large");
+  if (all.empty()) all.push_back(~0ull);
+  int prev = 0;
+  hipGetDevice(&prev);
+  KCMC_TRY(hip_check(hipSetDevice(ctx->device), "hipSetDevice"));
+  free_model_tables(T);
+  int rc = hip_check(hipMalloc(&T.dev, all.size() * sizeof(uint64_t)), "hipMalloc(model hyp)");
+  if (rc == KCMC_OK) rc = hip_check(hipMalloc(&T.off, off.size() * sizeof(int32_t)), "hipMalloc(model hyp_off)");
+  if (rc == KCMC_OK)
+    rc = hip_check(hipMemcpy(T.dev, all.data(), all.size() * sizeof(uint64_t), hipMemcpyHostToDevice),
+                   "hipMemcpy(model hyp)");
+  if (rc == KCMC_OK)
+    rc = hip_check(hipMemcpy(T.off, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice),
+                   "hipMemcpy(model hyp_off)");
+  hipSetDevice(prev);
+  if (rc != KCMC_OK) {
+    free_model_tables(T);
+    T.host.clear();
+    return rc;
+  }
+  T.off_len = off_len;
   return KCMC_OK;
 }

@@ -10,8 +10,21 @@
 
 #include "../../include/kcmc.h"
 
+// Hypothesis tables of the min_samples-point models (3: affine, 4: projective): per
+// point count n, `trials` samples packed as four 16-bit indices in a u64 (unused slots
+// 0xffff).  dev = all tables back to back, off[n] = start of n's table or -1.
+struct HypTables {
+  std::map<int, std::vector<uint64_t>> host;
+  uint64_t* dev = nullptr;
+  int32_t* off = nullptr;
+  int off_len = 0;
+  int trials = 0;
+  uint32_t seed = 0;
+};
+
 struct kcmc_ctx {
   int device = 0;
+  HypTables mhyp[5];  // indexed by min_samples (3 and 4 used)
   // RANSAC hypothesis tables, built on demand per point count n: `hyp_trials` packed
   // (i | j << 16) u32 samples per n.  Device: hyp (all tables back to back) and
   // hyp_off[n] = start of n's table in hyp, or -1 (n in [0, hyp_off_len)).

@@ -23,13 +23,12 @@
 #include <cmath>
 
 #include "kcmc_internal.h"
+#include "ransac_common.h"
 
 namespace kcmc {
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kMaxN = 4096;  // numpy's pairwise split tree has depth <= 6 for n <= 4096
-constexpr int kPwDepth = 6;
+using namespace ransac_common;
 
 struct Model {
   double c, s, tx, ty;
@@ -97,57 +96,8 @@ __device__ __forceinline__ double pw_leaf(const Model& m, const Pts& P, int star
   return res;
 }
 
-// For n > 128 numpy recurses: pairwise(a, n) = pairwise(a, n2) + pairwise(a + n2, n - n2)
-// with n2 = n/2 rounded down to a multiple of 8.  The split tree depends on N only, so
-// one thread writes it once per frame as a post-order plan: leaves in order, each with
-// the number of "pop b, pop a, push a+b" combines that follow it.  Every thread then
-// evaluates its hypotheses with one copy of the leaf loop and a per-thread stack in LDS.
-constexpr int kMaxLeaves = 128;
-constexpr int kMaxStack = kPwDepth + 2;
-
-struct Plan {
-  int16_t start[kMaxLeaves];
-  int16_t len[kMaxLeaves];
-  int8_t pops[kMaxLeaves];
-  int n;
-};
-
-template <int DEPTH>
-__device__ __forceinline__ void plan_gen(Plan& p, int s, int n) {
-  if (DEPTH == 0 || n <= 128) {
-    p.start[p.n] = (int16_t)s;
-    p.len[p.n] = (int16_t)n;
-    p.pops[p.n] = 0;
-    ++p.n;
-    return;
-  }
-  if constexpr (DEPTH > 0) {
-    int n2 = n / 2;
-    n2 -= n2 % 8;
-    plan_gen<DEPTH - 1>(p, s, n2);
-    plan_gen<DEPTH - 1>(p, s + n2, n - n2);
-    ++p.pops[p.n - 1];
-  }
-}
-
-// (count desc, S asc, t asc); invalid trials (NaN S, or 0 inliers with S = inf) never win.
-__device__ __forceinline__ bool better(int c, double S, int t, int bc, double bS, int bt) {
-  if (c != bc) return c > bc;
-  if (S != bS) return S < bS;
-  return t < bt;
-}
-
-__device__ double block_sum(double v, double* red) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  double s = 0.0;
-  for (int w = 0; w < kThreads / 64; ++w) s += red[w];
-  return s;
-}
-
+// For N > 128 the numpy pairwise order comes from the per-frame split Plan
+// (ransac_common.h); invalid trials (NaN S, or 0 inliers with S = inf) never win.
 // LARGE = false handles frames with N <= 128 (one pairwise leaf, fully in registers)
 // and the NaN frames; LARGE = true handles 128 < N <= kMaxN through the split plan.
 template <bool LARGE>

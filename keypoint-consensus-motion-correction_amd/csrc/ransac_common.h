@@ -1,0 +1,76 @@
+// Model-independent pieces of the batched RANSAC kernels (ransac.hip: rigid,
+// ransac_model.hip: affine / projective): launch shape, numpy's pairwise-summation
+// split plan, skimage's selection order and workgroup / wave sums.
+#pragma once
+
+#include <climits>
+#include <cstdint>
+
+#include "kcmc_internal.h"
+
+namespace kcmc {
+namespace ransac_common {
+
+constexpr int kThreads = 256;
+constexpr int kMaxN = 4096;  // numpy's pairwise split tree has depth <= 6 for n <= 4096
+constexpr int kPwDepth = 6;
+
+// For n > 128 numpy's pairwise_sum recurses: pairwise(a, n) = pairwise(a, n2) +
+// pairwise(a + n2, n - n2) with n2 = n/2 rounded down to a multiple of 8.  The split
+// tree depends on N only, so one thread writes it once per frame as a post-order plan:
+// leaves in order, each with the number of "pop b, pop a, push a+b" combines that
+// follow it.  Every thread then evaluates its hypotheses with one copy of the leaf
+// loop and a per-thread stack in LDS.
+constexpr int kMaxLeaves = 128;
+constexpr int kMaxStack = kPwDepth + 2;
+
+struct Plan {
+  int16_t start[kMaxLeaves];
+  int16_t len[kMaxLeaves];
+  int8_t pops[kMaxLeaves];
+  int n;
+};
+
+template <int DEPTH>
+__device__ __forceinline__ void plan_gen(Plan& p, int s, int n) {
+  if (DEPTH == 0 || n <= 128) {
+    p.start[p.n] = (int16_t)s;
+    p.len[p.n] = (int16_t)n;
+    p.pops[p.n] = 0;
+    ++p.n;
+    return;
+  }
+  if constexpr (DEPTH > 0) {
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    plan_gen<DEPTH - 1>(p, s, n2);
+    plan_gen<DEPTH - 1>(p, s + n2, n - n2);
+    ++p.pops[p.n - 1];
+  }
+}
+
+// skimage's selection order (fit.py:851-861): (count desc, S asc, trial asc).
+__device__ __forceinline__ bool better(int c, double S, int t, int bc, double bS, int bt) {
+  if (c != bc) return c > bc;
+  if (S != bS) return S < bS;
+  return t < bt;
+}
+
+__device__ inline double block_sum(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int w = 0; w < kThreads / 64; ++w) s += red[w];
+  return s;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+}  // namespace ransac_common
+}  // namespace kcmc

@@ -1,0 +1,761 @@
+// K2 extension: batched affine / projective RANSAC with scikit-image 0.18.3 semantics.
+//
+// The reference fits EuclideanTransform only (VA:311, kernel in ransac.hip).  BASELINE
+// configs 3-5 ask for affine and homography models; this file implements
+//   skimage.measure.ransac((src, dst), AffineTransform,     min_samples=3, ...)
+//   skimage.measure.ransac((src, dst), ProjectiveTransform, min_samples=4, ...)
+// (fit.py:621-881; _geometric.py:18-69, 548-562, 596-703, 746-845) with the seeded
+// hypothesis stream skimage draws: trial t uses the t-th
+// RandomState(seed).choice(N, k, replace=False) = the first k entries of the t-th
+// legacy MT19937 permutation of N (host tables per (k, N), kcmc_ransac_prepare_samples).
+//
+// ransac_model_score_kernel -- one workgroup per frame, the N point pairs in LDS, one
+//   thread per hypothesis:
+//   * minimal fit: affine = the exact 3-point solve (what skimage's total-least-squares
+//     SVD returns for a non-degenerate triple); projective = the 8x8 DLT system in
+//     Hartley-normalised coordinates with h22 = 1 (skimage's normalisation and scale),
+//     Gaussian elimination with partial pivoting, de-normalised like skimage;
+//   * skimage's degeneracy tests, where estimate() returns False and the trial is
+//     skipped (fit.py:835-838): a sample with rms 0 (ZeroDivisionError), a singular
+//     system, or np.isclose(V[-1,-1], 0) <=> 1/sqrt(1 + |h|^2) <= 1e-8 with h the model
+//     in normalised coordinates;
+//   * residuals as _apply_mat computes them ([x y 1] @ H^T in the dgemm operation
+//     order used for the rigid model; w == 0 -> eps; divide), inlier iff r < threshold,
+//     S = sum r^2 in numpy's pairwise order;
+//   * selection (count desc, S asc, trial asc) with skimage's S <= 0 early exit, then
+//     the winner's inlier mask and model.
+// ransac_model_refit_kernel -- one wave per frame: the final total-least-squares fit on
+//   the inliers (fit.py:871-875 -> ProjectiveTransform.estimate): Hartley
+//   normalisation, A^T A of the 2N x 7 (affine) / 2N x 9 (projective) system in fp64
+//   (its smallest eigenvector is the last right singular vector of A that skimage
+//   takes from np.linalg.svd), found by Cholesky inverse iteration, then
+//   H = inv(N_dst) Hn N_src.  As in skimage, a refit with |v_last| <= 1e-8 keeps the
+//   hypothesis model and rms == 0 gives NaN.
+// Output params [F, 3, 3] (row-major), NaN where skimage returns no model, scaled for
+// spatial downsampling as S H S^-1 with S = diag(rate, rate, 1) (for affine models
+// exactly the reference's translation scaling, VA:320).
+#include <cfloat>
+#include <cmath>
+
+#include "kcmc_internal.h"
+#include "ransac_common.h"
+
+namespace kcmc {
+namespace {
+
+using namespace ransac_common;
+
+constexpr double kSqrt2 = 1.4142135623730951;  // math.sqrt(2)
+
+struct HModel {
+  double h[9];
+  bool ok;
+};
+
+struct Pts {
+  const double* sx;
+  const double* sy;
+  const double* dx;
+  const double* dy;
+};
+
+// skimage _center_and_normalize_points for the K sample points: centroid = numpy's
+// sequential axis-0 mean, rms = sqrt(pairwise_sum of the 2K squared deviations / K)
+// (2K < 8: sequential; 2K == 8: numpy's 8-accumulator combine).  false: rms == 0.
+template <int K>
+__device__ __forceinline__ bool center_normalize(const double* px, const double* py, const int (&sel)[K], double& cx,
+                                                 double& cy, double& nf) {
+  double sx = 0.0, sy = 0.0;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    sx += px[sel[i]];
+    sy += py[sel[i]];
+  }
+  cx = sx / K;
+  cy = sy / K;
+  double dev[2 * K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const double ex = px[sel[i]] - cx, ey = py[sel[i]] - cy;
+    dev[2 * i] = ex * ex;
+    dev[2 * i + 1] = ey * ey;
+  }
+  double ss;
+  if constexpr (2 * K < 8) {
+    ss = 0.0;
+#pragma unroll
+    for (int i = 0; i < 2 * K; ++i) ss += dev[i];
+  } else {
+    ss = ((dev[0] + dev[1]) + (dev[2] + dev[3])) + ((dev[4] + dev[5]) + (dev[6] + dev[7]));
+  }
+  const double rms = sqrt(ss / K);
+  if (rms == 0.0) return false;
+  nf = kSqrt2 / rms;
+  return true;
+}
+
+// Affine model through 3 correspondences: L = [v1 v2][u1 u2]^-1 (u_k = s_k - s_0,
+// v_k = d_k - d_0), t = c_d - L c_s.
+__device__ __forceinline__ HModel affine_fit3(const Pts& P, const int (&sel)[3]) {
+  HModel m;
+  m.ok = false;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) m.h[k] = 0.0;
+  double csx, csy, nfs, cdx, cdy, nfd;
+  if (!center_normalize<3>(P.sx, P.sy, sel, csx, csy, nfs)) return m;
+  if (!center_normalize<3>(P.dx, P.dy, sel, cdx, cdy, nfd)) return m;
+  const double u1x = P.sx[sel[1]] - P.sx[sel[0]], u1y = P.sy[sel[1]] - P.sy[sel[0]];
+  const double u2x = P.sx[sel[2]] - P.sx[sel[0]], u2y = P.sy[sel[2]] - P.sy[sel[0]];
+  const double v1x = P.dx[sel[1]] - P.dx[sel[0]], v1y = P.dy[sel[1]] - P.dy[sel[0]];
+  const double v2x = P.dx[sel[2]] - P.dx[sel[0]], v2y = P.dy[sel[2]] - P.dy[sel[0]];
+  const double det = u1x * u2y - u2x * u1y;
+  if (det == 0.0) return m;
+  const double l00 = (v1x * u2y - v2x * u1y) / det;
+  const double l01 = (v2x * u1x - v1x * u2x) / det;
+  const double l10 = (v1y * u2y - v2y * u1y) / det;
+  const double l11 = (v2y * u1x - v1y * u2x) / det;
+  const double g = nfd / nfs;
+  const double hn2 = g * g * (((l00 * l00 + l01 * l01) + l10 * l10) + l11 * l11);
+  if (1.0 / sqrt(1.0 + hn2) <= 1e-8) return m;
+  m.h[0] = l00;
+  m.h[1] = l01;
+  m.h[2] = cdx - (l00 * csx + l01 * csy);
+  m.h[3] = l10;
+  m.h[4] = l11;
+  m.h[5] = cdy - (l10 * csx + l11 * csy);
+  m.h[8] = 1.0;
+  m.ok = true;
+  return m;
+}
+
+// H = inv(N_dst) Hn N_src with N = [[nf, 0, -nf c_x], [0, nf, -nf c_y], [0, 0, 1]] and
+// Hn = [[h0 h1 h2] [h3 h4 h5] [h6 h7 1]] (skimage _geometric.py:699).
+__device__ __forceinline__ void denormalize(const double (&h)[8], double csx, double csy, double nfs, double cdx,
+                                            double cdy, double nfd, double (&H)[9]) {
+  double T[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const double a = h[3 * r], b = h[3 * r + 1], c = (r == 2) ? 1.0 : h[(3 * r + 2) % 8];
+    T[3 * r] = a * nfs;
+    T[3 * r + 1] = b * nfs;
+    T[3 * r + 2] = c - (a * nfs * csx + b * nfs * csy);
+  }
+  const double id = 1.0 / nfd;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    H[k] = T[k] * id + cdx * T[6 + k];
+    H[3 + k] = T[3 + k] * id + cdy * T[6 + k];
+    H[6 + k] = T[6 + k];
+  }
+}
+
+// Projective model through 4 correspondences, in skimage's normalised coordinates:
+// rows = the four x-equations then the four y-equations of its A matrix,
+//   xs h0 + ys h1 + h2 - xd xs h6 - xd ys h7 = xd,  xs h3 + ys h4 + h5 - yd xs h6 - yd ys h7 = yd.
+__device__ __forceinline__ HModel projective_fit4(const Pts& P, const int (&sel)[4]) {
+  HModel m;
+  m.ok = false;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) m.h[k] = 0.0;
+  double csx, csy, nfs, cdx, cdy, nfd;
+  if (!center_normalize<4>(P.sx, P.sy, sel, csx, csy, nfs)) return m;
+  if (!center_normalize<4>(P.dx, P.dy, sel, cdx, cdy, nfd)) return m;
+  double M[8][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double xs = (P.sx[sel[i]] - csx) * nfs, ys = (P.sy[sel[i]] - csy) * nfs;
+    const double xd = (P.dx[sel[i]] - cdx) * nfd, yd = (P.dy[sel[i]] - cdy) * nfd;
+    M[i][0] = xs;
+    M[i][1] = ys;
+    M[i][2] = 1.0;
+    M[i][3] = 0.0;
+    M[i][4] = 0.0;
+    M[i][5] = 0.0;
+    M[i][6] = -(xd * xs);
+    M[i][7] = -(xd * ys);
+    M[i][8] = xd;
+    M[4 + i][0] = 0.0;
+    M[4 + i][1] = 0.0;
+    M[4 + i][2] = 0.0;
+    M[4 + i][3] = xs;
+    M[4 + i][4] = ys;
+    M[4 + i][5] = 1.0;
+    M[4 + i][6] = -(yd * xs);
+    M[4 + i][7] = -(yd * ys);
+    M[4 + i][8] = yd;
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    int piv = c;
+    double best = fabs(M[c][c]);
+#pragma unroll
+    for (int r = c + 1; r < 8; ++r) {
+      const double a = fabs(M[r][c]);
+      if (a > best) {
+        best = a;
+        piv = r;
+      }
+    }
+    if (best == 0.0) return m;
+#pragma unroll
+    for (int r = c + 1; r < 8; ++r) {
+      if (r == piv) {
+#pragma unroll
+        for (int k = c; k < 9; ++k) {
+          const double t = M[c][k];
+          M[c][k] = M[r][k];
+          M[r][k] = t;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = c + 1; r < 8; ++r) {
+      const double f = M[r][c] / M[c][c];
+#pragma unroll
+      for (int k = c; k < 9; ++k) M[r][k] -= f * M[c][k];
+    }
+  }
+  double h[8];
+#pragma unroll
+  for (int c = 7; c >= 0; --c) {
+    double v = M[c][8];
+#pragma unroll
+    for (int k = c + 1; k < 8; ++k) v -= M[c][k] * h[k];
+    h[c] = v / M[c][c];
+  }
+  double hn2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) hn2 += h[k] * h[k];
+  if (1.0 / sqrt(1.0 + hn2) <= 1e-8) return m;
+  denormalize(h, csx, csy, nfs, cdx, cdy, nfd, m.h);
+  m.ok = true;
+  return m;
+}
+
+template <int MODEL>
+__device__ __forceinline__ double resid2(const double (&h)[9], const Pts& P, int k, double thresh, int& cnt) {
+  const double x = P.sx[k], y = P.sy[k];
+  double X = fma(y, h[1], x * h[0]) + h[2];
+  double Y = fma(y, h[4], x * h[3]) + h[5];
+  if (MODEL == KCMC_MODEL_PROJECTIVE) {
+    double w = fma(y, h[7], x * h[6]) + h[8];
+    if (w == 0.0) w = DBL_EPSILON;
+    X = X / w;
+    Y = Y / w;
+  }
+  const double ex = X - P.dx[k], ey = Y - P.dy[k];
+  const double r = sqrt(ex * ex + ey * ey);
+  cnt += (r < thresh) ? 1 : 0;
+  return r * r;
+}
+
+template <int MODEL>
+__device__ __forceinline__ double pw_leaf(const double (&h)[9], const Pts& P, int start, int n, double thresh,
+                                          int& cnt) {
+  if (n < 8) {
+    double res = 0.0;
+    for (int i = 0; i < n; ++i) res += resid2<MODEL>(h, P, start + i, thresh, cnt);
+    return res;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = resid2<MODEL>(h, P, start + j, thresh, cnt);
+  int i = 8;
+  const int nfull = n - (n % 8);
+  for (; i < nfull; i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] += resid2<MODEL>(h, P, start + i + j, thresh, cnt);
+  }
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += resid2<MODEL>(h, P, start + i, thresh, cnt);
+  return res;
+}
+
+template <int MODEL>
+__device__ __forceinline__ HModel fit_trial(const Pts& P, uint64_t pr) {
+  if constexpr (MODEL == KCMC_MODEL_AFFINE) {
+    const int sel[3] = {(int)(pr & 0xffffu), (int)((pr >> 16) & 0xffffu), (int)((pr >> 32) & 0xffffu)};
+    return affine_fit3(P, sel);
+  } else {
+    const int sel[4] = {(int)(pr & 0xffffu), (int)((pr >> 16) & 0xffffu), (int)((pr >> 32) & 0xffffu),
+                        (int)((pr >> 48) & 0xffffu)};
+    return projective_fit4(P, sel);
+  }
+}
+
+__device__ __forceinline__ void gather_point(const double* __restrict__ src, const double* __restrict__ dst,
+                                             const int32_t* __restrict__ pt_idx, int src_stride, int f, int p,
+                                             double& x, double& y, double& u, double& v) {
+  size_t si, di;
+  if (pt_idx) {
+    const int q = pt_idx[p];
+    si = (size_t)f * src_stride + q;
+    di = (size_t)q;
+  } else {
+    si = di = (size_t)p;
+  }
+  x = src[2 * si];
+  y = src[2 * si + 1];
+  u = dst[2 * di];
+  v = dst[2 * di + 1];
+}
+
+// ---------------------------------------------------------------------- scoring
+// LARGE = false: frames with N <= 128 (one pairwise leaf) and the NaN frames;
+// LARGE = true: 128 < N <= kMaxN through the split plan.
+template <int MODEL, bool LARGE>
+__global__ __launch_bounds__(kThreads) void ransac_model_score_kernel(
+    const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
+    const int32_t* __restrict__ pt_off, int src_stride, const uint64_t* __restrict__ hyp,
+    const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, int n_skip,
+    double* __restrict__ out_params, double* __restrict__ best_model, uint8_t* __restrict__ out_inl,
+    int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
+  constexpr int K = MODEL == KCMC_MODEL_AFFINE ? 3 : 4;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int s_best[kThreads / 64 * 2];
+  __shared__ double s_bestS[kThreads / 64];
+  __shared__ int s_any_zero;
+  __shared__ int s_final_t;
+  __shared__ int s_final_c;
+  __shared__ Plan s_plan;
+
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int p0 = pt_off[f];
+  const int N = pt_off[f + 1] - p0;
+
+  const bool skip_frame = N < n_skip || N <= K || N > kMaxN;
+  const int hoff = (!skip_frame && N < hyp_off_len) ? hyp_off[N] : -1;
+  const bool nan_frame = skip_frame || hoff < 0;
+  if (LARGE != (!nan_frame && N > 128)) return;  // the other launch owns this frame
+  if (nan_frame) {
+    if (tid < 9) out_params[9 * (size_t)f + tid] = NAN;
+    for (int k = tid; k < N; k += kThreads) out_inl[p0 + k] = 0;
+    if (tid == 0) {
+      out_nin[f] = skip_frame ? 0 : -1;  // -1: no hypothesis table was prepared for N
+      out_best[f] = -1;
+    }
+    return;
+  }
+
+  // LDS: sx, sy, dx, dy [N] f64 | trial S [T] f64 | [LARGE: stack [kMaxStack][256] f64]
+  //      | trial count [T] i32
+  double* sx = smem;
+  double* sy = sx + N;
+  double* dxs = sy + N;
+  double* dys = dxs + N;
+  double* tS = dys + N;
+  double* stk = tS + T;
+  int* tC = reinterpret_cast<int*>(stk + (LARGE ? kMaxStack * kThreads : 0));
+  if (LARGE && tid == 0) {
+    s_plan.n = 0;
+    plan_gen<kPwDepth>(s_plan, 0, N);
+  }
+  for (int k = tid; k < N; k += kThreads)
+    gather_point(src, dst, pt_idx, src_stride, f, p0 + k, sx[k], sy[k], dxs[k], dys[k]);
+  if (tid == 0) s_any_zero = 0;
+  __syncthreads();
+
+  const Pts P{sx, sy, dxs, dys};
+  const uint64_t* H = hyp + hoff;
+  int bc = -1, bt = INT_MAX;
+  double bS = INFINITY;
+  bool any_zero = false;
+  for (int t = tid; t < T; t += kThreads) {
+    const HModel m = fit_trial<MODEL>(P, H[t]);
+    int cnt = 0;
+    double S = NAN;
+    if (m.ok) {
+      if (!LARGE) {
+        S = pw_leaf<MODEL>(m.h, P, 0, N, thresh, cnt);
+      } else {
+        int sp = 0;
+        for (int l = 0; l < s_plan.n; ++l) {
+          stk[sp++ * kThreads + tid] = pw_leaf<MODEL>(m.h, P, s_plan.start[l], s_plan.len[l], thresh, cnt);
+          for (int c = s_plan.pops[l]; c > 0; --c) {
+            const double b = stk[--sp * kThreads + tid];
+            const double a = stk[(sp - 1) * kThreads + tid];
+            stk[(sp - 1) * kThreads + tid] = a + b;
+          }
+        }
+        S = stk[tid];
+      }
+    }
+    tS[t] = S;
+    tC[t] = cnt;
+    // skipped trials (estimate() False) and NaN scores never win; with 0 inliers a
+    // trial wins only with S < inf (skimage's strict comparisons against (0, inf))
+    const bool valid = m.ok && !isnan(S) && (cnt > 0 || S < INFINITY);
+    if (valid) {
+      if (S <= 0.0) any_zero = true;
+      if (better(cnt, S, t, bc, bS, bt)) {
+        bc = cnt;
+        bS = S;
+        bt = t;
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const int oc = __shfl_xor(bc, o);
+    const double oS = __shfl_xor(bS, o);
+    const int ot = __shfl_xor(bt, o);
+    if (better(oc, oS, ot, bc, bS, bt)) {
+      bc = oc;
+      bS = oS;
+      bt = ot;
+    }
+  }
+  if (lane == 0) {
+    s_best[2 * wave] = bc;
+    s_best[2 * wave + 1] = bt;
+    s_bestS[wave] = bS;
+  }
+  if (any_zero) atomicOr(&s_any_zero, 1);
+  __syncthreads();
+  if (tid == 0) {
+    int fc = -1, ft = INT_MAX;
+    double fS = INFINITY;
+    for (int w = 0; w < kThreads / 64; ++w)
+      if (better(s_best[2 * w], s_bestS[w], s_best[2 * w + 1], fc, fS, ft)) {
+        fc = s_best[2 * w];
+        fS = s_bestS[w];
+        ft = s_best[2 * w + 1];
+      }
+    if (s_any_zero) {
+      // skimage stops as soon as the running best has S <= 0 (fit.py:862-869)
+      int c0 = 0, t0 = -1;
+      double S0 = INFINITY;
+      for (int t = 0; t < T; ++t) {
+        const double S = tS[t];
+        const int c = tC[t];
+        if (isnan(S)) continue;
+        if (c > c0 || (c == c0 && S < S0)) {
+          c0 = c;
+          S0 = S;
+          t0 = t;
+          if (S0 <= 0.0) break;
+        }
+      }
+      ft = t0 < 0 ? INT_MAX : t0;
+      fc = c0;
+    }
+    s_final_t = (ft == INT_MAX) ? -1 : ft;
+    s_final_c = (ft == INT_MAX) ? 0 : fc;
+  }
+  __syncthreads();
+  const int best_t = s_final_t;
+  const int best_c = s_final_c;
+
+  HModel bm;
+  bm.ok = false;
+  if (best_t >= 0) bm = fit_trial<MODEL>(P, H[best_t]);
+  const bool has_model = bm.ok && best_c > 0;
+  for (int k = tid; k < N; k += kThreads) {
+    int c = 0;
+    if (has_model) resid2<MODEL>(bm.h, P, k, thresh, c);
+    out_inl[p0 + k] = (uint8_t)c;
+  }
+  if (tid < 9) {
+    best_model[9 * (size_t)f + tid] = has_model ? bm.h[tid] : NAN;
+    if (!has_model) out_params[9 * (size_t)f + tid] = NAN;  // skimage: model None (fit.py:876-879)
+  }
+  if (tid == 0) {
+    out_nin[f] = has_model ? best_c : 0;
+    out_best[f] = best_t;
+  }
+}
+
+// ------------------------------------------------------------------------ refit
+// Smallest eigenvector of a symmetric positive semi-definite n x n matrix by inverse
+// iteration on its Cholesky factor (pivots floored at trace * 2^-52, a shift far below
+// the second-smallest eigenvalue of any non-degenerate point set).  Every lane of the
+// wave runs it on identical data, so the iteration count is wave-uniform.
+template <int n>
+__device__ __forceinline__ void smallest_eigvec(const double (&A)[n][n], double (&x)[n]) {
+  double L[n][n];
+  double dinv[n];
+  double tr = 0.0;
+#pragma unroll
+  for (int i = 0; i < n; ++i) tr += A[i][i];
+  const double floor_v = tr * 2.220446049250313e-16 + DBL_MIN;
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+    double d = A[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
+    if (!(d > floor_v)) d = floor_v;
+    const double ljj = sqrt(d);
+    L[j][j] = ljj;
+    dinv[j] = 1.0 / ljj;
+#pragma unroll
+    for (int i = j + 1; i < n; ++i) {
+      double a = A[i][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) a -= L[i][k] * L[j][k];
+      L[i][j] = a * dinv[j];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < n; ++i) x[i] = 1.0;
+  for (int it = 0; it < 200; ++it) {
+    double y[n], z[n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      double a = x[i];
+#pragma unroll
+      for (int k = 0; k < i; ++k) a -= L[i][k] * y[k];
+      y[i] = a * dinv[i];
+    }
+#pragma unroll
+    for (int i = n - 1; i >= 0; --i) {
+      double a = y[i];
+#pragma unroll
+      for (int k = i + 1; k < n; ++k) a -= L[k][i] * z[k];
+      z[i] = a * dinv[i];
+    }
+    double nn = 0.0, dot = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      nn += z[i] * z[i];
+      dot += z[i] * x[i];
+    }
+    const double s = (dot < 0.0 ? -1.0 : 1.0) / sqrt(nn);
+    double diff = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const double v = z[i] * s;
+      diff = fmax(diff, fabs(v - x[i]));
+      x[i] = v;
+    }
+    if (it > 0 && diff < 1e-15) break;
+  }
+}
+
+template <int MODEL>
+__global__ __launch_bounds__(256) void ransac_model_refit_kernel(
+    const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
+    const int32_t* __restrict__ pt_off, int src_stride, const uint8_t* __restrict__ inl,
+    const int32_t* __restrict__ nin, const double* __restrict__ best_model, int n_frames, double rate,
+    double* __restrict__ out_params) {
+  constexpr int n = MODEL == KCMC_MODEL_AFFINE ? 7 : 9;
+  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (f >= n_frames || nin[f] <= 0) return;  // NaN params already written by the scoring kernel
+  const int p0 = pt_off[f], N = pt_off[f + 1] - p0;
+  double* o = out_params + 9 * (size_t)f;
+
+  // centroids (np.mean(points, axis=0) of the inliers)
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, sc = 0.0;
+  for (int k = lane; k < N; k += 64)
+    if (inl[p0 + k]) {
+      double x, y, u, v;
+      gather_point(src, dst, pt_idx, src_stride, f, p0 + k, x, y, u, v);
+      s0 += x;
+      s1 += y;
+      s2 += u;
+      s3 += v;
+      sc += 1.0;
+    }
+  const double cnt = wave_sum(sc);
+  const double csx = wave_sum(s0) / cnt, csy = wave_sum(s1) / cnt;
+  const double cdx = wave_sum(s2) / cnt, cdy = wave_sum(s3) / cnt;
+  double q0 = 0.0, q1 = 0.0;
+  for (int k = lane; k < N; k += 64)
+    if (inl[p0 + k]) {
+      double x, y, u, v;
+      gather_point(src, dst, pt_idx, src_stride, f, p0 + k, x, y, u, v);
+      q0 += (x - csx) * (x - csx) + (y - csy) * (y - csy);
+      q1 += (u - cdx) * (u - cdx) + (v - cdy) * (v - cdy);
+    }
+  const double rms_s = sqrt(wave_sum(q0) / cnt), rms_d = sqrt(wave_sum(q1) / cnt);
+  if (rms_s == 0.0 || rms_d == 0.0) {  // skimage: ZeroDivisionError -> params = NaN
+    if (lane < 9) o[lane] = NAN;
+    return;
+  }
+  const double nfs = kSqrt2 / rms_s, nfd = kSqrt2 / rms_d;
+
+  // Normal-equation sums of the normalised system.  Per point, with s = (xs, ys, 1),
+  // e = xd, g = yd, q = e^2 + g^2:  affine rows (s, 0, e), (0, s, g);
+  // projective rows (s, 0, -e xs, -e ys, e), (0, s, -g xs, -g ys, g).
+  // acc[0..5] = sums of xx, xy, yy, x, y, 1; then per weight w the same six moments
+  // times w (projective: w = e, g, q) or (affine) e*s, g*s, q.
+  constexpr int NA = MODEL == KCMC_MODEL_AFFINE ? 13 : 24;
+  double acc[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) acc[a] = 0.0;
+  for (int k = lane; k < N; k += 64)
+    if (inl[p0 + k]) {
+      double x, y, u, v;
+      gather_point(src, dst, pt_idx, src_stride, f, p0 + k, x, y, u, v);
+      const double xs = (x - csx) * nfs, ys = (y - csy) * nfs;
+      const double e = (u - cdx) * nfd, g = (v - cdy) * nfd;
+      const double q = e * e + g * g;
+      const double xx = xs * xs, xy = xs * ys, yy = ys * ys;
+      acc[0] += xx;
+      acc[1] += xy;
+      acc[2] += yy;
+      acc[3] += xs;
+      acc[4] += ys;
+      acc[5] += 1.0;
+      if constexpr (MODEL == KCMC_MODEL_AFFINE) {
+        acc[6] += e * xs;
+        acc[7] += e * ys;
+        acc[8] += e;
+        acc[9] += g * xs;
+        acc[10] += g * ys;
+        acc[11] += g;
+        acc[12] += q;
+      } else {
+        const double w[3] = {e, g, q};
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          acc[6 + 6 * b] += w[b] * xx;
+          acc[7 + 6 * b] += w[b] * xy;
+          acc[8 + 6 * b] += w[b] * yy;
+          acc[9 + 6 * b] += w[b] * xs;
+          acc[10 + 6 * b] += w[b] * ys;
+          acc[11 + 6 * b] += w[b];
+        }
+      }
+    }
+#pragma unroll
+  for (int a = 0; a < NA; ++a) acc[a] = wave_sum(acc[a]);
+
+  double A[n][n];
+#pragma unroll
+  for (int i = 0; i < n; ++i)
+#pragma unroll
+    for (int j = 0; j < n; ++j) A[i][j] = 0.0;
+  // the two identical 3x3 blocks: sum s s^T
+  const double ss[3][3] = {{acc[0], acc[1], acc[3]}, {acc[1], acc[2], acc[4]}, {acc[3], acc[4], acc[5]}};
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      A[i][j] = ss[i][j];
+      A[3 + i][3 + j] = ss[i][j];
+    }
+  if constexpr (MODEL == KCMC_MODEL_AFFINE) {
+    const double es[3] = {acc[6], acc[7], acc[8]}, gs[3] = {acc[9], acc[10], acc[11]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      A[i][n - 1] = A[n - 1][i] = es[i];
+      A[3 + i][n - 1] = A[n - 1][3 + i] = gs[i];
+    }
+    A[n - 1][n - 1] = acc[12];
+  } else {
+    // s u^T with s = (xs, ys, 1), u = (xs, ys) -> moment indices [[xx, xy], [xy, yy], [x, y]]
+    const int su[3][2] = {{0, 1}, {1, 2}, {3, 4}};
+    const int sw[3] = {3, 4, 5};  // s * w -> [x, y, 1] moments
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        A[i][6 + j] = A[6 + j][i] = -acc[6 + su[i][j]];
+        A[3 + i][6 + j] = A[6 + j][3 + i] = -acc[12 + su[i][j]];
+      }
+      A[i][8] = A[8][i] = acc[6 + sw[i]];
+      A[3 + i][8] = A[8][3 + i] = acc[12 + sw[i]];
+    }
+    A[6][6] = acc[18];
+    A[6][7] = A[7][6] = acc[19];
+    A[7][7] = acc[20];
+    A[6][8] = A[8][6] = -acc[21];
+    A[7][8] = A[8][7] = -acc[22];
+    A[8][8] = acc[23];
+  }
+
+  double v[n];
+  smallest_eigvec<n>(A, v);
+  double Hm[9];
+  if (fabs(v[n - 1]) <= 1e-8) {
+    // np.isclose(V[-1, -1], 0): estimate() returns False and keeps the hypothesis model
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Hm[k] = best_model[9 * (size_t)f + k];
+  } else {
+    double h[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < n - 1; ++k) h[k] = -v[k] / v[n - 1];
+    denormalize(h, csx, csy, nfs, cdx, cdy, nfd, Hm);
+  }
+  if (lane == 0) {
+    o[0] = Hm[0];
+    o[1] = Hm[1];
+    o[2] = Hm[2] * rate;
+    o[3] = Hm[3];
+    o[4] = Hm[4];
+    o[5] = Hm[5] * rate;
+    o[6] = Hm[6] / rate;
+    o[7] = Hm[7] / rate;
+    o[8] = Hm[8];
+  }
+}
+
+}  // namespace
+}  // namespace kcmc
+
+using namespace kcmc;
+
+extern "C" int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src, const double* dst,
+                                 const int32_t* pt_idx, const int32_t* pt_off, int src_frame_stride, int n_frames,
+                                 int max_n, int trials, double thresh, double rate, int n_skip, double* out_params,
+                                 uint8_t* out_inliers, int32_t* out_n_inliers, int32_t* out_best_trial,
+                                 kcmc_stream_t stream) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_ransac_model: ctx is NULL");
+  if (model != KCMC_MODEL_AFFINE && model != KCMC_MODEL_PROJECTIVE)
+    return fail(KCMC_EINVAL, "kcmc_ransac_model: model must be KCMC_MODEL_AFFINE or KCMC_MODEL_PROJECTIVE "
+                             "(the Euclidean model is kcmc_ransac_rigid)");
+  if (n_frames < 0 || max_n < 0 || trials < 1) return fail(KCMC_EINVAL, "kcmc_ransac_model: bad sizes");
+  if (!(rate > 0.0)) return fail(KCMC_EINVAL, "kcmc_ransac_model: spatial_rate must be > 0");
+  if (n_frames == 0) return KCMC_OK;
+  if (!pt_off || !out_params || !out_n_inliers || !out_best_trial || (max_n > 0 && (!src || !dst || !out_inliers)))
+    return fail(KCMC_EINVAL, "kcmc_ransac_model: NULL pointer");
+  if (max_n > kMaxN) return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_model: max_n > 4096 points per frame");
+  if (pt_idx && src_frame_stride <= 0) return fail(KCMC_EINVAL, "kcmc_ransac_model: src_frame_stride must be > 0");
+  const int ms = model == KCMC_MODEL_AFFINE ? 3 : 4;
+  const HypTables& tab = ctx->mhyp[ms];
+  if (!tab.dev || tab.trials != trials)
+    return fail(KCMC_EINVAL, "kcmc_ransac_model: hypothesis tables not prepared for min_samples=" +
+                                 std::to_string(ms) + ", trials=" + std::to_string(trials) +
+                                 " (call kcmc_ransac_prepare_samples)");
+  const int need = max_n < ms + 1 ? ms + 1 : max_n;
+  const int n_small = need < 128 ? need : 128;
+  const size_t lds_small = (size_t)n_small * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) + 16;
+  const size_t lds_large = (size_t)need * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) +
+                           (size_t)kMaxStack * kThreads * sizeof(double) + 16;
+  if ((max_n > 128 ? lds_large : lds_small) > 150 * 1024)
+    return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_model: max_n/trials exceed the LDS budget");
+  hipStream_t s = (hipStream_t)stream;
+  void* ws = nullptr;
+  KCMC_TRY(workspace_alloc(ctx, &ws, (size_t)n_frames * 9 * sizeof(double), s));
+  double* best_model = static_cast<double*>(ws);
+  const dim3 refit_grid((unsigned)ceil_div(n_frames, 4));
+  if (model == KCMC_MODEL_AFFINE) {
+    hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, false>), dim3(n_frames), dim3(kThreads),
+                       lds_small, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
+                       trials, thresh, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
+    if (max_n > 128)
+      hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, true>), dim3(n_frames), dim3(kThreads),
+                         lds_large, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
+                         trials, thresh, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
+    hipLaunchKernelGGL((ransac_model_refit_kernel<KCMC_MODEL_AFFINE>), refit_grid, dim3(256), 0, s, src, dst, pt_idx,
+                       pt_off, src_frame_stride, out_inliers, out_n_inliers, best_model, n_frames, rate, out_params);
+  } else {
+    hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_PROJECTIVE, false>), dim3(n_frames), dim3(kThreads),
+                       lds_small, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
+                       trials, thresh, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
+    if (max_n > 128)
+      hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_PROJECTIVE, true>), dim3(n_frames), dim3(kThreads),
+                         lds_large, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
+                         trials, thresh, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
+    hipLaunchKernelGGL((ransac_model_refit_kernel<KCMC_MODEL_PROJECTIVE>), refit_grid, dim3(256), 0, s, src, dst,
+                       pt_idx, pt_off, src_frame_stride, out_inliers, out_n_inliers, best_model, n_frames, rate,
+                       out_params);
+  }
+  const int rc = launch_check("ransac_model kernels");
+  KCMC_TRY(workspace_free(ctx, ws, s));
+  return rc;
+}

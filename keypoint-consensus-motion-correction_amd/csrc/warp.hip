@@ -430,10 +430,271 @@ void launch_warp(const uint16_t* src, uint16_t* dst, const double* M, int n_fram
                      dst, plan, minv, H, W);
 }
 
+// ================================================================ warpPerspective
+// cv2.warpPerspective(frame, H, (W, H), INTER_LINEAR), BORDER_CONSTANT 0 -- the warp of
+// the homography extension (BASELINE config 5; the reference only calls warpAffine).
+// OpenCV classic path: invert(M) (closed-form 3x3, core/src/lapack.cpp) unless
+// WARP_INVERSE_MAP, then WarpPerspectiveInvoker (imgwarp.cpp) per block of bw0 columns:
+//   X0 = M0*xo + M1*y + M2, Y0 = M3*xo + M4*y + M5, W0 = M6*xo + M7*y + M8  (xo = block's
+//   first column, x1 = x - xo), W = W0 + M6*x1, W = W ? 32/W : 0,
+//   X = cvRound(clamp((X0 + M0*x1)*W)), Y likewise -> 1/32-px coordinates,
+// and the same remapBilinear blend as warpAffine.  The coordinates are not separable,
+// so each pixel evaluates them in fp64; the tile machinery (plan, LDS-staged box,
+// exact integer blend, direct gather, zeros) is the affine kernel's.
+
+__device__ __forceinline__ void invert_perspective(const double* S, double* M) {
+  double d = S[0] * (S[4] * S[8] - S[5] * S[7]) - S[1] * (S[3] * S[8] - S[5] * S[6]) +
+             S[2] * (S[3] * S[7] - S[4] * S[6]);
+  if (d == 0.0) {
+    for (int k = 0; k < 9; ++k) M[k] = 0.0;
+    return;
+  }
+  d = 1. / d;
+  M[0] = (S[4] * S[8] - S[5] * S[7]) * d;
+  M[1] = (S[2] * S[7] - S[1] * S[8]) * d;
+  M[2] = (S[1] * S[5] - S[2] * S[4]) * d;
+  M[3] = (S[5] * S[6] - S[3] * S[8]) * d;
+  M[4] = (S[0] * S[8] - S[2] * S[6]) * d;
+  M[5] = (S[2] * S[3] - S[0] * S[5]) * d;
+  M[6] = (S[3] * S[7] - S[4] * S[6]) * d;
+  M[7] = (S[1] * S[6] - S[0] * S[7]) * d;
+  M[8] = (S[0] * S[4] - S[1] * S[3]) * d;
+}
+
+// WarpPerspectiveInvoker's fixed-point source coordinate of output pixel (x, y), where
+// xo is the first column of x's bw0-wide block and x1 = x - xo.
+__device__ __forceinline__ void persp_coord(const double* M, int xo, int x1, int y, int& X, int& Y) {
+  const double X0 = M[0] * xo + M[1] * y + M[2];
+  const double Y0 = M[3] * xo + M[4] * y + M[5];
+  const double W0 = M[6] * xo + M[7] * y + M[8];
+  double w = W0 + M[6] * x1;
+  w = w != 0.0 ? 32.0 / w : 0.0;
+  const double fX = fmax((double)INT_MIN, fmin((double)INT_MAX, (X0 + M[0] * x1) * w));
+  const double fY = fmax((double)INT_MIN, fmin((double)INT_MAX, (Y0 + M[3] * x1) * w));
+  X = (int)__builtin_rint(fX);
+  Y = (int)__builtin_rint(fY);
+}
+
+// Source box of a tile: when the projective denominator has one sign over the tile,
+// the tile's image is the convex hull of its corner images; one pixel of margin on each
+// side absorbs the 1/32-px rounding and the second tap.  Otherwise: direct gather.
+template <class Cfg, int C>
+__device__ __forceinline__ Box persp_box(const double* M, int xb, int yb, int H, int W) {
+  const int xl = min(xb + kTileW, W) - 1, yl = min(yb + Cfg::kTileH, H) - 1;
+  const int cx[4] = {xb, xl, xb, xl}, cy[4] = {yb, yb, yl, yl};
+  double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY;
+  bool pos = true, neg = true;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double w = M[6] * cx[k] + M[7] * cy[k] + M[8];
+    pos = pos && w > 0.0;
+    neg = neg && w < 0.0;
+    const double sx = (M[0] * cx[k] + M[1] * cy[k] + M[2]) / w;
+    const double sy = (M[3] * cx[k] + M[4] * cy[k] + M[5]) / w;
+    mnx = fmin(mnx, sx);
+    mxx = fmax(mxx, sx);
+    mny = fmin(mny, sy);
+    mxy = fmax(mxy, sy);
+  }
+  Box b;
+  b.mode = 2;
+  b.ax0 = b.sy0 = b.pitch = b.rows = 0;
+  const double lim = 30000.0;  // keep clear of saturate_cast<short> on coordinates
+  if (!(pos || neg) || !(mnx > -lim && mxx < lim && mny > -lim && mxy < lim)) return b;
+  const long long sx0 = (long long)floor(mnx) - 1, sx1 = (long long)floor(mxx) + 2;
+  const long long sy0 = (long long)floor(mny) - 1, sy1 = (long long)floor(mxy) + 2;
+  const long long ax0 = (sx0 >> 3) << 3;
+  const long long pitch = ((sx1 - ax0 + 1) + 7) & ~7ll;
+  const long long rows = sy1 - sy0 + 1;
+  if (sx1 < 0 || sx0 > W - 1 || sy1 < 0 || sy0 > H - 1)
+    b.mode = 1;
+  else if (pitch <= kMaxPitch && rows <= 8 * Cfg::kRowPasses && pitch * rows * C <= Cfg::kLdsElems)
+    b.mode = 0;
+  b.ax0 = (int)ax0;
+  b.sy0 = (int)sy0;
+  b.pitch = (int)pitch;
+  b.rows = (int)rows;
+  return b;
+}
+
+template <int C, class Cfg>
+__global__ __launch_bounds__(256) void persp_plan_kernel(const double* __restrict__ Mall, int n_frames, int H, int W,
+                                                         int inverse_map, int ntx, int nty, TilePlan* __restrict__ plan,
+                                                         double* __restrict__ minv) {
+  const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (t >= (long long)ntx * nty * n_frames) return;
+  const int f = (int)(t / (ntx * nty)), t2 = (int)(t - (long long)f * ntx * nty);
+  const int xb = (t2 % ntx) * kTileW, yb = (t2 / ntx) * Cfg::kTileH;
+  double M[9];
+  if (inverse_map) {
+    for (int k = 0; k < 9; ++k) M[k] = Mall[9 * (size_t)f + k];
+  } else {
+    invert_perspective(Mall + 9 * (size_t)f, M);
+  }
+  if (t2 == 0)
+    for (int k = 0; k < 9; ++k) minv[9 * (size_t)f + k] = M[k];
+  const Box b = persp_box<Cfg, C>(M, xb, yb, H, W);
+  plan[t] = TilePlan{b.mode, b.ax0, b.sy0, b.pitch | (b.rows << 16)};
+}
+
+// remapBilinear's blend of four taps: exact integer evaluation, with the float-faithful
+// re-blend for sums >= 2^24 (see output_rows).
+__device__ __forceinline__ uint16_t blend_exact(uint32_t v00, uint32_t v01, uint32_t v10, uint32_t v11, int fx,
+                                                int fy) {
+  const uint32_t ax = 32 - fx, ay = 32 - fy;
+  uint32_t h0 = __umul24(v00, ax) + __umul24(v01, (uint32_t)fx);
+  uint32_t h1 = __umul24(v10, ax) + __umul24(v11, (uint32_t)fx);
+  asm volatile("" : "+v"(h0), "+v"(h1));
+  const uint32_t Sv = __umul24(h0, ay) + __umul24(h1, (uint32_t)fy);
+  uint16_t r = round_q10(Sv);
+  if (Sv >> 24) r = blend_int(v00, v01, v10, v11, fx, fy);
+  return r;
+}
+
+template <class Cfg, int C, int MODE>
+__device__ __forceinline__ void persp_rows(const uint16_t* stile, const Box& box, const uint16_t* __restrict__ S,
+                                           uint16_t* __restrict__ Dst, const double* M, int H, int W, int xb, int yb,
+                                           int wave, int lane, int bw0) {
+  const int x = xb + 2 * lane;
+  const bool pair_store = C == 1 && (W & 1) == 0 && x + 2 <= W;
+  int xo[2], x1[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int xc = min(x + q, W - 1);  // columns past the edge reuse the last column's taps
+    xo[q] = xc - xc % bw0;
+    x1[q] = xc - xo[q];
+  }
+#pragma unroll
+  for (int i = 0; i < Cfg::kTileH / 4; ++i) {
+    const int y = yb + wave + 4 * i;  // wave-uniform
+    if (y >= H) break;
+    uint16_t o[2 * C];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      int X, Y;
+      persp_coord(M, xo[p], x1[p], y, X, Y);
+      if (MODE == 0) {
+        const int fx = X & 31, fy = Y & 31;
+        const int li = ((Y >> 5) - box.sy0) * box.pitch + ((X >> 5) - box.ax0);
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+          const int i00 = li * C + k, i10 = i00 + box.pitch * C;
+          o[p * C + k] = blend_exact(tap(stile, i00), tap(stile, i00 + C), tap(stile, i10), tap(stile, i10 + C), fx, fy);
+        }
+      } else if (MODE == 1) {
+#pragma unroll
+        for (int k = 0; k < C; ++k) o[p * C + k] = 0;
+      } else {
+        bilinear_px<C>(S, H, W, X, Y, o + p * C);
+      }
+    }
+    uint16_t* drow = Dst + ((size_t)y * W + x) * C;
+    if (pair_store) {
+      *reinterpret_cast<uint32_t*>(drow) = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (x + q < W)
+#pragma unroll
+          for (int k = 0; k < C; ++k) drow[q * C + k] = o[q * C + k];
+    }
+  }
+}
+
+template <int C, class Cfg = BlockCfg>
+__global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-access-mode"))) void
+warp_perspective_u16_kernel(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
+                            const TilePlan* __restrict__ plan, const double* __restrict__ minv, int H, int W, int bw0) {
+  __shared__ __attribute__((aligned(16))) uint16_t stile[Cfg::kLdsElems];
+  const int ntx = gridDim.x, nty = gridDim.y;
+  const int tile = xcd_remap(blockIdx.x + ntx * (blockIdx.y + nty * blockIdx.z), ntx * nty * gridDim.z);
+  const int f = tile / (ntx * nty);
+  const int t2 = tile - f * ntx * nty;
+  const int xb = (t2 % ntx) * kTileW, yb = (t2 / ntx) * Cfg::kTileH;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const uint16_t* S = src + (size_t)f * H * W * C;
+  uint16_t* Dst = dst + (size_t)f * H * W * C;
+
+  const Box box = unpack(plan[tile]);
+  const bool vec_stage = (C == 1) && ((W & 7) == 0);
+  uint4 chunk[Cfg::kRowPasses];
+  if (box.mode == 0 && vec_stage) stage_issue<Cfg>(S, box, H, W, tid, chunk);
+  double M[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) M[k] = minv[9 * (size_t)f + k];
+  if (box.mode == 0) {
+    if (vec_stage)
+      stage_land<Cfg>(stile, box, tid, chunk);
+    else
+      stage_scalar<C>(S, stile, box, H, W, tid);
+  }
+  __syncthreads();
+  if (box.mode == 0)
+    persp_rows<Cfg, C, 0>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0);
+  else if (box.mode == 1)
+    persp_rows<Cfg, C, 1>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0);
+  else
+    persp_rows<Cfg, C, 2>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0);
+}
+
+template <class Cfg>
+size_t persp_workspace_bytes(int n_frames, int H, int W) {
+  const size_t tiles = (size_t)ceil_div(W, kTileW) * ceil_div(H, Cfg::kTileH) * n_frames;
+  return tiles * sizeof(TilePlan) + (size_t)n_frames * 9 * sizeof(double);
+}
+
+template <int C, class Cfg = BlockCfg>
+void launch_persp(const uint16_t* src, uint16_t* dst, const double* M, int n_frames, int H, int W, int inverse_map,
+                  void* ws, hipStream_t s) {
+  const int ntx = ceil_div(W, kTileW), nty = ceil_div(H, Cfg::kTileH);
+  const long long tiles = (long long)ntx * nty * n_frames;
+  // WarpPerspectiveInvoker's block width: bh0 = min(16, H), bw0 = min(1024 / bh0, W)
+  const int bh0 = H < 16 ? H : 16;
+  const int bw0 = 1024 / bh0 < W ? 1024 / bh0 : W;
+  double* minv = static_cast<double*>(ws);
+  TilePlan* plan = reinterpret_cast<TilePlan*>(minv + 9 * (size_t)n_frames);
+  hipLaunchKernelGGL((persp_plan_kernel<C, Cfg>), dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, s, M, n_frames,
+                     H, W, inverse_map, ntx, nty, plan, minv);
+  hipLaunchKernelGGL((warp_perspective_u16_kernel<C, Cfg>), dim3(ntx, nty, n_frames), dim3(kThreads), 0, s, src, dst,
+                     plan, minv, H, W, bw0);
+}
+
 }  // namespace
 }  // namespace kcmc
 
 using namespace kcmc;
+
+extern "C" int kcmc_warp_perspective_u16(kcmc_ctx* ctx, const uint16_t* src, uint16_t* dst, const double* M,
+                                         int n_frames, int H, int W, int C, int inverse_map, kcmc_stream_t stream) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_warp_perspective_u16: ctx is NULL");
+  if (n_frames < 0 || H < 0 || W < 0) return fail(KCMC_EINVAL, "kcmc_warp_perspective_u16: negative size");
+  if (n_frames == 0 || H == 0 || W == 0) return KCMC_OK;
+  if (!src || !dst || !M) return fail(KCMC_EINVAL, "kcmc_warp_perspective_u16: NULL pointer");
+  if (H > 32767 || W > 32767) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_perspective_u16: H, W must be < 32768");
+  if (n_frames > 65535) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_perspective_u16: at most 65535 frames per call");
+  if (C != 1 && C != 3 && C != 4) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_perspective_u16: C must be 1, 3 or 4");
+  if (src == dst) return fail(KCMC_EINVAL, "kcmc_warp_perspective_u16: in-place warp is not supported");
+  if ((long long)ceil_div(W, kTileW) * ceil_div(H, BlockCfg::kTileH) * n_frames >= (1ll << 31))
+    return fail(KCMC_EUNSUPPORTED, "kcmc_warp_perspective_u16: too many tiles in one call");
+  hipStream_t s = (hipStream_t)stream;
+  void* ws = nullptr;
+  KCMC_TRY(workspace_alloc(ctx, &ws, persp_workspace_bytes<BlockCfg>(n_frames, H, W), s));
+  switch (C) {
+    case 1:
+      launch_persp<1>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
+      break;
+    case 3:
+      launch_persp<3>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
+      break;
+    default:
+      launch_persp<4>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
+      break;
+  }
+  const int rc = launch_check("warp_perspective_u16_kernel");
+  KCMC_TRY(workspace_free(ctx, ws, s));
+  return rc;
+}
 
 extern "C" int kcmc_warp_affine_u16(kcmc_ctx* ctx, const uint16_t* src, uint16_t* dst, const double* M,
                                     int n_frames, int H, int W, int C, int inverse_map, kcmc_stream_t stream) {

@@ -240,6 +240,64 @@ def ransac_rigid(
     return res
 
 
+def ransac_model(
+    src: torch.Tensor,
+    dst: torch.Tensor,
+    pt_off: torch.Tensor,
+    pt_off_host: np.ndarray,
+    model: str = "affine",
+    pt_idx: Optional[torch.Tensor] = None,
+    src_frame_stride: int = 0,
+    trials: int = 1000,
+    residual_threshold: float = 2.0,
+    spatial_rate: float = 1.0,
+    n_skip: int = 3,
+    seed: int = 42,
+) -> RansacResult:
+    """skimage ransac with AffineTransform (min_samples 3) or ProjectiveTransform
+    (min_samples 4) per frame, all frames in one launch (the extension behind BASELINE
+    configs 3-5; same call shape as VA:309-316).  params: [F, 3, 3] f64.
+
+    Frames with n_skip <= N <= min_samples raise ValueError like skimage
+    (fit.py:798-799); frames with N < n_skip get NaN (VA:306-307)."""
+    if model not in ("affine", "projective"):
+        raise ValueError(f"model must be 'affine' or 'projective' (got {model!r}); rigid: ransac_rigid")
+    dev = _device_of(src)
+    _require(src, "src", torch.float64, dev, 2)
+    _require(dst, "dst", torch.float64, dev, 2)
+    _require(pt_off, "pt_off", torch.int32, dev, 1)
+    if pt_idx is not None:
+        _require(pt_idx, "pt_idx", torch.int32, dev, 1)
+    ms = _lib.MODEL_MIN_SAMPLES[model]
+    F = pt_off.numel() - 1
+    pt_off_host = np.asarray(pt_off_host)
+    _check_offsets(pt_off_host, F)
+    ns = np.diff(pt_off_host)
+    bad = (ns >= n_skip) & (ns <= ms)
+    if bad.any():
+        raise ValueError("`min_samples` must be in range (0, <number-of-samples>)")
+    max_n = int(ns.max()) if F else 0
+    P = int(pt_off_host[-1]) if F else 0
+    res = RansacResult(
+        params=torch.empty((F, 3, 3), dtype=torch.float64, device=dev),
+        inliers=torch.empty((max(P, 0),), dtype=torch.uint8, device=dev),
+        n_inliers=torch.empty((F,), dtype=torch.int32, device=dev),
+        best_trial=torch.empty((F,), dtype=torch.int32, device=dev),
+    )
+    if F == 0:
+        return res
+    ctx = _ctx(dev)
+    L = _lib.load()
+    n_run = np.unique(ns[ns >= max(int(n_skip), ms + 1)]).astype(np.int32)
+    _lib.check(L.kcmc_ransac_prepare_samples(ctx.handle, ms, _np_ptr(n_run), int(n_run.size), int(trials),
+                                             int(seed) & 0xFFFFFFFF))
+    _lib.check(L.kcmc_ransac_model(
+        ctx.handle, _lib.MODEL_IDS[model], _ptr(src), _ptr(dst), _ptr(pt_idx), _ptr(pt_off), int(src_frame_stride), F,
+        max_n, int(trials), float(residual_threshold), float(spatial_rate), int(n_skip), _ptr(res.params),
+        _ptr(res.inliers), _ptr(res.n_inliers), _ptr(res.best_trial), _stream(dev)))
+    return res
+
+
 # ----------------------------------------------------------------------- K3
 def warp_affine_u16(frames: torch.Tensor, affines: torch.Tensor, out: Optional[torch.Tensor] = None,
                     inverse_map: bool = False) -> torch.Tensor:
@@ -267,4 +325,32 @@ def warp_affine_u16(frames: torch.Tensor, affines: torch.Tensor, out: Optional[t
     L = _lib.load()
     _lib.check(L.kcmc_warp_affine_u16(_ctx(dev).handle, _ptr(frames), _ptr(out), _ptr(affines), F, H, W, C,
                                       int(bool(inverse_map)), _stream(dev)))
+    return out
+
+
+def warp_perspective_u16(frames: torch.Tensor, homographies: torch.Tensor, out: Optional[torch.Tensor] = None,
+                         inverse_map: bool = False) -> torch.Tensor:
+    """cv2.warpPerspective(frame, H, (W, H), INTER_LINEAR) for every frame (the warp of
+    the homography extension).  frames [F, H, W] or [F, H, W, C] uint16; homographies
+    [F, 3, 3] f64 (forward maps, frame -> template, as RANSAC returns them)."""
+    dev = _device_of(frames)
+    if frames.dtype != torch.uint16:
+        raise TypeError(f"frames: expected torch.uint16, got {frames.dtype}")
+    if frames.dim() not in (3, 4):
+        raise ValueError("frames must be [F, H, W] or [F, H, W, C]")
+    _require(frames, "frames", torch.uint16, dev)
+    _require(homographies, "homographies", torch.float64, dev, 3)
+    F, H, W = frames.shape[:3]
+    C = 1 if frames.dim() == 3 else frames.shape[3]
+    if homographies.shape != (F, 3, 3):
+        raise ValueError(f"homographies must be [{F}, 3, 3], got {tuple(homographies.shape)}")
+    if out is None:
+        out = torch.empty_like(frames)
+    else:
+        _require(out, "out", torch.uint16, dev)
+        if out.shape != frames.shape:
+            raise ValueError("out must have the shape of frames")
+    L = _lib.load()
+    _lib.check(L.kcmc_warp_perspective_u16(_ctx(dev).handle, _ptr(frames), _ptr(out), _ptr(homographies), F, H, W, C,
+                                           int(bool(inverse_map)), _stream(dev)))
     return out

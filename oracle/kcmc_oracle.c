@@ -185,6 +185,100 @@ int kcmc_oracle_warp_affine_u16(const uint16_t* src, int H, int W, int C,
 }
 
 /* ------------------------------------------------------------------------- */
+/* K3 extension oracle: cv2.warpPerspective(img, M, (W, H), INTER_LINEAR) on   */
+/* uint16, BORDER_CONSTANT 0 (BASELINE config 5, homography model; the        */
+/* reference itself only calls warpAffine, VA:458).  Classic OpenCV 4.x path: */
+/* imgwarp.cpp WarpPerspectiveInvoker (per 1024-pixel block of bw0 x bh0      */
+/* pixels, double coordinates relative to the block's first column, 1/32-px   */
+/* rounding) + remapBilinear's float-weight blend (same as warpAffine).       */
+/* ------------------------------------------------------------------------- */
+
+/* cv::invert(M, M) of a 3x3 double matrix with the default DECOMP_LU: OpenCV's
+ * closed-form n == 3 branch (core/src/lapack.cpp): det3, then the adjugate times 1/d;
+ * a singular matrix gives all zeros.  Returns 1 if invertible. */
+int kcmc_oracle_invert_perspective(const double* S, double* M) {
+#define SD(r, c) S[3 * (r) + (c)]
+  double d = SD(0, 0) * (SD(1, 1) * SD(2, 2) - SD(1, 2) * SD(2, 1)) -
+             SD(0, 1) * (SD(1, 0) * SD(2, 2) - SD(1, 2) * SD(2, 0)) +
+             SD(0, 2) * (SD(1, 0) * SD(2, 1) - SD(1, 1) * SD(2, 0));
+  double t[9];
+  if (d == 0) {
+    for (int k = 0; k < 9; ++k) M[k] = 0;
+    return 0;
+  }
+  d = 1. / d;
+  t[0] = (SD(1, 1) * SD(2, 2) - SD(1, 2) * SD(2, 1)) * d;
+  t[1] = (SD(0, 2) * SD(2, 1) - SD(0, 1) * SD(2, 2)) * d;
+  t[2] = (SD(0, 1) * SD(1, 2) - SD(0, 2) * SD(1, 1)) * d;
+  t[3] = (SD(1, 2) * SD(2, 0) - SD(1, 0) * SD(2, 2)) * d;
+  t[4] = (SD(0, 0) * SD(2, 2) - SD(0, 2) * SD(2, 0)) * d;
+  t[5] = (SD(0, 2) * SD(1, 0) - SD(0, 0) * SD(1, 2)) * d;
+  t[6] = (SD(1, 0) * SD(2, 1) - SD(1, 1) * SD(2, 0)) * d;
+  t[7] = (SD(0, 1) * SD(2, 0) - SD(0, 0) * SD(2, 1)) * d;
+  t[8] = (SD(0, 0) * SD(1, 1) - SD(0, 1) * SD(1, 0)) * d;
+#undef SD
+  memcpy(M, t, sizeof(t));
+  return 1;
+}
+
+/* remapBilinear<Cast<float,ushort>> for one output pixel at fixed-point source
+ * coordinate (X, Y) in 1/32 px: taps outside [0,W)x[0,H) read 0. */
+static void bilinear_u16(const uint16_t* src, int H, int W, int C, int X, int Y, const float* tab1, uint16_t* D) {
+  const size_t sstep = (size_t)W * C;
+  int sx = sat_short(X >> 5), sy = sat_short(Y >> 5);
+  int fx = X & 31, fy = Y & 31;
+  float w[4] = {tab1[2 * fy] * tab1[2 * fx], tab1[2 * fy] * tab1[2 * fx + 1], tab1[2 * fy + 1] * tab1[2 * fx],
+                tab1[2 * fy + 1] * tab1[2 * fx + 1]};
+  for (int k = 0; k < C; ++k) {
+    int xs[2] = {sx, sx + 1}, ys[2] = {sy, sy + 1};
+    float v[4];
+    for (int q = 0; q < 4; ++q) {
+      int xx = xs[q & 1], yy = ys[q >> 1];
+      v[q] = ((unsigned)xx < (unsigned)W && (unsigned)yy < (unsigned)H) ? src[(size_t)yy * sstep + (size_t)xx * C + k]
+                                                                        : 0.f;
+    }
+    D[k] = sat_ushort_f(v[0] * w[0] + v[1] * w[1] + v[2] * w[2] + v[3] * w[3]);
+  }
+}
+
+int kcmc_oracle_warp_perspective_u16(const uint16_t* src, int H, int W, int C, const double* M9, int inverse_map,
+                                     uint16_t* dst, int dH, int dW) {
+  if (H <= 0 || W <= 0 || C <= 0 || dH < 0 || dW < 0) return -1;
+  if (dH == 0 || dW == 0) return 0;
+  double M[9];
+  if (inverse_map)
+    memcpy(M, M9, sizeof(M));
+  else
+    kcmc_oracle_invert_perspective(M9, M);
+  float tab1[2 * 32];
+  for (int i = 0; i < 32; ++i) {
+    float x = i * (1.f / 32);
+    tab1[2 * i] = 1.f - x;
+    tab1[2 * i + 1] = x;
+  }
+  /* WarpPerspectiveInvoker block shape: BLOCK_SZ = 32 */
+  int bh0 = 16 < dH ? 16 : dH;
+  int bw0 = 1024 / bh0 < dW ? 1024 / bh0 : dW;
+  for (int y = 0; y < dH; ++y) {
+    for (int xb = 0; xb < dW; xb += bw0) {
+      int bw = bw0 < dW - xb ? bw0 : dW - xb;
+      double X0 = M[0] * xb + M[1] * y + M[2];
+      double Y0 = M[3] * xb + M[4] * y + M[5];
+      double W0 = M[6] * xb + M[7] * y + M[8];
+      for (int x1 = 0; x1 < bw; ++x1) {
+        double Wd = W0 + M[6] * x1;
+        Wd = Wd != 0 ? 32 / Wd : 0;
+        double fX = fmax((double)INT32_MIN, fmin((double)INT32_MAX, (X0 + M[0] * x1) * Wd));
+        double fY = fmax((double)INT32_MIN, fmin((double)INT32_MAX, (Y0 + M[3] * x1) * Wd));
+        int X = cv_round(fX), Y = cv_round(fY);
+        bilinear_u16(src, H, W, C, X, Y, tab1, dst + ((size_t)y * dW + xb + x1) * C);
+      }
+    }
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------------- */
 /* K2 oracle: skimage 0.18.3 ransac(EuclideanTransform, min_samples=2, ...)   */
 /* as called at VA:309-316, in closed form.                                    */
 /* ------------------------------------------------------------------------- */
@@ -313,4 +407,199 @@ int kcmc_oracle_ransac_rigid(const double* src, const double* dst, int N, const 
   free(cur);
   free(sel);
   return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* K2 extension oracle: skimage 0.18.3 ransac with AffineTransform            */
+/* (min_samples = 3) or ProjectiveTransform (min_samples = 4), the build's     */
+/* configs 3-5 (the reference itself only uses EuclideanTransform, VA:311).   */
+/* The hypothesis loop is restated in closed form; the final total-least-      */
+/* squares refit on the inliers is done in oracle.py with numpy's SVD, as      */
+/* skimage does it (_geometric.py:596-703).                                    */
+/* ------------------------------------------------------------------------- */
+
+/* skimage _center_and_normalize_points (_geometric.py:18-69) on the k points
+ * sel[0..k): centroid = sequential axis-0 mean, rms = sqrt(pairwise_sum of the 2k
+ * squared deviations (row-major) / k).  Returns 0 on success, 1 when rms == 0
+ * (skimage: ZeroDivisionError -> estimate returns False). */
+static int center_normalize(const double* p, const int32_t* sel, int k, double* cx, double* cy, double* nf) {
+  double sx = 0, sy = 0;
+  for (int i = 0; i < k; ++i) {
+    sx += p[2 * sel[i]];
+    sy += p[2 * sel[i] + 1];
+  }
+  *cx = sx / k;
+  *cy = sy / k;
+  double dev[8];
+  for (int i = 0; i < k; ++i) {
+    double ex = p[2 * sel[i]] - *cx, ey = p[2 * sel[i] + 1] - *cy;
+    dev[2 * i] = ex * ex;
+    dev[2 * i + 1] = ey * ey;
+  }
+  double rms = sqrt(kcmc_oracle_pairwise_sum(dev, 2 * k) / k);
+  if (rms == 0) return 1;
+  *nf = sqrt(2.0) / rms;
+  return 0;
+}
+
+/* Affine model through 3 correspondences: the exact solution skimage's TLS finds
+ * for a non-degenerate triple, L = [v1 v2][u1 u2]^-1 with u_k = s_k - s_0,
+ * v_k = d_k - d_0, t = c_d - L c_s.  Degenerate (skimage's estimate returns False):
+ * a point set with rms 0, det == 0, or |V[-1,-1]| = 1/sqrt(1 + |h|^2) <= 1e-8 with h
+ * the model in normalised coordinates (np.isclose(V[-1,-1], 0)).  H: 3x3 row-major. */
+static int affine_fit3(const double* src, const double* dst, const int32_t* sel, double* H) {
+  double csx, csy, nfs, cdx, cdy, nfd;
+  if (center_normalize(src, sel, 3, &csx, &csy, &nfs) || center_normalize(dst, sel, 3, &cdx, &cdy, &nfd)) return 1;
+  const double *s0 = src + 2 * sel[0], *s1 = src + 2 * sel[1], *s2 = src + 2 * sel[2];
+  const double *d0 = dst + 2 * sel[0], *d1 = dst + 2 * sel[1], *d2 = dst + 2 * sel[2];
+  double u1x = s1[0] - s0[0], u1y = s1[1] - s0[1], u2x = s2[0] - s0[0], u2y = s2[1] - s0[1];
+  double v1x = d1[0] - d0[0], v1y = d1[1] - d0[1], v2x = d2[0] - d0[0], v2y = d2[1] - d0[1];
+  double det = u1x * u2y - u2x * u1y;
+  if (det == 0) return 1;
+  double l00 = (v1x * u2y - v2x * u1y) / det;
+  double l01 = (v2x * u1x - v1x * u2x) / det;
+  double l10 = (v1y * u2y - v2y * u1y) / det;
+  double l11 = (v2y * u1x - v1y * u2x) / det;
+  double g = nfd / nfs;
+  double hn2 = g * g * (((l00 * l00 + l01 * l01) + l10 * l10) + l11 * l11);
+  if (1.0 / sqrt(1.0 + hn2) <= 1e-8) return 1;
+  H[0] = l00;
+  H[1] = l01;
+  H[2] = cdx - (l00 * csx + l01 * csy);
+  H[3] = l10;
+  H[4] = l11;
+  H[5] = cdy - (l10 * csx + l11 * csy);
+  H[6] = 0;
+  H[7] = 0;
+  H[8] = 1;
+  return 0;
+}
+
+/* Projective model through 4 correspondences as skimage normalises it: Hartley
+ * normalisation of both sets, the 8x8 DLT system with h22 = 1 in normalised
+ * coordinates (rows: the four x-equations, then the four y-equations, like skimage's
+ * A), Gaussian elimination with partial pivoting, H = inv(N_dst) Hn N_src.
+ * Degenerate: rms 0, a zero pivot, or 1/sqrt(1 + |h|^2) <= 1e-8. */
+static int projective_fit4(const double* src, const double* dst, const int32_t* sel, double* H) {
+  double csx, csy, nfs, cdx, cdy, nfd;
+  if (center_normalize(src, sel, 4, &csx, &csy, &nfs) || center_normalize(dst, sel, 4, &cdx, &cdy, &nfd)) return 1;
+  double M[8][9];
+  for (int i = 0; i < 4; ++i) {
+    double xs = (src[2 * sel[i]] - csx) * nfs, ys = (src[2 * sel[i] + 1] - csy) * nfs;
+    double xd = (dst[2 * sel[i]] - cdx) * nfd, yd = (dst[2 * sel[i] + 1] - cdy) * nfd;
+    double rx[9] = {xs, ys, 1, 0, 0, 0, -(xd * xs), -(xd * ys), xd};
+    double ry[9] = {0, 0, 0, xs, ys, 1, -(yd * xs), -(yd * ys), yd};
+    memcpy(M[i], rx, sizeof(rx));
+    memcpy(M[4 + i], ry, sizeof(ry));
+  }
+  for (int c = 0; c < 8; ++c) {
+    int piv = c;
+    for (int r = c + 1; r < 8; ++r)
+      if (fabs(M[r][c]) > fabs(M[piv][c])) piv = r;
+    if (M[piv][c] == 0) return 1;
+    if (piv != c)
+      for (int k = c; k < 9; ++k) {
+        double t = M[c][k];
+        M[c][k] = M[piv][k];
+        M[piv][k] = t;
+      }
+    for (int r = c + 1; r < 8; ++r) {
+      double f = M[r][c] / M[c][c];
+      for (int k = c; k < 9; ++k) M[r][k] -= f * M[c][k];
+    }
+  }
+  double h[8];
+  for (int c = 7; c >= 0; --c) {
+    double v = M[c][8];
+    for (int k = c + 1; k < 8; ++k) v -= M[c][k] * h[k];
+    h[c] = v / M[c][c];
+  }
+  double hn2 = 0;
+  for (int k = 0; k < 8; ++k) hn2 += h[k] * h[k];
+  if (1.0 / sqrt(1.0 + hn2) <= 1e-8) return 1;
+  /* H = inv(Nd) Hn Ns with inv(Nd) = [[1/nfd, 0, cdx], [0, 1/nfd, cdy], [0, 0, 1]] */
+  double T[9];
+  for (int r = 0; r < 3; ++r) {
+    double a = h[3 * r], b = h[3 * r + 1], c = (r == 2) ? 1.0 : h[3 * r + 2];
+    T[3 * r] = a * nfs;
+    T[3 * r + 1] = b * nfs;
+    T[3 * r + 2] = c - (a * nfs * csx + b * nfs * csy);
+  }
+  double id = 1.0 / nfd;
+  for (int k = 0; k < 3; ++k) {
+    H[k] = T[k] * id + cdx * T[6 + k];
+    H[3 + k] = T[3 + k] * id + cdy * T[6 + k];
+    H[6 + k] = T[6 + k];
+  }
+  return 0;
+}
+
+/* ProjectiveTransform._apply_mat + residuals (_geometric.py:183-202, 548-562):
+ * [x y 1] @ H^T in the dgemm operation order used for the rigid model, w == 0 -> eps,
+ * divide, r = sqrt(dx^2 + dy^2).  An affine H has an exact [0 0 1] last row, so
+ * w == 1 and the division is exact (skipped). */
+static double model_residual(int model, const double* H, double x, double y, double xd, double yd) {
+  double X = fma(y, H[1], x * H[0]) + H[2];
+  double Y = fma(y, H[4], x * H[3]) + H[5];
+  if (model == 2) {
+    double w = fma(y, H[7], x * H[6]) + H[8];
+    if (w == 0) w = DBL_EPSILON;
+    X = X / w;
+    Y = Y / w;
+  }
+  double ex = X - xd, ey = Y - yd;
+  return sqrt(ex * ex + ey * ey);
+}
+
+/* model 1 = affine (hyp [T,3]), 2 = projective (hyp [T,4]).  out_model [9] = the
+ * winning hypothesis' 3x3 model (NaN if none), out_inliers [N], best trial and its
+ * inlier count as skimage's loop leaves them.  Returns 0 if skimage refits (a best
+ * hypothesis with >= 1 inlier), 1 if its model is None, -1/-2 on bad input. */
+int kcmc_oracle_ransac_model(int model, const double* src, const double* dst, int N, const int32_t* hyp, int T,
+                             double thresh, double* out_model, uint8_t* out_inliers, int32_t* out_best_trial,
+                             int32_t* out_n_inliers) {
+  if (model != 1 && model != 2) return -1;
+  const int ms = model == 1 ? 3 : 4;
+  double* r2 = (double*)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1));
+  uint8_t* cur = (uint8_t*)malloc((size_t)(N > 0 ? N : 1));
+  if (!r2 || !cur) {
+    free(r2);
+    free(cur);
+    return -2;
+  }
+  int best_n = 0, best_t = -1;
+  double best_S = INFINITY;
+  for (int k = 0; k < 9; ++k) out_model[k] = NAN;
+  memset(out_inliers, 0, (size_t)N);
+  for (int t = 0; t < T; ++t) {
+    const int32_t* sel = hyp + (size_t)t * ms;
+    double Hm[9];
+    int bad = model == 1 ? affine_fit3(src, dst, sel, Hm) : projective_fit4(src, dst, sel, Hm);
+    if (bad) continue; /* estimate() returned False: the trial is skipped (fit.py:835-838) */
+    int cnt = 0;
+    for (int k = 0; k < N; ++k) {
+      double r = model_residual(model, Hm, src[2 * k], src[2 * k + 1], dst[2 * k], dst[2 * k + 1]);
+      cur[k] = r < thresh;
+      cnt += cur[k];
+      r2[k] = r * r;
+    }
+    double S = kcmc_oracle_pairwise_sum(r2, N);
+    if (cnt > best_n || (cnt == best_n && S < best_S)) {
+      best_n = cnt;
+      best_S = S;
+      best_t = t;
+      memcpy(out_inliers, cur, (size_t)N);
+      memcpy(out_model, Hm, sizeof(Hm));
+      if (best_S <= 0) break; /* stop_residuals_sum = 0 (fit.py:862-869) */
+    }
+  }
+  if (best_n == 0) {
+    memset(out_inliers, 0, (size_t)N);
+    for (int k = 0; k < 9; ++k) out_model[k] = NAN;
+  }
+  *out_best_trial = best_t;
+  *out_n_inliers = best_n;
+  free(r2);
+  free(cur);
+  return best_n > 0 ? 0 : 1;
 }

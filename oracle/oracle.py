@@ -30,6 +30,7 @@ OpenCV is absent from this image ("parity vs real OpenCV unpinned").
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 from collections import Counter
 from typing import Dict, List, Sequence, Set, Tuple
@@ -58,6 +59,10 @@ def lib() -> ctypes.CDLL:
         L.kcmc_oracle_pairwise_sum.argtypes = [P, i]
         L.kcmc_oracle_pairwise_sum.restype = ctypes.c_double
         L.kcmc_oracle_ransac_rigid.argtypes = [P, P, i, P, i, ctypes.c_double, P, P, P, P]
+        L.kcmc_oracle_ransac_model.argtypes = [i, P, P, i, P, i, ctypes.c_double, P, P, P, P]
+        L.kcmc_oracle_warp_perspective_u16.argtypes = [P, i, i, i, P, i, P, i, i]
+        L.kcmc_oracle_invert_perspective.argtypes = [P, P]
+        L.kcmc_oracle_invert_perspective.restype = i
         _LIB = L
     return _LIB
 
@@ -237,6 +242,120 @@ def ransac_rigid_skimage(src, dst, trials=1000, thresh=2.0, seed=42):
     return np.full((2, 3), np.nan), None
 
 
+# ------------------------------------------------- K2 extension: affine / projective
+MODEL_IDS = {"affine": 1, "projective": 2}
+MODEL_MIN_SAMPLES = {"affine": 3, "projective": 4}
+_TLS_COEFFS = {"affine": list(range(6)), "projective": list(range(8))}
+
+
+def _center_and_normalize(points: np.ndarray):
+    """skimage 0.18.3 _center_and_normalize_points (_geometric.py:18-69), restated:
+    the Hartley similarity taking the centroid to 0 and the rms distance to sqrt(2).
+    Raises ZeroDivisionError for coincident points, like skimage."""
+    centroid = np.mean(points, axis=0)
+    rms = math.sqrt(np.sum((points - centroid) ** 2) / points.shape[0])
+    nf = math.sqrt(2) / rms
+    N = np.array([[nf, 0, -nf * centroid[0]], [0, nf, -nf * centroid[1]], [0, 0, 1]])
+    ph = np.vstack([points.T, np.ones(points.shape[0])])
+    q = (N @ ph).T
+    out = q[:, :2]
+    out[:, 0] /= q[:, 2]
+    out[:, 1] /= q[:, 2]
+    return N, out
+
+
+def estimate_tls(src: np.ndarray, dst: np.ndarray, model: str):
+    """ProjectiveTransform/AffineTransform.estimate of skimage 0.18.3
+    (_geometric.py:596-703): total least squares through np.linalg.svd of the 2N x 7
+    (affine) / 2N x 9 (projective) system in Hartley-normalised coordinates.
+    Returns (ok, params); params is NaN on ZeroDivisionError and None when
+    np.isclose(V[-1,-1], 0) (skimage then leaves the previous params in place)."""
+    try:
+        Ns, s = _center_and_normalize(np.asarray(src, np.float64))
+        Nd, d = _center_and_normalize(np.asarray(dst, np.float64))
+    except ZeroDivisionError:
+        return False, np.full((3, 3), np.nan)
+    xs, ys, xd, yd = s[:, 0], s[:, 1], d[:, 0], d[:, 1]
+    n = s.shape[0]
+    A = np.zeros((2 * n, 9))
+    A[:n, 0], A[:n, 1], A[:n, 2] = xs, ys, 1
+    A[n:, 3], A[n:, 4], A[n:, 5] = xs, ys, 1
+    A[:n, 6], A[:n, 7], A[:n, 8] = -xd * xs, -xd * ys, xd
+    A[n:, 6], A[n:, 7], A[n:, 8] = -yd * xs, -yd * ys, yd
+    cols = _TLS_COEFFS[model] + [8]
+    _, _, V = np.linalg.svd(A[:, cols])
+    if np.isclose(V[-1, -1], 0):
+        return False, None
+    H = np.zeros((3, 3))
+    H.flat[_TLS_COEFFS[model]] = -V[-1, :-1] / V[-1, -1]
+    H[2, 2] = 1
+    return True, np.linalg.inv(Nd) @ H @ Ns
+
+
+def _apply_h(H: np.ndarray, pts: np.ndarray) -> np.ndarray:
+    """ProjectiveTransform._apply_mat (_geometric.py:548-562)."""
+    x, y = np.transpose(pts)
+    q = np.vstack((x, y, np.ones_like(x))).T @ H.T
+    q[q[:, 2] == 0, 2] = np.finfo(float).eps
+    q[:, :2] /= q[:, 2:3]
+    return q[:, :2]
+
+
+def ransac_model(src, dst, model: str, trials: int = 1000, thresh: float = 2.0, seed: int = 42):
+    """skimage ransac(..., AffineTransform/ProjectiveTransform, min_samples=3/4, ...)
+    with the hypothesis loop in closed form (C) and skimage's own SVD refit on the
+    inliers.  src = frame keypoints, dst = template keypoints.  Returns (params [3,3]
+    (NaN if no model), inliers bool [N], best_trial, n_inliers)."""
+    src = np.ascontiguousarray(src, np.float64)
+    dst = np.ascontiguousarray(dst, np.float64)
+    n = src.shape[0]
+    ms = MODEL_MIN_SAMPLES[model]
+    hyp = np.ascontiguousarray(hypothesis_table(n, trials, seed, ms))
+    hm = np.empty(9, np.float64)
+    inl = np.zeros(max(n, 1), np.uint8)
+    bt = np.zeros(1, np.int32)
+    ni = np.zeros(1, np.int32)
+    rc = lib().kcmc_oracle_ransac_model(MODEL_IDS[model], _p(src), _p(dst), n, _p(hyp), trials, float(thresh),
+                                        _p(hm), _p(inl), _p(bt), _p(ni))
+    assert rc in (0, 1), rc
+    inliers = inl[:n].astype(bool)
+    if rc == 1:
+        return np.full((3, 3), np.nan), inliers, int(bt[0]), int(ni[0])
+    ok, H = estimate_tls(src[inliers], dst[inliers], model)
+    if H is None:  # refit degenerate: skimage keeps the hypothesis model
+        H = hm.reshape(3, 3).copy()
+    return H, inliers, int(bt[0]), int(ni[0])
+
+
+def ransac_model_skimage(src, dst, model: str, trials: int = 1000, thresh: float = 2.0, seed: int = 42):
+    """Operation-for-operation numpy restatement of skimage 0.18.3 ransac with
+    AffineTransform / ProjectiveTransform (fit.py:784-881; one SVD per trial).  Slow by
+    design: the reference-style CPU cost structure.  Returns (params [3,3], inliers)."""
+    rs = np.random.RandomState(seed)
+    n = len(src)
+    ms = MODEL_MIN_SAMPLES[model]
+    best_H, best_n, best_S, best_inl = None, 0, np.inf, None
+    spl = rs.choice(n, ms, replace=False)
+    for _ in range(trials):
+        s_src, s_dst = src[spl], dst[spl]
+        spl = rs.choice(n, ms, replace=False)
+        ok, H = estimate_tls(s_src, s_dst, model)
+        if not ok:
+            continue
+        r = np.abs(np.sqrt(np.sum((_apply_h(H, src) - dst) ** 2, axis=1)))
+        inl = r < thresh
+        S = np.sum(r ** 2)
+        ni = np.sum(inl)
+        if ni > best_n or (ni == best_n and S < best_S):
+            best_H, best_n, best_S, best_inl = H, ni, S, inl
+            if best_S <= 0:
+                break
+    if best_inl is not None and any(best_inl):
+        ok, H = estimate_tls(src[best_inl], dst[best_inl], model)
+        return (best_H if H is None else H), best_inl
+    return np.full((3, 3), np.nan), None
+
+
 # --------------------------------------------------------------------------- K3
 def invert_affine(M: np.ndarray) -> np.ndarray:
     M = np.ascontiguousarray(M, np.float64).reshape(6)
@@ -264,3 +383,26 @@ def warp_affine_u16(img: np.ndarray, M: np.ndarray, dsize=None, inverse_map: boo
 def pairwise_sum(a: np.ndarray) -> float:
     a = np.ascontiguousarray(a, np.float64)
     return lib().kcmc_oracle_pairwise_sum(_p(a), a.size)
+
+
+# ------------------------------------------------------------ K3 extension: perspective
+def invert_perspective(M: np.ndarray) -> np.ndarray:
+    """cv::invert of a 3x3 double matrix (OpenCV's closed-form 3x3 branch)."""
+    M9 = np.ascontiguousarray(M, np.float64).reshape(9)
+    out = np.empty(9, np.float64)
+    lib().kcmc_oracle_invert_perspective(_p(M9), _p(out))
+    return out.reshape(3, 3)
+
+
+def warp_perspective_u16(img: np.ndarray, M: np.ndarray, dsize=None, inverse_map: bool = False) -> np.ndarray:
+    """OpenCV ``warpPerspective(img, M, dsize, INTER_LINEAR)`` on uint16, border 0
+    (classic WarpPerspectiveInvoker + remapBilinear arithmetic)."""
+    src = np.ascontiguousarray(img, np.uint16)
+    H, W = src.shape[:2]
+    C = 1 if src.ndim == 2 else src.shape[2]
+    dW, dH = (W, H) if dsize is None else dsize
+    out = np.empty((dH, dW) + (() if src.ndim == 2 else (C,)), np.uint16)
+    M9 = np.ascontiguousarray(M, np.float64).reshape(9)
+    rc = lib().kcmc_oracle_warp_perspective_u16(_p(src), H, W, C, _p(M9), int(inverse_map), _p(out), dH, dW)
+    assert rc == 0
+    return out

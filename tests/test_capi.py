@@ -51,4 +51,8 @@ def test_launch_entry_points_validate_before_touching_the_gpu():
                                None) == _lib.KCMC_EINVAL
     assert L.kcmc_ransac_prepare(None, None, 1, 1000, 42) == _lib.KCMC_EINVAL
     assert L.kcmc_consensus(None, -1, 0, 0, 0, None, None, None, None, None) == _lib.KCMC_EINVAL
+    assert L.kcmc_ransac_model(None, 1, None, None, None, None, 0, 1, 10, 1000, 2.0, 1.0, 3, None, None, None,
+                               None, None) == _lib.KCMC_EINVAL
+    assert L.kcmc_ransac_prepare_samples(None, 3, None, 1, 1000, 42) == _lib.KCMC_EINVAL
+    assert L.kcmc_warp_perspective_u16(None, None, None, None, 1, 4, 4, 1, 0, None) == _lib.KCMC_EINVAL
     del P

@@ -1,0 +1,183 @@
+"""Parity of the affine / projective RANSAC and warpPerspective kernels (the extension
+behind BASELINE configs 3-5) with scikit-image 0.18.3 goldens and the CPU oracle.
+Inlier sets / winning trials bit-exact; parameters within 1e-4 relative (north_star;
+observed ~1e-10); warped pixels bit-exact to the oracle."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import load_golden
+from kcmc_amd import stages, synthetic
+
+pytestmark = pytest.mark.gpu
+MODELS = ["affine", "projective"]
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _csr(lists):
+    off = np.zeros(len(lists) + 1, np.int32)
+    off[1:] = np.cumsum([len(x) for x in lists])
+    return off
+
+
+def _run(dev, model, tpls, qs, rate=1.0, trials=1000, n_skip=3):
+    off = _csr(qs)
+    r = stages.ransac_model(_t(np.concatenate(qs).reshape(-1, 2), dev), _t(np.concatenate(tpls).reshape(-1, 2), dev),
+                            _t(off, dev), off, model=model, trials=trials, spatial_rate=rate, n_skip=n_skip)
+    return (off, r.params.cpu().numpy(), r.inliers.cpu().numpy().astype(bool), r.n_inliers.cpu().numpy(),
+            r.best_trial.cpu().numpy())
+
+
+@pytest.mark.parametrize("model", MODELS)
+def test_ransac_model_vs_skimage_golden(dev, model):
+    g = load_golden("ransac_models_golden.npz")
+    off = g[f"{model}_offsets"]
+    F = len(off) - 1
+    tpls = [g[f"{model}_kp_template"][off[f]:off[f + 1]] for f in range(F)]
+    qs = [g[f"{model}_kp_query"][off[f]:off[f + 1]] for f in range(F)]
+    o2, params, inl, nin, _ = _run(dev, model, tpls, qs)
+    for f in range(F):
+        ref = g[f"{model}_params"][f]
+        if np.isnan(ref).any():
+            assert np.isnan(params[f]).all(), f
+            continue
+        np.testing.assert_allclose(params[f], ref, rtol=1e-4, atol=1e-6, err_msg=str(f))
+        np.testing.assert_allclose(params[f], ref, rtol=1e-6, atol=1e-8, err_msg=str(f))
+        assert np.array_equal(inl[o2[f]:o2[f + 1]], g[f"{model}_inliers"][off[f]:off[f + 1]]), f
+        assert nin[f] == g[f"{model}_n_inliers"][f], f
+
+
+def _frames(rng, model, Ns):
+    tpls, qs = [], []
+    for N in Ns:
+        tpl = rng.uniform(0, 1000, (N, 2))
+        Hm = np.eye(3)
+        Hm[:2, :2] += rng.normal(0, 0.01, (2, 2))
+        Hm[:2, 2] = rng.normal(0, 5, 2)
+        if model == "projective":
+            Hm[2, :2] = rng.normal(0, 1e-5, 2)
+        q = oracle._apply_h(np.linalg.inv(Hm), tpl) + rng.normal(0, rng.uniform(0.1, 1.5), (N, 2))
+        out = rng.random(N) < rng.uniform(0, 0.6)
+        q[out] = rng.uniform(0, 1000, (int(out.sum()), 2))
+        tpls.append(tpl.astype(np.float32).astype(np.float64))
+        qs.append(q.astype(np.float32).astype(np.float64))
+    return tpls, qs
+
+
+@pytest.mark.parametrize("model", MODELS)
+def test_ransac_model_bit_exact_selection_vs_oracle(dev, model):
+    """Same hypotheses and arithmetic as the C oracle -> identical winning trial and
+    inlier set, including N > 128 (numpy's recursive pairwise order)."""
+    rng = np.random.default_rng(71 if model == "affine" else 72)
+    Ns = [5, 6, 8, 9, 20, 50, 100, 127, 128, 129, 136, 200, 256, 257, 300, 500, 1024]
+    tpls, qs = _frames(rng, model, Ns)
+    off, params, inl, nin, best = _run(dev, model, tpls, qs)
+    for f in range(len(qs)):
+        p, i_ref, bt, ni = oracle.ransac_model(qs[f], tpls[f], model)
+        assert best[f] == bt, f
+        assert nin[f] == ni, f
+        assert np.array_equal(inl[off[f]:off[f + 1]], i_ref), f
+        np.testing.assert_allclose(params[f], p, rtol=1e-8, atol=1e-9, err_msg=str(f))
+
+
+@pytest.mark.parametrize("model", MODELS)
+def test_ransac_model_skips_degenerate_and_scales(dev, model):
+    rng = np.random.default_rng(73)
+    tpl = rng.uniform(0, 100, (12, 2))
+    same = np.repeat(tpl[:1], 12, 0)
+    ms = 3 if model == "affine" else 4
+    tpls = [tpl, tpl[:2], tpl[:0], tpl]
+    qs = [same, tpl[:2] + 1, tpl[:0], tpl - 3.0]
+    off, params, inl, nin, best = _run(dev, model, tpls, qs, rate=2.0)
+    assert np.isnan(params[0]).all() and nin[0] == 0 and best[0] == -1
+    assert np.isnan(params[1]).all() and np.isnan(params[2]).all()  # N < N_KP_FRAME_SKIP
+    expect = np.array([[1, 0, 6.0], [0, 1, 6.0], [0, 0, 1]])  # translation 3 * spatial rate 2
+    np.testing.assert_allclose(params[3], expect, atol=1e-8)
+    with pytest.raises(ValueError):  # skimage: min_samples must be < number of samples
+        _run(dev, model, [tpl[:ms]], [tpl[:ms] + 1])
+
+
+@pytest.mark.parametrize("model", MODELS)
+def test_ransac_model_gather_mode_matches_contiguous(dev, model):
+    rng = np.random.default_rng(74)
+    n_tpl, F = 80, 6
+    n_skip = 5 if model == "projective" else 4
+    kp_tpl = rng.uniform(0, 500, (n_tpl, 2))
+    kp_ord = kp_tpl[None] * 1.01 + rng.normal(0, 0.5, (F, n_tpl, 2)) + 2.0
+    lists = [rng.permutation(n_tpl)[: int(rng.integers(0, 60))].astype(np.int32) for _ in range(F)]
+    off = _csr(lists)
+    r = stages.ransac_model(_t(kp_ord.reshape(-1, 2), dev), _t(kp_tpl, dev), _t(off, dev), off, model=model,
+                            pt_idx=_t(np.concatenate(lists), dev), src_frame_stride=n_tpl, n_skip=n_skip)
+    _, p2, _, _, _ = _run(dev, model, [kp_tpl[L] for L in lists], [kp_ord[f][L] for f, L in enumerate(lists)],
+                          n_skip=n_skip)
+    np.testing.assert_array_equal(r.params.cpu().numpy(), p2)
+
+
+# ------------------------------------------------------------------ warpPerspective
+def _homographies(rng, F, H, W):
+    Ms = []
+    for _ in range(F):
+        Hm = np.eye(3)
+        Hm[:2, :2] += rng.normal(0, 0.02, (2, 2))
+        Hm[:2, 2] = rng.normal(0, 6, 2)
+        Hm[2, :2] = rng.normal(0, 1e-2 / max(H, W), 2)
+        Ms.append(Hm)
+    return np.stack(Ms)
+
+
+@pytest.mark.parametrize("shape", [(1, 5, 7), (3, 64, 128), (2, 67, 131), (2, 130, 257), (1, 1080, 1920)])
+def test_warp_perspective_matches_oracle(dev, shape):
+    F, H, W = shape
+    rng = np.random.default_rng(H * W + 1)
+    imgs = rng.integers(0, 65536, shape).astype(np.uint16)
+    Ms = _homographies(rng, F, H, W)
+    out = stages.warp_perspective_u16(_t(imgs, dev), _t(Ms, dev)).cpu().numpy()
+    for f in range(F):
+        assert np.array_equal(out[f], oracle.warp_perspective_u16(imgs[f], Ms[f])), f
+
+
+def test_warp_perspective_extreme_maps_and_inverse(dev):
+    """Horizon inside the frame (denominator changes sign -> direct gather), singular
+    map, strong zoom, frames far outside, and WARP_INVERSE_MAP."""
+    rng = np.random.default_rng(81)
+    H, W = 200, 300
+    img = rng.integers(0, 65536, (H, W)).astype(np.uint16)
+    Ms = [np.eye(3), np.array([[1, 0.1, 5], [0.02, 1, -3], [0.004, 0.001, 1.0]]),
+          np.zeros((3, 3)), np.array([[2.5, 0, -100], [0, 2.5, -80], [0, 0, 1.0]]),
+          np.array([[1, 0, 5000], [0, 1, 0], [0, 0, 1.0]]),
+          np.array([[0.9, 0.05, 3], [-0.04, 1.1, 2], [-2e-4, 1e-4, 1]])]
+    imgs = np.broadcast_to(img, (len(Ms), H, W)).copy()
+    for inv in (False, True):
+        out = stages.warp_perspective_u16(_t(imgs, dev), _t(np.stack(Ms), dev), inverse_map=inv).cpu().numpy()
+        for f, M in enumerate(Ms):
+            assert np.array_equal(out[f], oracle.warp_perspective_u16(img, M, inverse_map=inv)), (f, inv)
+    assert np.array_equal(out[0], img)
+
+
+@pytest.mark.parametrize("C", [3, 4])
+def test_warp_perspective_multichannel(dev, C):
+    rng = np.random.default_rng(90 + C)
+    imgs = rng.integers(0, 65536, (2, 60, 90, C)).astype(np.uint16)
+    Ms = _homographies(rng, 2, 60, 90)
+    out = stages.warp_perspective_u16(_t(imgs, dev), _t(Ms, dev)).cpu().numpy()
+    for f in range(2):
+        assert np.array_equal(out[f], oracle.warp_perspective_u16(imgs[f], Ms[f]))
+
+
+def test_warp_perspective_of_affine_close_to_affine_path(dev):
+    """An affine homography through warpPerspective differs from warpAffine only by the
+    coordinate rounding (double per pixel vs 1/1024 fixed point): at most a 1/32-px tap
+    shift, i.e. a few LSB on a smooth ramp."""
+    H, W = 120, 160
+    yy, xx = np.mgrid[0:H, 0:W]
+    img = (20000 + 50 * xx + 30 * yy).astype(np.uint16)
+    A = synthetic.rigid(0.01, 3.3, -2.1)
+    Hm = np.vstack([A, [0, 0, 1]])
+    a = stages.warp_affine_u16(_t(img[None], dev), _t(A[None], dev)).cpu().numpy()[0].astype(int)
+    p = stages.warp_perspective_u16(_t(img[None], dev), _t(Hm[None], dev)).cpu().numpy()[0].astype(int)
+    inner = (slice(8, H - 8), slice(8, W - 8))
+    assert np.abs(a[inner] - p[inner]).max() <= 8
