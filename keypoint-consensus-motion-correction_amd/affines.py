@@ -81,9 +81,41 @@ def interpolate_affines(affines: np.ndarray) -> Tuple[np.ndarray, List[int]]:
     return aff, interpolated
 
 
+def interpolate_linear(maps: np.ndarray) -> Tuple[np.ndarray, List[int]]:
+    """Gap filling for the extension models (affine [n, 2, 3], projective [n, 3, 3]):
+    the reference's edge-fill and reporting rules (VA:347-407) with entry-wise linear
+    interpolation inside gaps (its arccos/arcsin lerp, VA:423-436, assumes rotation
+    entries and returns NaN for scaled matrices)."""
+    m = np.array(maps, dtype=np.float64, copy=True)
+    n = len(m)
+    missing = np.isnan(m.reshape(n, -1)).any(axis=1)
+    if not missing.any():
+        return m, []
+    if missing.all():
+        raise AlignmentError(
+            "No transformations were calculated because too few keypoints were identified "
+            "(probably because too few keypoints were identified)"
+        )
+    present = np.flatnonzero(~missing)
+    interpolated: List[int] = []
+    first = int(present[0])
+    if first > 0:
+        m[:first] = m[first]
+        interpolated += list(range(first))
+    for g in np.flatnonzero(np.diff(present) > 1):
+        lo, hi = int(present[g]), int(present[g + 1])
+        t = (np.arange(lo + 1, hi, dtype=np.float64) - lo) / float(hi - lo)
+        m[lo + 1 : hi] = m[lo][None] + (m[hi] - m[lo])[None] * t[:, None, None]
+        interpolated += list(range(lo + 1, hi))
+    last = int(present[-1])
+    if last < n - 1:
+        m[last + 1 :] = m[last]
+    return m, interpolated
+
+
 def euclidean_transforms(affines: np.ndarray) -> np.ndarray:
     """VA:440-453: [x_translation, y_translation, arccos(a00)] per frame."""
     t = np.zeros((affines.shape[0], 3))
-    t[:, :2] = affines[:, :, 2]
+    t[:, :2] = affines[:, :2, 2]
     t[:, 2] = np.arccos(affines[:, 0, 0])
     return t

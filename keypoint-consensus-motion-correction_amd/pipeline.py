@@ -36,6 +36,17 @@ class AlignConfig:
     seed: int = 42                      # RANDOM_SEED
     spatial_rate: float = 1             # SPATIAL_DOWNSAMPLE_RATE
     frame_downsample_rate: int = 1      # max(1, frame_rate // FRAME_SAMPLE_RATE)
+    # Extension (BASELINE configs 3-5): the skimage model class RANSAC fits.  The
+    # reference always uses "euclidean" (EuclideanTransform, VA:311).
+    ransac_model: str = "euclidean"     # "euclidean" | "affine" | "projective"
+
+    @property
+    def effective_frame_skip(self) -> int:
+        """Frames with fewer points get NaN: N_KP_FRAME_SKIP, raised to min_samples + 1
+        for the extension models (skimage needs min_samples < N, fit.py:798)."""
+        if self.ransac_model == "euclidean":
+            return self.n_kp_frame_skip
+        return max(self.n_kp_frame_skip, {"affine": 3, "projective": 4}[self.ransac_model] + 1)
 
 
 @dataclass
@@ -102,27 +113,50 @@ def consensus_stage(keep_bits_host: np.ndarray, n_tpl: int, n_frames: int, cfg: 
 
 def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.Consensus,
                  cfg: AlignConfig) -> stages.RansacResult:
+    """VA:137-142: RANSAC of every frame's consensus points (src = the frame's matched
+    keypoints, dst = template keypoints).  params [F, 2, 3] for the euclidean and
+    affine models (model.params[:2], like VA:319), [F, 3, 3] for the projective one."""
     dev = kp_tpl.device
     F, n_tpl = match.kp_ordered.shape[:2]
     pt_off = torch.from_numpy(cons.pt_off).to(dev, non_blocking=False)
     pt_idx = torch.from_numpy(cons.pt_idx if cons.pt_idx.size else np.zeros(1, np.int32)).to(dev)
-    return stages.ransac_rigid(match.kp_ordered.view(F * n_tpl, 2), kp_tpl, pt_off, cons.pt_off, pt_idx=pt_idx,
-                               src_frame_stride=n_tpl, trials=cfg.ransac_trials,
-                               residual_threshold=cfg.ransac_threshold, spatial_rate=cfg.spatial_rate,
-                               n_skip=cfg.n_kp_frame_skip, seed=cfg.seed, min_samples=cfg.ransac_min_samples)
+    if cfg.ransac_model == "euclidean":
+        return stages.ransac_rigid(match.kp_ordered.view(F * n_tpl, 2), kp_tpl, pt_off, cons.pt_off, pt_idx=pt_idx,
+                                   src_frame_stride=n_tpl, trials=cfg.ransac_trials,
+                                   residual_threshold=cfg.ransac_threshold, spatial_rate=cfg.spatial_rate,
+                                   n_skip=cfg.n_kp_frame_skip, seed=cfg.seed, min_samples=cfg.ransac_min_samples)
+    rr = stages.ransac_model(match.kp_ordered.view(F * n_tpl, 2), kp_tpl, pt_off, cons.pt_off, model=cfg.ransac_model,
+                             pt_idx=pt_idx, src_frame_stride=n_tpl, trials=cfg.ransac_trials,
+                             residual_threshold=cfg.ransac_threshold, spatial_rate=cfg.spatial_rate,
+                             n_skip=cfg.effective_frame_skip, seed=cfg.seed)
+    if cfg.ransac_model == "affine":
+        rr.params = rr.params[:, :2].contiguous()
+    return rr
 
 
 def postprocess_affines(params_host: np.ndarray, cfg: AlignConfig):
-    """VA:143-145 on the host: NaN-pad, interpolate, Euclidean summary."""
+    """VA:143-145 on the host: NaN-pad, interpolate, Euclidean summary.  The
+    reference's rotation-angle lerp (VA:409-437) assumes rigid matrices; the extension
+    models interpolate their gaps entry-wise linearly instead."""
     affines, skipped = _aff.process_affines(np.asarray(params_host), cfg.frame_downsample_rate)
-    affines, interpolated = _aff.interpolate_affines(affines)
+    if cfg.ransac_model == "euclidean":
+        affines, interpolated = _aff.interpolate_affines(affines)
+    else:
+        affines, interpolated = _aff.interpolate_linear(affines)
     return affines, skipped, interpolated, _aff.euclidean_transforms(affines)
+
+
+def warp_frames(frames: torch.Tensor, maps: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """VA:150 on the device: warpAffine for [F, 2, 3] maps, warpPerspective for [F, 3, 3]."""
+    if maps.shape[1:] == (3, 3):
+        return stages.warp_perspective_u16(frames, maps, out=out)
+    return stages.warp_affine_u16(frames, maps, out=out)
 
 
 def warp_stage(frames: torch.Tensor, affines: np.ndarray, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     F = frames.shape[0]
     a = torch.from_numpy(np.ascontiguousarray(affines[:F], dtype=np.float64)).to(frames.device)
-    return stages.warp_affine_u16(frames, a, out=out)
+    return warp_frames(frames, a, out=out)
 
 
 def align_slab(inp: SlabInputs, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
@@ -221,7 +255,7 @@ class OverlappedSlabs:
             a = torch.from_numpy(np.ascontiguousarray(affines[f0:f0 + inp.frames.shape[0]], dtype=np.float64))
             a = a.pin_memory().to(self.dev, non_blocking=True)
             mark("w0")
-            aligned = stages.warp_affine_u16(inp.frames, a, out=out)
+            aligned = warp_frames(inp.frames, a, out=out)
             mark("w1")
             done = torch.cuda.Event()
             done.record(self.warp)

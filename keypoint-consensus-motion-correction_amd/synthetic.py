@@ -30,12 +30,38 @@ class KeypointSet:
     gt: np.ndarray          # [F, 2, 3] frame->template rigid maps used to place the points
 
 
+def ground_truth(rng: np.random.Generator, model: str, jitter: float, rot_deg: float,
+                 size_hw: Tuple[int, int]) -> np.ndarray:
+    """A frame -> template map (SURVEY 8d): rigid jitter N(0, jitter px), N(0, rot_deg);
+    "affine" adds +-1 % scale/shear; "projective" adds perspective terms ~1e-5 / px
+    (scaled to the frame size) and is returned as [3, 3]."""
+    A = rigid(np.deg2rad(rng.normal(0, rot_deg)), rng.normal(0, jitter), rng.normal(0, jitter))
+    if model == "euclidean":
+        return A
+    A[:, :2] = A[:, :2] @ (np.eye(2) + rng.uniform(-0.01, 0.01, (2, 2)))
+    if model == "affine":
+        return A
+    Hm = np.vstack([A, [0.0, 0.0, 1.0]])
+    Hm[2, :2] = rng.normal(0, 1e-5 * 512.0 / max(size_hw), 2)
+    return Hm
+
+
+def apply_map(M: np.ndarray, pts: np.ndarray) -> np.ndarray:
+    """Apply a [2, 3] affine or [3, 3] projective map to points [n, 2]."""
+    q = pts @ M[:2, :2].T + M[:2, 2]
+    if M.shape == (3, 3):
+        w = pts @ M[2, :2] + M[2, 2]
+        q = q / w[:, None]
+    return q
+
+
 def make_keypoints(n_frames: int, n_tpl: int, D: int, size_hw: Tuple[int, int], seed: int = 3,
                    jitter: float = 4.0, rot_deg: float = 0.5, noise: float = 0.3, drop: float = 0.1,
                    distract: float = 0.2, perturb: int = 8, perturb_frac: float = 0.25,
-                   frame_seed: Optional[int] = None) -> KeypointSet:
+                   frame_seed: Optional[int] = None, model: str = "euclidean") -> KeypointSet:
     """``seed`` fixes the template; ``frame_seed`` (e.g. a rank) draws an independent
-    slab of frames against that same template."""
+    slab of frames against that same template; ``model`` picks the ground-truth motion
+    family (gt is [F, 2, 3], or [F, 3, 3] for "projective")."""
     rng = np.random.default_rng(seed)
     H, W = size_hw
     kp_tpl = np.stack([rng.uniform(0, W, n_tpl), rng.uniform(0, H, n_tpl)], 1).astype(np.float32).astype(np.float64)
@@ -46,10 +72,18 @@ def make_keypoints(n_frames: int, n_tpl: int, D: int, size_hw: Tuple[int, int], 
     kps, dess, counts, gts = [], [], [], []
     for f in range(n_frames):
         # frame -> template map A (what RANSAC recovers); frame points = A^-1(template points)
-        A = rigid(np.deg2rad(rng.normal(0, rot_deg)), rng.normal(0, jitter), rng.normal(0, jitter))
-        R, t = A[:, :2], A[:, 2]
+        if model == "euclidean":
+            A = rigid(np.deg2rad(rng.normal(0, rot_deg)), rng.normal(0, jitter), rng.normal(0, jitter))
+        else:
+            A = ground_truth(rng, model, jitter, rot_deg, size_hw)
         keep = rng.random(n_tpl) >= drop
-        pts = (kp_tpl[keep] - t) @ R + rng.normal(0, noise, (int(keep.sum()), 2))
+        if model == "euclidean":  # rigid inverse (kept bit-identical to earlier rounds' fixtures)
+            R, t = A[:, :2], A[:, 2]
+            pts = (kp_tpl[keep] - t) @ R
+        else:
+            Ah = A if A.shape == (3, 3) else np.vstack([A, [0.0, 0.0, 1.0]])
+            pts = apply_map(np.linalg.inv(Ah), kp_tpl[keep])
+        pts = pts + rng.normal(0, noise, (int(keep.sum()), 2))
         des = des_tpl[keep].astype(np.int16)
         m = rng.random(des.shape) < perturb_frac
         des[m] += rng.integers(-perturb, perturb + 1, int(m.sum()), dtype=np.int16)

@@ -78,6 +78,11 @@ class VideoAligner:
     RANDOM_SEED = 42
     # New: which GPU runs the hot path (None = torch's current device).
     DEVICE: Optional[int] = None
+    # New (extension, BASELINE configs 3-5): the skimage model class RANSAC fits --
+    # "euclidean" (the reference's EuclideanTransform, VA:311), "affine"
+    # (AffineTransform, min_samples 3) or "projective" (ProjectiveTransform, min_samples 4,
+    # frames warped with warpPerspective).
+    RANSAC_MODEL = "euclidean"
 
     def __init__(self, logger: LoggerAdapter = None):
         self.logger = logger
@@ -107,7 +112,7 @@ class VideoAligner:
             ratio=cls.DESCRIPTOR_DISTANCE_RATIO_THRESH, d_lo=d_lo, d_hi=d_hi, ransac_trials=cls.RANSAC_MAX_TRIALS,
             ransac_threshold=float(cls.RANSAC_RESIDUAL_THRESH), ransac_min_samples=cls.RANSAC_MIN_SAMPLES,
             seed=cls.RANDOM_SEED, spatial_rate=cls.SPATIAL_DOWNSAMPLE_RATE,
-            frame_downsample_rate=int(frame_downsample_rate))
+            frame_downsample_rate=int(frame_downsample_rate), ransac_model=cls.RANSAC_MODEL)
 
     # ------------------------------------------------------------- public API
     def align_images(

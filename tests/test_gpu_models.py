@@ -181,3 +181,57 @@ def test_warp_perspective_of_affine_close_to_affine_path(dev):
     p = stages.warp_perspective_u16(_t(img[None], dev), _t(Hm[None], dev)).cpu().numpy()[0].astype(int)
     inner = (slice(8, H - 8), slice(8, W - 8))
     assert np.abs(a[inner] - p[inner]).max() <= 8
+
+
+# ------------------------------------------------------------------ whole slab
+@pytest.mark.parametrize("model", MODELS)
+def test_slab_end_to_end_with_model(dev, model):
+    """match -> consensus -> affine/projective RANSAC -> gap filling -> warp, checked
+    frame by frame against the oracle (RANSAC on the same consensus point lists, warp of
+    the resulting maps)."""
+    from kcmc_amd import pipeline
+
+    F, H, W = 12, 256, 320
+    ks = synthetic.make_keypoints(F, 300, 61, (H, W), seed=11, model=model)
+    base = synthetic.make_texture((H, W), seed=12)
+    frames = torch.from_numpy(np.broadcast_to(base, (F, H, W)).copy()).to(dev)
+    inp = pipeline.SlabInputs(frames, _t(ks.des_tpl, dev), _t(ks.kp_tpl, dev), _t(ks.des_q, dev), _t(ks.kp_q, dev),
+                              _t(ks.q_off, dev), ks.q_off)
+    cfg = pipeline.AlignConfig(n_kp_global=60, ransac_model=model)
+    res = pipeline.align_slab(inp, cfg, keep_intermediates=True)
+    torch.cuda.synchronize()
+    kq = res.match.kp_ordered.cpu().numpy()
+    po, pi = res.consensus.pt_off, res.consensus.pt_idx
+    out = res.aligned.cpu().numpy()
+    assert res.affines.shape[1:] == ((2, 3) if model == "affine" else (3, 3))
+    n_fit = 0
+    for f in range(F):
+        L = pi[po[f]:po[f + 1]]
+        p, _, _, _ = oracle.ransac_model(kq[f][L], ks.kp_tpl[L], model)
+        if model == "affine":
+            p = p[:2]
+        if not np.isnan(p).any():
+            n_fit += 1
+            np.testing.assert_allclose(res.affines[f], p, rtol=1e-6, atol=1e-8, err_msg=str(f))
+            # the recovered map is the ground truth up to the keypoint noise
+            assert np.abs(res.affines[f][:2, 2] - ks.gt[f][:2, 2]).max() < 1.0
+        ref = (oracle.warp_affine_u16(base, res.affines[f]) if model == "affine"
+               else oracle.warp_perspective_u16(base, res.affines[f]))
+        assert np.array_equal(out[f], ref), f
+    assert n_fit == F
+
+
+def test_video_aligner_model_selector(dev):
+    from kcmc_amd import VideoAligner
+
+    class AffineAligner(VideoAligner):
+        RANSAC_MODEL = "affine"
+
+    F, H, W = 6, 128, 160
+    ks = synthetic.make_keypoints(F, 200, 32, (H, W), seed=13, model="affine")
+    imgs = np.broadcast_to(synthetic.make_texture((H, W), seed=14), (F, H, W)).copy()
+    kps = [ks.kp_q[ks.q_off[f]:ks.q_off[f + 1]] for f in range(F)]
+    des = [ks.des_q[ks.q_off[f]:ks.q_off[f + 1]] for f in range(F)]
+    aligned, eu, skipped = AffineAligner().align_keypoints(imgs, ks.kp_tpl, ks.des_tpl, kps, des, n_kp_global=50)
+    assert aligned.shape == imgs.shape and eu.shape == (F, 3) and skipped == []
+    np.testing.assert_allclose(eu[:, :2], ks.gt[:, :, 2], atol=1.0)
