@@ -23,6 +23,7 @@ import json
 import os
 import sys
 import time
+from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -35,25 +36,64 @@ from kcmc_amd import distributed as kdist  # noqa: E402
 from kcmc_amd import pipeline, stages, synthetic  # noqa: E402
 
 METRIC = "aligned frames/sec (whole node) at 1080p; RANSAC hypotheses scored/sec/GPU"
-H, W = 1080, 1920
-N_TPL, D = 500, 32
-N_KP_GLOBAL = 100
-TRIALS = 1000
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+TRIALS = 1000
+
+
+@dataclass
+class BenchConfig:
+    name: str
+    workload: str
+    H: int
+    W: int
+    C: int
+    n_tpl: int
+    D: int
+    n_kp_global: int
+    model: str
+    frames_per_gpu: int
+    cpu_sample: int
+
+
+# BASELINE.json configs.  c2 (configs[1]) is the headline line; the others are the
+# extension workloads (affine / 4K RGB), reported with --config.  Frames per GPU are the
+# config's frame count divided over the 8 GPUs it names (weak scaling per GPU).
+CONFIGS = {
+    "c2": BenchConfig("c2", "BASELINE config[1]: 1080p grayscale u16, 2000 frames per GPU, ORB-like keypoints "
+                      "(n_tpl=500, D=32 B, ~550/frame), rigid RANSAC 1000 trials, n_kp_global=100",
+                      1080, 1920, 1, 500, 32, 100, "euclidean", 2000, 240),
+    "c3": BenchConfig("c3", "BASELINE config[2]: 512x512 two-photon-style u16, 20000 frames over 8 GPUs (2500 per GPU), "
+                      "n_tpl=500, D=61 B (AKAZE-sized), affine RANSAC 1000 trials, n_kp_global=50",
+                      512, 512, 1, 500, 61, 50, "affine", 2500, 60),
+    "c4": BenchConfig("c4", "BASELINE config[3]: 4K RGB u16 (2160x3840x3), 5000 frames over 8 GPUs (625 per GPU), "
+                      "4096 keypoints/frame template, D=61 B, affine RANSAC 1000 trials, n_kp_global=500",
+                      2160, 3840, 3, 4096, 61, 500, "affine", 625, 4),
+}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_inputs(frames_per_gpu: int, rank: int, dev: torch.device):
-    ks = synthetic.make_keypoints(frames_per_gpu, N_TPL, D, (H, W), seed=3, frame_seed=rank)
-    base = synthetic.make_texture((H, W), seed=0)
-    base_t = torch.from_numpy(base).to(dev)
-    src = base_t.expand(frames_per_gpu, H, W).contiguous()
+def make_texture(bc: BenchConfig) -> np.ndarray:
+    if bc.C == 1:
+        return synthetic.make_texture((bc.H, bc.W), seed=0)
+    return np.stack([synthetic.make_texture((bc.H, bc.W), seed=c) for c in range(bc.C)], axis=-1)
+
+
+def make_inputs(bc: BenchConfig, frames_per_gpu: int, rank: int, dev: torch.device):
+    ks = synthetic.make_keypoints(frames_per_gpu, bc.n_tpl, bc.D, (bc.H, bc.W), seed=3, frame_seed=rank,
+                                  model=bc.model)
+    base_t = torch.from_numpy(make_texture(bc)).to(dev)
+    src = base_t.expand((frames_per_gpu,) + tuple(base_t.shape)).contiguous()
+    gt = torch.from_numpy(ks.gt).to(dev)
     # jittered video: each frame is the base texture seen through the inverse of its
-    # ground-truth frame->template map (generated once, outside the timed region)
-    frames = stages.warp_affine_u16(src, torch.from_numpy(ks.gt).to(dev), inverse_map=True)
+    # ground-truth frame->template map (one launch, outside the timed region; the PMC
+    # summary skips this first warp dispatch)
+    if bc.model == "projective":
+        frames = stages.warp_perspective_u16(src, gt, inverse_map=True)
+    else:
+        frames = stages.warp_affine_u16(src, gt, inverse_map=True)
     del src
     inp = pipeline.SlabInputs(
         frames=frames,
@@ -122,21 +162,22 @@ def run_step(inp, cfg, out, timer=None, world=1, counts=None):
     a_dev = torch.from_numpy(np.ascontiguousarray(affines[: inp.frames.shape[0]])).to(inp.frames.device)
     if timer:
         timer.mark("w0")
-    stages.warp_affine_u16(inp.frames, a_dev, out=out)
+    pipeline.warp_frames(inp.frames, a_dev, out=out)
     if timer:
         timer.mark("w1")
     return cons, rr
 
 
-def cpu_baseline(ks, n_sample: int):
+def cpu_baseline(bc: BenchConfig, ks, n_sample: int):
     """The oracle restatement of the reference CPU path on a bounded sample (1 thread):
     C knnMatch + the reference's numpy filters, CPython consensus, the numpy/LAPACK
-    restatement of skimage 0.18.3 ransac (per-trial SVD, like the reference), C warpAffine."""
+    restatement of skimage 0.18.3 ransac (per-trial SVD, like the reference), C warp."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # cpu_baseline leg: the oracle is what is timed here
     from threadpoolctl import threadpool_limits
 
-    base = synthetic.make_texture((H, W), seed=0)
+    base = make_texture(bc)
+    skip = {"euclidean": 3, "affine": 4, "projective": 5}[bc.model]
     with threadpool_limits(1):
         t0 = time.perf_counter()
         sets, kqs = [], []
@@ -147,20 +188,27 @@ def cpu_baseline(ks, n_sample: int):
             sets.append(s)
             kqs.append(kq)
         t1 = time.perf_counter()
-        cons, _, _ = oracle.consensus(sets, N_KP_GLOBAL)
+        cons, _, _ = oracle.consensus(sets, bc.n_kp_global)
         lists = oracle.lookup(cons, sets)
         t2 = time.perf_counter()
         affs = []
         for f in range(n_sample):
             L = lists[f]
-            if len(L) < 3:
-                affs.append(np.full((2, 3), np.nan))
+            if len(L) < skip:
+                affs.append(np.full((2, 3) if bc.model != "projective" else (3, 3), np.nan))
                 continue
-            p, _ = oracle.ransac_rigid_skimage(kqs[f][L], ks.kp_tpl[L])
+            if bc.model == "euclidean":
+                p, _ = oracle.ransac_rigid_skimage(kqs[f][L], ks.kp_tpl[L])
+            else:
+                p, _ = oracle.ransac_model_skimage(kqs[f][L], ks.kp_tpl[L], bc.model)
+                p = p[:2] if bc.model == "affine" else p
             affs.append(p)
         t3 = time.perf_counter()
         for f in range(n_sample):
-            oracle.warp_affine_u16(base, affs[f])
+            if bc.model == "projective":
+                oracle.warp_perspective_u16(base, affs[f])
+            else:
+                oracle.warp_affine_u16(base, affs[f])
         t4 = time.perf_counter()
     total = t4 - t0
     return {
@@ -168,18 +216,21 @@ def cpu_baseline(ks, n_sample: int):
         "unit": "aligned frames/s",
         "cores": 1,
         "kind": "port",
-        "sample": (f"{n_sample} frames of config[1] (1080p u16, n_tpl=500, D=32, n_kp_global=100), 1 thread: "
+        "sample": (f"{n_sample} frames of {bc.name} ({bc.H}x{bc.W}x{bc.C} u16, n_tpl={bc.n_tpl}, D={bc.D}, "
+                   f"n_kp_global={bc.n_kp_global}, {bc.model}), 1 thread: "
                    f"match {1e3 * (t1 - t0) / n_sample:.1f} ms/frame (C oracle knnMatch + reference numpy filters), "
                    f"consensus {1e3 * (t2 - t1):.1f} ms (CPython set/Counter), "
                    f"RANSAC {1e3 * (t3 - t2) / n_sample:.1f} ms/frame (numpy/LAPACK restatement of skimage 0.18.3, "
-                   f"1000 trials), warp {1e3 * (t4 - t3) / n_sample:.1f} ms/frame (C oracle warpAffine)"),
+                   f"1000 trials), warp {1e3 * (t4 - t3) / n_sample:.1f} ms/frame (C oracle)"),
         "seconds": total,
     }
 
 
-def load_traffic():
-    """HBM bytes per warp launch from the committed rocprofv3 PMC pass, if present."""
-    p = os.path.join(REPO, "profiles", "warp_pmc_traffic.json")
+def load_traffic(config: str):
+    """HBM bytes per warp launch from the committed rocprofv3 PMC pass of this config
+    (tools/pmc_warp.sh + tools/pmc_summary.py), if present."""
+    name = "warp_pmc_traffic.json" if config == "c2" else f"warp_pmc_traffic_{config}.json"
+    p = os.path.join(REPO, "profiles", name)
     try:
         with open(p) as f:
             d = json.load(f)
@@ -193,11 +244,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--frames", type=int, default=2000, help="frames per GPU (config[1]: 2000)")
-    ap.add_argument("--cpu-sample", type=int, default=240, help="frames in the CPU-baseline sample (0: skip)")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
+                    help="BASELINE workload (c2 = configs[1], the headline line)")
+    ap.add_argument("--frames", type=int, default=None, help="frames per GPU (default: the config's)")
+    ap.add_argument("--cpu-sample", type=int, default=None, help="frames in the CPU-baseline sample (0: skip)")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
+    bc = CONFIGS[args.config]
+    if args.frames is None:
+        args.frames = bc.frames_per_gpu
+    if args.cpu_sample is None:
+        args.cpu_sample = bc.cpu_sample
 
     rank, world, local = kdist.init_from_env("nccl")
     if world != args.gpus:
@@ -205,11 +263,11 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     t_setup = time.perf_counter()
-    inp, ks = make_inputs(args.frames, rank, dev)
+    inp, ks = make_inputs(bc, args.frames, rank, dev)
     out = torch.empty_like(inp.frames)
-    cfg = pipeline.AlignConfig(n_kp_global=N_KP_GLOBAL)
+    cfg = pipeline.AlignConfig(n_kp_global=bc.n_kp_global, ransac_model=bc.model)
     counts = [args.frames] * world
-    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s; {args.frames} frames {H}x{W} on {dev}")
+    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s; {args.frames} frames {bc.H}x{bc.W}x{bc.C} on {dev}")
 
     ov = None if args.serial else pipeline.OverlappedSlabs(dev, cfg, counts=counts if world > 1 else None)
 
@@ -248,10 +306,10 @@ def main():
     n_pts = np.diff(cons.pt_off)
     if len(n_pts) > args.frames:  # overlapped multi-rank steps return the global consensus
         n_pts = n_pts[rank * args.frames:(rank + 1) * args.frames]
-    n_ransac = int((n_pts >= cfg.n_kp_frame_skip).sum())
+    n_ransac = int((n_pts >= cfg.effective_frame_skip).sum())
     warp_bytes = 2 * inp.frames.numel() * inp.frames.element_size()  # read + write, algorithmic
     achieved = warp_bytes / (warp_ms * 1e-3) / 1e9
-    traffic, _ = load_traffic()
+    traffic, _ = load_traffic(bc.name)
     stage_ms = {"match": round(match_ms, 3), "ransac": round(ransac_ms, 3), "warp": round(warp_ms, 3)}
     if ov is None:
         stage_ms["host_and_transfers"] = round(ms_step - match_ms - ransac_ms - warp_ms, 3)
@@ -272,16 +330,17 @@ def main():
         "dtype": "u16 frames; i8 MFMA match, f64 RANSAC, f32 warp weights",
         "data": "synthetic (seeded jittered 1080p texture + ORB-shaped keypoints; no detector in image)",
         "config": {
-            "workload": "BASELINE config[1]: 1080p grayscale u16, 2000 frames per GPU, ORB-like keypoints "
-                        "(n_tpl=500, D=32 B, ~550/frame), rigid RANSAC 1000 trials, n_kp_global=100",
-            "frames_per_gpu": args.frames, "height": H, "width": W, "n_tpl": N_TPL, "descriptor_bytes": D,
-            "n_kp_global": N_KP_GLOBAL, "ransac_trials": TRIALS, "parallelism": f"frame-sharded x{world}",
+            "workload": bc.workload,
+            "frames_per_gpu": args.frames, "height": bc.H, "width": bc.W, "channels": bc.C, "n_tpl": bc.n_tpl,
+            "descriptor_bytes": bc.D, "n_kp_global": bc.n_kp_global, "ransac_model": bc.model,
+            "ransac_trials": TRIALS, "parallelism": f"frame-sharded x{world}",
         },
         "ransac_hypotheses_per_s_per_gpu": round(n_ransac * TRIALS / (ransac_ms * 1e-3), 1),
         "ransac_mean_points": round(float(n_pts.mean()), 2),
         "stage_ms": stage_ms,
         "roofline": {
-            "kernel": "warp_affine_u16_kernel<1>",
+            "kernel": (f"warp_perspective_u16_kernel<{bc.C}>" if bc.model == "projective"
+                       else f"warp_affine_u16_kernel<{bc.C}>"),
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
@@ -293,7 +352,7 @@ def main():
         },
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        result["cpu_baseline"] = cpu_baseline(ks, args.cpu_sample)
+        result["cpu_baseline"] = cpu_baseline(bc, ks, args.cpu_sample)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -1,17 +1,19 @@
 #!/bin/bash
 # PMC passes for the dominant kernel (warp) of bench.py, one rocprofv3 run per counter
 # group (rocprofv3 does not split counters over passes).  Run on the GPU box from the
-# repo root:  bash tools/pmc_warp.sh <out_dir> [kernel_regex]
+# repo root:  bash tools/pmc_warp.sh <out_dir> [kernel_regex] [bench args...]
 set -u
 OUT=${1:-gpurun_out/pmc}
 RE=${2:-warp_affine}
+shift 2 2>/dev/null
+EXTRA=("$@")
 R=$PWD
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$R"
 run() {  # name, counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --kernel-include-regex "$RE" --pmc "$@" --output-format csv \
-    -d "$R/$OUT/$name" -o run -- python bench.py --steps 2 --warmup 1 --cpu-sample 0 \
+    -d "$R/$OUT/$name" -o run -- python bench.py --steps 2 --warmup 1 --cpu-sample 0 "${EXTRA[@]}" \
     > "$OUT/$name.json" 2> "$OUT/$name.err"
   local rc=$?
   echo "pass $name rc=$rc"
