@@ -95,6 +95,22 @@ int kcmc_match_frames(kcmc_ctx* ctx, const uint8_t* des_tpl_dev, const double* k
                       double* out_kp_ordered_dev, uint32_t* out_keep_bits_dev,
                       int32_t* out_counts_dev, kcmc_stream_t stream);
 
+/* -------------------------------------------------- K1 extension: float descriptors
+ * BFMatcher(NORM_L2).knnMatch(k=2) on float32 descriptors (BASELINE config 5,
+ * SIFT-style; the reference's AKAZE/BRISK descriptors are uint8, VA:22-25).  Distance:
+ * dist = sqrtf((float)sum_k ((double)a_k - (double)b_k)^2) (sequential fp64 sum; OpenCV's
+ * own float accumulation order is build-dependent), ties to the lower
+ * frame index.  1 <= D <= 128.  Arguments as kcmc_knn2_l2u8 / kcmc_match_frames. */
+int kcmc_knn2_l2f32(kcmc_ctx* ctx, const float* des_tpl_dev, int n_tpl, int D, const float* des_q_dev,
+                    const int32_t* q_off_dev, int n_frames, int max_nq, int32_t* out_idx_dev,
+                    float* out_dist_dev, kcmc_stream_t stream);
+int kcmc_match_frames_f32(kcmc_ctx* ctx, const float* des_tpl_dev, const double* kp_tpl_dev, int n_tpl,
+                          int D, const float* des_q_dev, const double* kp_q_dev,
+                          const int32_t* q_off_dev, int n_frames, int max_nq, double ratio,
+                          double d_lo, double d_hi, int32_t* out_idx_dev, float* out_dist_dev,
+                          double* out_kp_ordered_dev, uint32_t* out_keep_bits_dev,
+                          int32_t* out_counts_dev, kcmc_stream_t stream);
+
 /* ------------------------------------------------------- host: keypoint consensus
  * VA:224-286 on the host, reproducing CPython 3 set/Counter iteration order exactly:
  *   keep_bits_host [n_frames, ceil(n_tpl/32)] u32 (output of kcmc_match_frames)

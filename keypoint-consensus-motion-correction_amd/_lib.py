@@ -28,6 +28,8 @@ EXPORTED_SYMBOLS = (
     "kcmc_destroy",
     "kcmc_knn2_l2u8",
     "kcmc_match_frames",
+    "kcmc_knn2_l2f32",
+    "kcmc_match_frames_f32",
     "kcmc_consensus",
     "kcmc_hypothesis_table",
     "kcmc_ransac_prepare",
@@ -71,6 +73,8 @@ _SIGNATURES = {
     "kcmc_destroy": ([P], I),
     "kcmc_knn2_l2u8": ([P, P, I, I, P, P, I, I, P, P, P], I),
     "kcmc_match_frames": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
+    "kcmc_knn2_l2f32": ([P, P, I, I, P, P, I, I, P, P, P], I),
+    "kcmc_match_frames_f32": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
     "kcmc_consensus": ([P, I, I, I, I, P, P, P, P, P], I),
     "kcmc_hypothesis_table": ([I, I, U32, I, P], I),
     "kcmc_ransac_prepare": ([P, P, I, I, U32], I),

@@ -54,6 +54,12 @@ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 int workspace_alloc(kcmc_ctx* ctx, void** p, size_t bytes, hipStream_t s);
 int workspace_free(kcmc_ctx* ctx, void* p, hipStream_t s);
 
+// VA:196-214 per frame on knn output (match.hip): reorder, ratio and displacement
+// filters, survivor bitmask, log counts.  Shared by the uint8 and float32 matchers.
+int launch_match_filter(const int32_t* idx, const float* dist, const double* kp_tpl, const double* kp_q,
+                        const int32_t* q_off, int n_frames, int n_tpl, double ratio, double d_lo, double d_hi,
+                        double* kp_ordered, uint32_t* keep_bits, int32_t* counts, hipStream_t s);
+
 }  // namespace kcmc
 
 #define KCMC_TRY(expr)            \

@@ -363,6 +363,17 @@ int check_match_args(const void* des_tpl, int n_tpl, int D, const void* des_q, c
 }
 
 }  // namespace
+
+int launch_match_filter(const int32_t* idx, const float* dist, const double* kp_tpl, const double* kp_q,
+                        const int32_t* q_off, int n_frames, int n_tpl, double ratio, double d_lo, double d_hi,
+                        double* kp_ordered, uint32_t* keep_bits, int32_t* counts, hipStream_t s) {
+  int P = 1;
+  while (P < n_tpl) P <<= 1;
+  hipLaunchKernelGGL(match_filter_kernel, dim3(n_frames), dim3(kFilterThreads), (size_t)P * sizeof(double), s, idx,
+                     dist, kp_tpl, kp_q, q_off, n_tpl, ratio, d_lo, d_hi, kp_ordered, keep_bits, counts);
+  return launch_check("match_filter_kernel");
+}
+
 }  // namespace kcmc
 
 using namespace kcmc;
@@ -388,10 +399,6 @@ extern "C" int kcmc_match_frames(kcmc_ctx* ctx, const uint8_t* des_tpl, const do
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
   hipStream_t s = (hipStream_t)stream;
   KCMC_TRY(launch_knn(des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, out_idx, out_dist, s));
-  int P = 1;
-  while (P < n_tpl) P <<= 1;
-  hipLaunchKernelGGL(match_filter_kernel, dim3(n_frames), dim3(kFilterThreads), (size_t)P * sizeof(double), s,
-                     out_idx, out_dist, kp_tpl, kp_q, q_off, n_tpl, ratio, d_lo, d_hi, out_kp_ordered,
-                     out_keep_bits, out_counts);
-  return launch_check("match_filter_kernel");
+  return launch_match_filter(out_idx, out_dist, kp_tpl, kp_q, q_off, n_frames, n_tpl, ratio, d_lo, d_hi,
+                             out_kp_ordered, out_keep_bits, out_counts, s);
 }

@@ -456,11 +456,12 @@ __global__ __launch_bounds__(kThreads) void ransac_model_score_kernel(
     if (has_model) resid2<MODEL>(bm.h, P, k, thresh, c);
     out_inl[p0 + k] = (uint8_t)c;
   }
-  if (tid < 9) {
-    best_model[9 * (size_t)f + tid] = has_model ? bm.h[tid] : NAN;
-    if (!has_model) out_params[9 * (size_t)f + tid] = NAN;  // skimage: model None (fit.py:876-879)
-  }
   if (tid == 0) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      best_model[9 * (size_t)f + k] = has_model ? bm.h[k] : NAN;
+      if (!has_model) out_params[9 * (size_t)f + k] = NAN;  // skimage: model None (fit.py:876-879)
+    }
     out_nin[f] = has_model ? best_c : 0;
     out_best[f] = best_t;
   }

@@ -79,18 +79,21 @@ def _check_offsets(q_off_host: np.ndarray, n_frames: int) -> None:
 
 
 def knn2_l2u8(des_tpl: torch.Tensor, des_q: torch.Tensor, q_off: torch.Tensor, max_nq: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """cv2.BFMatcher().knnMatch(des_tpl, des_q[frame], k=2) for every frame at once."""
+    """cv2.BFMatcher().knnMatch(des_tpl, des_q[frame], k=2) for every frame at once.
+    uint8 descriptors (the reference's AKAZE/BRISK) or float32 (SIFT-style extension)."""
     dev = _device_of(des_tpl)
-    _require(des_tpl, "des_tpl", torch.uint8, dev, 2)
-    _require(des_q, "des_q", torch.uint8, dev, 2)
+    f32 = des_tpl.dtype == torch.float32
+    _require(des_tpl, "des_tpl", torch.float32 if f32 else torch.uint8, dev, 2)
+    _require(des_q, "des_q", torch.float32 if f32 else torch.uint8, dev, 2)
     _require(q_off, "q_off", torch.int32, dev, 1)
     n_tpl, D = des_tpl.shape
     F = q_off.numel() - 1
     idx = torch.empty((F, n_tpl, 2), dtype=torch.int32, device=dev)
     dist = torch.empty((F, n_tpl, 2), dtype=torch.float32, device=dev)
     L = _lib.load()
-    _lib.check(L.kcmc_knn2_l2u8(_ctx(dev).handle, _ptr(des_tpl), n_tpl, D, _ptr(des_q), _ptr(q_off), F, int(max_nq),
-                                _ptr(idx), _ptr(dist), _stream(dev)))
+    fn = L.kcmc_knn2_l2f32 if f32 else L.kcmc_knn2_l2u8
+    _lib.check(fn(_ctx(dev).handle, _ptr(des_tpl), n_tpl, D, _ptr(des_q), _ptr(q_off), F, int(max_nq),
+                  _ptr(idx), _ptr(dist), _stream(dev)))
     return idx, dist
 
 
@@ -105,11 +108,13 @@ def match_frames(
     d_lo: float = 0.5,
     d_hi: float = 2.0,
 ) -> MatchResult:
-    """VA:194-214 for every frame: knn k=2 + reorder + ratio + median filters."""
+    """VA:194-214 for every frame: knn k=2 + reorder + ratio + median filters.
+    uint8 descriptors (the reference's) or float32 (SIFT-style extension)."""
     dev = _device_of(des_tpl)
-    _require(des_tpl, "des_tpl", torch.uint8, dev, 2)
+    f32 = des_tpl.dtype == torch.float32
+    _require(des_tpl, "des_tpl", torch.float32 if f32 else torch.uint8, dev, 2)
     _require(kp_tpl, "kp_tpl", torch.float64, dev, 2)
-    _require(des_q, "des_q", torch.uint8, dev, 2)
+    _require(des_q, "des_q", torch.float32 if f32 else torch.uint8, dev, 2)
     _require(kp_q, "kp_q", torch.float64, dev, 2)
     _require(q_off, "q_off", torch.int32, dev, 1)
     n_tpl, D = des_tpl.shape
@@ -131,7 +136,8 @@ def match_frames(
         counts=torch.empty((F, 4), dtype=torch.int32, device=dev),
     )
     L = _lib.load()
-    _lib.check(L.kcmc_match_frames(
+    fn = L.kcmc_match_frames_f32 if f32 else L.kcmc_match_frames
+    _lib.check(fn(
         _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F,
         int(nq.max()) if F else 0, float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist),
         _ptr(res.kp_ordered), _ptr(res.keep_bits), _ptr(res.counts), _stream(dev)))

@@ -58,14 +58,21 @@ def apply_map(M: np.ndarray, pts: np.ndarray) -> np.ndarray:
 def make_keypoints(n_frames: int, n_tpl: int, D: int, size_hw: Tuple[int, int], seed: int = 3,
                    jitter: float = 4.0, rot_deg: float = 0.5, noise: float = 0.3, drop: float = 0.1,
                    distract: float = 0.2, perturb: int = 8, perturb_frac: float = 0.25,
-                   frame_seed: Optional[int] = None, model: str = "euclidean") -> KeypointSet:
+                   frame_seed: Optional[int] = None, model: str = "euclidean",
+                   descriptor: str = "u8", f32_noise: float = 0.05) -> KeypointSet:
     """``seed`` fixes the template; ``frame_seed`` (e.g. a rank) draws an independent
     slab of frames against that same template; ``model`` picks the ground-truth motion
-    family (gt is [F, 2, 3], or [F, 3, 3] for "projective")."""
+    family (gt is [F, 2, 3], or [F, 3, 3] for "projective").  ``descriptor="f32"`` gives
+    SIFT-style float descriptors (template N(0, 1) L2-normalised; frames add
+    N(0, f32_noise) per element; distractors are fresh unit vectors)."""
     rng = np.random.default_rng(seed)
     H, W = size_hw
     kp_tpl = np.stack([rng.uniform(0, W, n_tpl), rng.uniform(0, H, n_tpl)], 1).astype(np.float32).astype(np.float64)
-    des_tpl = rng.integers(0, 256, (n_tpl, D), dtype=np.uint8)
+    if descriptor == "f32":
+        des_tpl = rng.normal(0, 1, (n_tpl, D))
+        des_tpl = (des_tpl / np.linalg.norm(des_tpl, axis=1, keepdims=True)).astype(np.float32)
+    else:
+        des_tpl = rng.integers(0, 256, (n_tpl, D), dtype=np.uint8)
     if frame_seed is not None:
         rng = np.random.default_rng([seed, 1 + int(frame_seed)])
     nd = int(distract * n_tpl)
@@ -84,12 +91,18 @@ def make_keypoints(n_frames: int, n_tpl: int, D: int, size_hw: Tuple[int, int], 
             Ah = A if A.shape == (3, 3) else np.vstack([A, [0.0, 0.0, 1.0]])
             pts = apply_map(np.linalg.inv(Ah), kp_tpl[keep])
         pts = pts + rng.normal(0, noise, (int(keep.sum()), 2))
-        des = des_tpl[keep].astype(np.int16)
-        m = rng.random(des.shape) < perturb_frac
-        des[m] += rng.integers(-perturb, perturb + 1, int(m.sum()), dtype=np.int16)
-        des = np.clip(des, 0, 255).astype(np.uint8)
+        if descriptor == "f32":
+            des = (des_tpl[keep] + rng.normal(0, f32_noise, (int(keep.sum()), D))).astype(np.float32)
+            extra = rng.normal(0, 1, (nd, D))
+            extra = (extra / np.linalg.norm(extra, axis=1, keepdims=True)).astype(np.float32)
+        else:
+            des = des_tpl[keep].astype(np.int16)
+            m = rng.random(des.shape) < perturb_frac
+            des[m] += rng.integers(-perturb, perturb + 1, int(m.sum()), dtype=np.int16)
+            des = np.clip(des, 0, 255).astype(np.uint8)
+            extra = rng.integers(0, 256, (nd, D), dtype=np.uint8)
         pts = np.concatenate([pts, np.stack([rng.uniform(0, W, nd), rng.uniform(0, H, nd)], 1)])
-        des = np.concatenate([des, rng.integers(0, 256, (nd, D), dtype=np.uint8)])
+        des = np.concatenate([des, extra])
         perm = rng.permutation(len(pts))
         kps.append(pts[perm].astype(np.float32).astype(np.float64))
         dess.append(des[perm])

@@ -79,6 +79,52 @@ int kcmc_oracle_knn2_l2u8(const uint8_t* query, int n_query, const uint8_t* trai
 }
 
 /* ------------------------------------------------------------------------- */
+/* K1 extension oracle: BFMatcher(NORM_L2).knnMatch(k=2) on float32            */
+/* descriptors (BASELINE config 5, SIFT-style; the reference's detectors only  */
+/* emit uint8 descriptors).  OpenCV's batchDistL2_32f sums (a-b)^2 in float    */
+/* with a build-dependent SIMD accumulation order, so the build defines the    */
+/* distance as the (near-)exact one: S = sum_k ((double)a_k - (double)b_k)^2   */
+/* accumulated sequentially in double, dist = sqrtf((float)S); top-2 by        */
+/* (dist, train index) like OpenCV's K-insertion.  Parity vs OpenCV: unpinned. */
+/* ------------------------------------------------------------------------- */
+float kcmc_oracle_l2f32_dist(const float* a, const float* b, int D) {
+  double S = 0.0;
+  for (int k = 0; k < D; ++k) {
+    double t = (double)a[k] - (double)b[k];
+    S += t * t;
+  }
+  return sqrtf((float)S);
+}
+
+int kcmc_oracle_knn2_l2f32(const float* query, int n_query, const float* train, int n_train, int D,
+                           int32_t* out_idx, float* out_dist) {
+  if (n_query < 0 || n_train < 0 || D <= 0) return -1;
+  for (int i = 0; i < n_query; ++i) {
+    float bd[2] = {FLT_MAX, FLT_MAX};
+    int32_t bi[2] = {-1, -1};
+    for (int j = 0; j < n_train; ++j) {
+      float d = kcmc_oracle_l2f32_dist(query + (size_t)i * D, train + (size_t)j * D, D);
+      if (d < bd[1]) {
+        if (d < bd[0]) {
+          bd[1] = bd[0];
+          bi[1] = bi[0];
+          bd[0] = d;
+          bi[0] = j;
+        } else {
+          bd[1] = d;
+          bi[1] = j;
+        }
+      }
+    }
+    out_idx[2 * i] = bi[0];
+    out_idx[2 * i + 1] = bi[1];
+    out_dist[2 * i] = bd[0];
+    out_dist[2 * i + 1] = bd[1];
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------------- */
 /* K3 oracle: cv2.warpAffine(img, M, (W, H), flags=INTER_LINEAR) on uint16     */
 /* (VA:455-458), BORDER_CONSTANT with value 0, classic fixed-point path.       */
 /* ------------------------------------------------------------------------- */

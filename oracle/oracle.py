@@ -59,6 +59,7 @@ def lib() -> ctypes.CDLL:
         L.kcmc_oracle_pairwise_sum.argtypes = [P, i]
         L.kcmc_oracle_pairwise_sum.restype = ctypes.c_double
         L.kcmc_oracle_ransac_rigid.argtypes = [P, P, i, P, i, ctypes.c_double, P, P, P, P]
+        L.kcmc_oracle_knn2_l2f32.argtypes = [P, i, P, i, i, P, P]
         L.kcmc_oracle_ransac_model.argtypes = [i, P, P, i, P, i, ctypes.c_double, P, P, P, P]
         L.kcmc_oracle_warp_perspective_u16.argtypes = [P, i, i, i, P, i, P, i, i]
         L.kcmc_oracle_invert_perspective.argtypes = [P, P]
@@ -85,6 +86,20 @@ def knn2_l2u8(query: np.ndarray, train: np.ndarray) -> Tuple[np.ndarray, np.ndar
     idx = np.empty((q.shape[0], 2), np.int32)
     dist = np.empty((q.shape[0], 2), np.float32)
     rc = lib().kcmc_oracle_knn2_l2u8(_p(q), q.shape[0], _p(t), t.shape[0], q.shape[1], _p(idx), _p(dist))
+    assert rc == 0
+    return idx, dist
+
+
+def knn2_l2f32(query: np.ndarray, train: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """``BFMatcher(NORM_L2).knnMatch(query, train, k=2)`` for float32 descriptors with
+    the build's distance definition (sequential fp64 sum of squared differences,
+    sqrtf of its float rounding; ties to the lower train index)."""
+    q = np.ascontiguousarray(query, dtype=np.float32)
+    t = np.ascontiguousarray(train, dtype=np.float32)
+    assert q.ndim == 2 and t.ndim == 2 and q.shape[1] == t.shape[1]
+    idx = np.empty((q.shape[0], 2), np.int32)
+    dist = np.empty((q.shape[0], 2), np.float32)
+    rc = lib().kcmc_oracle_knn2_l2f32(_p(q), q.shape[0], _p(t), t.shape[0], q.shape[1], _p(idx), _p(dist))
     assert rc == 0
     return idx, dist
 

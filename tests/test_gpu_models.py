@@ -235,3 +235,49 @@ def test_video_aligner_model_selector(dev):
     aligned, eu, skipped = AffineAligner().align_keypoints(imgs, ks.kp_tpl, ks.des_tpl, kps, des, n_kp_global=50)
     assert aligned.shape == imgs.shape and eu.shape == (F, 3) and skipped == []
     np.testing.assert_allclose(eu[:, :2], ks.gt[:, :, 2], atol=1.0)
+
+
+# ------------------------------------------------------------ float descriptors (K1f)
+@pytest.mark.parametrize("D", [1, 3, 64, 100, 128])
+def test_knn2_f32_matches_oracle(dev, D):
+    """MFMA candidate search + exact re-ranking == exact brute force (indices and
+    distances bit-exact), including exact duplicates (ties -> lower index) and runs of
+    4+ equidistant rows, which take the exact fallback path."""
+    rng = np.random.default_rng(100 + D)
+    n_tpl = 300
+    tpl = rng.normal(0, 1, (n_tpl, D)).astype(np.float32)
+    frames = []
+    for f, n_q in enumerate([700, 1500, 3, 2, 1, 0, 64, 65, 200]):
+        q = rng.normal(0, 1, (n_q, D)).astype(np.float32)
+        if n_q > 40:
+            q[: n_q // 3] = tpl[rng.integers(0, n_tpl, n_q // 3)] + rng.normal(0, 0.05, (n_q // 3, D)).astype(np.float32)
+            q[10] = q[11] = q[12] = q[13] = q[14] = tpl[5]  # five exact copies of one template row
+            q[20] = q[3]
+        frames.append(q)
+    off = _csr(frames)
+    idx, dist = stages.knn2_l2u8(_t(tpl, dev), _t(np.concatenate(frames).reshape(-1, D), dev), _t(off, dev),
+                                 int(np.diff(off).max()))
+    idx, dist = idx.cpu().numpy(), dist.cpu().numpy()
+    for f, q in enumerate(frames):
+        ri, rd = oracle.knn2_l2f32(tpl, q)
+        assert np.array_equal(idx[f], ri), f
+        assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), f
+
+
+def test_match_frames_f32_vs_oracle(dev):
+    """SIFT-style float descriptors through knn + the reference's filters (VA:196-214)."""
+    ks = synthetic.make_keypoints(12, 400, 128, (1080, 1920), seed=15, descriptor="f32")
+    m = stages.match_frames(_t(ks.des_tpl, dev), _t(ks.kp_tpl, dev), _t(ks.des_q, dev), _t(ks.kp_q, dev),
+                            _t(ks.q_off, dev), ks.q_off)
+    bits = m.keep_bits.cpu().numpy().view(np.uint32)
+    kqo = m.kp_ordered.cpu().numpy()
+    cnt = m.counts.cpu().numpy()
+    for f in range(12):
+        a, b = ks.q_off[f], ks.q_off[f + 1]
+        idx, dist = oracle.knn2_l2f32(ks.des_tpl, ks.des_q[a:b])
+        s, kq, c = oracle.filter_matches(idx, dist, ks.kp_tpl, ks.kp_q[a:b])
+        kept = [i for i in range(400) if (bits[f, i >> 5] >> (i & 31)) & 1]
+        assert kept == sorted(s)
+        assert np.array_equal(kqo[f], kq)
+        assert cnt[f].tolist() == list(c)
+        assert len(kept) > 250

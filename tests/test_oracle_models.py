@@ -105,3 +105,27 @@ def test_warp_perspective_identity_and_affine_homography_known_answers():
     out = oracle.warp_perspective_u16(img, T)
     assert np.array_equal(out[1:, 2:], img[:-1, :-2])
     assert not out[0].any() and not out[:, :2].any()
+
+
+# ------------------------------------------------------------ float descriptors
+def test_knn2_l2f32_oracle_matches_numpy_definition():
+    rng = np.random.default_rng(10)
+    q = rng.normal(0, 1, (40, 128)).astype(np.float32)
+    t = rng.normal(0, 1, (300, 128)).astype(np.float32)
+    t[7] = t[3]  # exact duplicates -> equal distances, lower index first
+    q[5] = t[3]
+    idx, dist = oracle.knn2_l2f32(q, t)
+    d = np.sqrt(((q[:, None, :].astype(np.float64) - t[None].astype(np.float64)) ** 2).sum(-1).astype(np.float32))
+    for i in range(len(q)):
+        order = sorted(range(len(t)), key=lambda j: (d[i, j], j))[:2]
+        assert idx[i].tolist() == order
+        np.testing.assert_allclose(dist[i], d[i, order], rtol=1e-6)
+    assert idx[5].tolist() == [3, 7] and dist[5, 0] == 0.0 and dist[5, 1] == 0.0
+
+
+def test_knn2_l2f32_oracle_degenerate_train_sets():
+    q = np.ones((3, 16), np.float32)
+    idx, dist = oracle.knn2_l2f32(q, np.zeros((1, 16), np.float32))
+    assert idx[:, 1].tolist() == [-1] * 3 and (dist[:, 1] == np.finfo(np.float32).max).all()
+    idx, _ = oracle.knn2_l2f32(q, np.zeros((0, 16), np.float32))
+    assert (idx == -1).all()
