@@ -53,6 +53,7 @@ class BenchConfig:
     model: str
     frames_per_gpu: int
     cpu_sample: int
+    descriptor: str = "u8"
 
 
 # BASELINE.json configs.  c2 (configs[1]) is the headline line; the others are the
@@ -68,6 +69,9 @@ CONFIGS = {
     "c4": BenchConfig("c4", "BASELINE config[3]: 4K RGB u16 (2160x3840x3), 5000 frames over 8 GPUs (625 per GPU), "
                       "4096 keypoints/frame template, D=61 B, affine RANSAC 1000 trials, n_kp_global=500",
                       2160, 3840, 3, 4096, 61, 500, "affine", 625, 4),
+    "c5": BenchConfig("c5", "BASELINE config[4]: 1080p u16, float SIFT-style descriptors (n_tpl=4096, D=128 f32, "
+                      "~4500/frame), homography RANSAC 1000 trials, n_kp_global=200, warpPerspective; "
+                      "500 frames per GPU", 1080, 1920, 1, 4096, 128, 200, "projective", 500, 2, "f32"),
 }
 
 
@@ -83,7 +87,7 @@ def make_texture(bc: BenchConfig) -> np.ndarray:
 
 def make_inputs(bc: BenchConfig, frames_per_gpu: int, rank: int, dev: torch.device):
     ks = synthetic.make_keypoints(frames_per_gpu, bc.n_tpl, bc.D, (bc.H, bc.W), seed=3, frame_seed=rank,
-                                  model=bc.model)
+                                  model=bc.model, descriptor=bc.descriptor)
     base_t = torch.from_numpy(make_texture(bc)).to(dev)
     src = base_t.expand((frames_per_gpu,) + tuple(base_t.shape)).contiguous()
     gt = torch.from_numpy(ks.gt).to(dev)
@@ -183,7 +187,8 @@ def cpu_baseline(bc: BenchConfig, ks, n_sample: int):
         sets, kqs = [], []
         for f in range(n_sample):
             a, b = ks.q_off[f], ks.q_off[f + 1]
-            idx, dist = oracle.knn2_l2u8(ks.des_tpl, ks.des_q[a:b])
+            knn = oracle.knn2_l2f32 if bc.descriptor == "f32" else oracle.knn2_l2u8
+            idx, dist = knn(ks.des_tpl, ks.des_q[a:b])
             s, kq, _ = oracle.filter_matches(idx, dist, ks.kp_tpl, ks.kp_q[a:b])
             sets.append(s)
             kqs.append(kq)
@@ -327,7 +332,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u16 frames; i8 MFMA match, f64 RANSAC, f32 warp weights",
+        "dtype": ("u16 frames; " + ("f32 MFMA match + f64 re-rank" if bc.descriptor == "f32" else "i8 MFMA match")
+                  + ", f64 RANSAC, f32 warp weights"),
         "data": "synthetic (seeded jittered 1080p texture + ORB-shaped keypoints; no detector in image)",
         "config": {
             "workload": bc.workload,
