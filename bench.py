@@ -338,7 +338,7 @@ def main():
         "config": {
             "workload": bc.workload,
             "frames_per_gpu": args.frames, "height": bc.H, "width": bc.W, "channels": bc.C, "n_tpl": bc.n_tpl,
-            "descriptor_bytes": bc.D, "n_kp_global": bc.n_kp_global, "ransac_model": bc.model,
+            "descriptor_len": bc.D, "descriptor_dtype": "float32" if bc.descriptor == "f32" else "uint8", "n_kp_global": bc.n_kp_global, "ransac_model": bc.model,
             "ransac_trials": TRIALS, "parallelism": f"frame-sharded x{world}",
         },
         "ransac_hypotheses_per_s_per_gpu": round(n_ransac * TRIALS / (ransac_ms * 1e-3), 1),

@@ -117,5 +117,6 @@ def euclidean_transforms(affines: np.ndarray) -> np.ndarray:
     """VA:440-453: [x_translation, y_translation, arccos(a00)] per frame."""
     t = np.zeros((affines.shape[0], 3))
     t[:, :2] = affines[:, :2, 2]
-    t[:, 2] = np.arccos(affines[:, 0, 0])
+    with np.errstate(invalid="ignore"):  # arccos(a00 > 1) -> NaN, as in the reference
+        t[:, 2] = np.arccos(affines[:, 0, 0])
     return t
