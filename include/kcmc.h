@@ -211,6 +211,22 @@ int kcmc_warp_perspective_u16(kcmc_ctx* ctx, const uint16_t* src_dev, uint16_t* 
                               const double* M_dev, int n_frames, int H, int W, int C, int inverse_map,
                               kcmc_stream_t stream);
 
+/* ------------------------------------------- f2: normalisation front end (VA:100-104)
+ * brightest = np.percentile(images, 99.99) (VA:479-482) needs two order statistics of
+ * the flattened uint16 stack; they come from two streaming 256-bin histogram passes:
+ *   kcmc_histogram_u16(..., shift = 8, match = -1, ...)   counts of every value's high byte
+ *   kcmc_histogram_u16(..., shift = 0, match = h, ...)    counts of the low byte of the values
+ *                                                          whose high byte is h
+ * out_hist_dev [256] u64 (overwritten).  src_dev 16-byte aligned, n elements. */
+int kcmc_histogram_u16(kcmc_ctx* ctx, const uint16_t* src_dev, unsigned long long n, int shift, int match,
+                       unsigned long long* out_hist_dev, kcmc_stream_t stream);
+
+/* images_u8 = lut[images] for every element: the host evaluates the reference's
+ * np.clip(v / brightest * 255, 0, 255).astype(uint8) (VA:484-492) once per uint16 value
+ * (lut_dev [65536] u8); all buffers 16-byte aligned. */
+int kcmc_lut_u16_to_u8(kcmc_ctx* ctx, const uint16_t* src_dev, unsigned long long n, const uint8_t* lut_dev,
+                       uint8_t* dst_dev, kcmc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

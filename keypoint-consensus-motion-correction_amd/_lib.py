@@ -38,6 +38,8 @@ EXPORTED_SYMBOLS = (
     "kcmc_ransac_model",
     "kcmc_warp_affine_u16",
     "kcmc_warp_perspective_u16",
+    "kcmc_histogram_u16",
+    "kcmc_lut_u16_to_u8",
 )
 
 KCMC_MODEL_EUCLIDEAN = 0
@@ -83,6 +85,8 @@ _SIGNATURES = {
     "kcmc_ransac_model": ([P, I, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, P], I),
     "kcmc_warp_affine_u16": ([P, P, P, P, I, I, I, I, I, P], I),
     "kcmc_warp_perspective_u16": ([P, P, P, P, I, I, I, I, I, P], I),
+    "kcmc_histogram_u16": ([P, P, ctypes.c_ulonglong, I, I, P, P], I),
+    "kcmc_lut_u16_to_u8": ([P, P, ctypes.c_ulonglong, P, P, P], I),
 }
 
 

@@ -360,3 +360,77 @@ def warp_perspective_u16(frames: torch.Tensor, homographies: torch.Tensor, out: 
     _lib.check(L.kcmc_warp_perspective_u16(_ctx(dev).handle, _ptr(frames), _ptr(out), _ptr(homographies), F, H, W, C,
                                            int(bool(inverse_map)), _stream(dev)))
     return out
+
+
+# ------------------------------------------------------------ f2: normalisation
+def _numpy_linear_percentile(n: int, q: float, value_at) -> np.float64:
+    """np.percentile(a, q) (default 'linear' method) of a flattened integer array of n
+    elements, given value_at(rank) = the rank-th smallest element: numpy's virtual
+    index (n - 1) * q' with q' = q/100 (numpy >= 1.22 'linear'), floor/next ranks
+    clipped to the array, and its _lerp (a + (b-a)*t, or b - (b-a)*(1-t) when t >= 0.5),
+    evaluated with the same float64 operations."""
+    qq = np.true_divide(np.float64(q), 100)
+    vi = (n - 1) * qq
+    prev = np.floor(vi)
+    if vi >= n - 1:
+        lo = hi = n - 1
+    elif vi < 0:
+        lo = hi = 0
+    else:
+        lo, hi = int(prev), int(prev) + 1
+    gamma = np.float64(vi - prev)
+    a, b = np.uint16(value_at(lo)), np.uint16(value_at(hi))
+    diff = np.subtract(b, a)
+    if gamma >= 0.5:
+        return np.float64(np.subtract(b, diff * (1 - gamma)))
+    return np.float64(np.add(a, diff * gamma))
+
+
+def brightest_px(frames: torch.Tensor, percentile: float = 99.99) -> np.float64:
+    """VA:479-482 on the device: np.percentile(images, 99.99) of a uint16 stack, exact
+    (two order statistics from two histogram passes, numpy's interpolation on the host)."""
+    dev = _device_of(frames)
+    _require(frames, "frames", torch.uint16, dev)
+    n = frames.numel()
+    if n == 0:
+        raise ValueError("percentile of an empty stack")
+    L = _lib.load()
+    ctx = _ctx(dev).handle
+    hist = torch.empty(256, dtype=torch.int64, device=dev)
+    _lib.check(L.kcmc_histogram_u16(ctx, _ptr(frames), n, 8, -1, _ptr(hist), _stream(dev)))
+    coarse = np.cumsum(hist.cpu().numpy())
+    fine_cache = {}
+
+    def value_at(rank: int) -> int:
+        hb = int(np.searchsorted(coarse, rank, side="right"))
+        if hb not in fine_cache:
+            _lib.check(L.kcmc_histogram_u16(ctx, _ptr(frames), n, 0, hb, _ptr(hist), _stream(dev)))
+            fine_cache[hb] = np.cumsum(hist.cpu().numpy())
+        below = int(coarse[hb - 1]) if hb > 0 else 0
+        lb = int(np.searchsorted(fine_cache[hb], rank - below, side="right"))
+        return (hb << 8) | lb
+
+    return _numpy_linear_percentile(n, percentile, value_at)
+
+
+def max_scale_lut(brightest: float, max_px: int = 255, dtype=np.uint8) -> np.ndarray:
+    """The reference's max-scaling (VA:490) evaluated once for every uint16 value."""
+    v = np.arange(65536, dtype=np.uint16)
+    return np.clip(v / brightest * max_px, a_min=0, a_max=max_px).astype(dtype)
+
+
+def max_scale_u8(frames: torch.Tensor, brightest: float, out: Optional[torch.Tensor] = None,
+                 max_px: int = 255) -> torch.Tensor:
+    """VA:484-492 on the device: np.clip(frames / brightest * 255, 0, 255).astype(uint8)."""
+    dev = _device_of(frames)
+    _require(frames, "frames", torch.uint16, dev)
+    if out is None:
+        out = torch.empty(frames.shape, dtype=torch.uint8, device=dev)
+    else:
+        _require(out, "out", torch.uint8, dev)
+        if out.shape != frames.shape:
+            raise ValueError("out must have the shape of frames")
+    lut = torch.from_numpy(max_scale_lut(float(brightest), max_px)).to(dev)
+    _lib.check(_lib.load().kcmc_lut_u16_to_u8(_ctx(dev).handle, _ptr(frames), frames.numel(), _ptr(lut), _ptr(out),
+                                              _stream(dev)))
+    return out

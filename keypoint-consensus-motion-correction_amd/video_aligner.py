@@ -132,19 +132,26 @@ class VideoAligner:
         self.logger.info(f"aligning {len(images)} frames with n_kp_global: {n_kp_global} and {detector_algorithm}")
         if not 0 <= self.TEMPLATE_FRAME_LOC <= 1:
             raise ValueError("`template_frame_loc` must be between 0 and 1")
-        images_np = _as_numpy(images)
+        on_device = isinstance(images, torch.Tensor)
+        images_np = None if on_device else np.asarray(images)
         if masked_template is not None:
             template = _as_numpy(masked_template)
         else:
-            template_idx = int(len(images_np) * self.TEMPLATE_FRAME_LOC)
-            template = images_np[template_idx]
+            template_idx = int(len(images) * self.TEMPLATE_FRAME_LOC)
+            template = _as_numpy(images[template_idx])
             self.logger.info(f"no masked template provided. Using frame {template_idx} as template")
 
         self.logger.info("normalizing frames...")
         t_start = time.time()
-        brightest_px = self._get_brightest_px(images_np)
-        images_i8, template_i8 = self._max_scale_images(images_np, template, brightest_px, np.uint8)
-        assert images_np.dtype == np.uint16 and images_i8.dtype == np.uint8
+        # VA:100-108 on the device: the stack is uploaded once (and reused by the warp),
+        # percentile and max-scaling run as HIP kernels; the uint8 copy comes back for the
+        # host detector.
+        assert (images.dtype == torch.uint16) if on_device else (images_np.dtype == np.uint16)  # VA:104
+        dev = self._device()
+        frames = images if on_device else torch.from_numpy(np.ascontiguousarray(images_np)).to(dev)
+        brightest_px = self._get_brightest_px(frames)
+        images_i8 = self._max_scale_images(frames, None, brightest_px, np.uint8)[0].cpu().numpy()
+        _, template_i8 = self._max_scale_images(None, template, brightest_px, np.uint8)
         frame_downsample_rate = max(1, frame_rate // self.FRAME_SAMPLE_RATE)
         images_sample, template = self._downsample(images_i8, template_i8, frame_downsample_rate,
                                                    self.SPATIAL_DOWNSAMPLE_RATE)
@@ -162,8 +169,11 @@ class VideoAligner:
             kp_list.append(np.array([p.pt for p in kq], dtype=np.float64).reshape(-1, 2))
             des_list.append(np.asarray(dq, dtype=np.uint8).reshape(len(kq), -1))
         self.logger.info(f"identified keypoints in: {round(time.time() - t_start)} s")
-        return self._align_detected(images, self._kp_template, self._des_template, kp_list, des_list, n_kp_global,
-                                    frame_downsample_rate, patch)
+        aligned, eu, skipped = self._align_detected(frames, self._kp_template, self._des_template, kp_list, des_list,
+                                                    n_kp_global, frame_downsample_rate, patch)
+        if not on_device:
+            aligned = aligned.cpu().numpy()
+        return aligned, eu, skipped
 
     def align_keypoints(
         self,
@@ -338,18 +348,32 @@ class VideoAligner:
         return tuple(np.array(arg) for arg in args)
 
     @classmethod
-    def _get_brightest_px(cls, images: np.ndarray) -> Union[float, int]:
-        """VA:479-482 (host numpy; a GPU histogram version is a listed next step)."""
+    def _get_brightest_px(cls, images) -> Union[float, int]:
+        """VA:479-482: np.percentile(images, 99.99).  A uint16 device tensor takes the exact
+        HIP path (two histogram passes + numpy's interpolation); a host array is the
+        reference's own numpy call."""
+        if isinstance(images, torch.Tensor):
+            return stages.brightest_px(images.contiguous(), cls.IMAGE_NORM_MAX_PERCENTILE)
         return np.percentile(images, cls.IMAGE_NORM_MAX_PERCENTILE)
 
     @classmethod
-    def _max_scale_images(cls, images: np.ndarray, template: np.ndarray, brightest_px: float,
-                          output_dtype: type) -> Tuple[np.ndarray, np.ndarray]:
-        """VA:484-492."""
+    def _max_scale_images(cls, images, template, brightest_px: float, output_dtype: type):
+        """VA:484-492.  uint16 device tensors are scaled on the GPU through the table of
+        the reference's expression (bit-exact); host arrays use the expression itself.
+        Either argument may be None (returned as None)."""
         max_px = cls.MAX_PIXEL_UINT8
-        images = np.clip(images / brightest_px * max_px, a_min=0, a_max=max_px).astype(output_dtype)
-        template = np.clip(template / brightest_px * max_px, a_min=0, a_max=max_px).astype(output_dtype)
-        return images, template
+
+        def scale(x):
+            if x is None:
+                return None
+            if isinstance(x, torch.Tensor) and x.dtype == torch.uint16 and output_dtype == np.uint8:
+                return stages.max_scale_u8(x.contiguous(), brightest_px, max_px=max_px)
+            x = _as_numpy(x)
+            if x.dtype == np.uint16 and output_dtype == np.uint8:
+                return stages.max_scale_lut(brightest_px, max_px)[x]
+            return np.clip(x / brightest_px * max_px, a_min=0, a_max=max_px).astype(output_dtype)
+
+        return scale(images), scale(template)
 
     @staticmethod
     def _downsample(images: np.ndarray, template: np.ndarray, frame_downsample_rate: int,

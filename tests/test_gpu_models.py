@@ -281,3 +281,29 @@ def test_match_frames_f32_vs_oracle(dev):
         assert np.array_equal(kqo[f], kq)
         assert cnt[f].tolist() == list(c)
         assert len(kept) > 250
+
+
+# ------------------------------------------------------------ f2: normalisation
+def test_brightest_px_and_max_scale_vs_reference_golden(dev):
+    g = load_golden("preprocess_golden.npz")
+    for k in range(int(g["n_cases"])):
+        imgs = g[f"p{k}_images"]
+        b = stages.brightest_px(_t(imgs, dev))
+        assert b == g[f"p{k}_brightest"], k
+        u8 = stages.max_scale_u8(_t(imgs, dev), b).cpu().numpy()
+        assert np.array_equal(u8, g[f"p{k}_u8"]), k
+
+
+@pytest.mark.parametrize("shape,hi", [((3, 37, 41), 65536), ((50, 128, 128), 4096), ((2, 1080, 1920), 65536),
+                                      ((5, 7, 3), 2), ((1, 1, 1), 65536)])
+def test_brightest_px_matches_numpy(dev, shape, hi):
+    rng = np.random.default_rng(int(np.prod(shape)) + hi)
+    imgs = rng.integers(0, hi, shape).astype(np.uint16)
+    if imgs.size > 100:
+        imgs.reshape(-1)[rng.integers(0, imgs.size, 20)] = 65000  # hot pixels above the 99.99th percentile
+    t = _t(imgs, dev)
+    for q in (99.99, 50.0, 0.0, 100.0):
+        assert stages.brightest_px(t, q) == np.percentile(imgs, q), q
+    b = np.percentile(imgs, 99.99)
+    ref = np.clip(imgs / b * 255, a_min=0, a_max=255).astype(np.uint8)
+    assert np.array_equal(stages.max_scale_u8(t, b).cpu().numpy(), ref)

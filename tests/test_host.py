@@ -193,3 +193,26 @@ def test_api_surface_matches_reference():
     assert issubclass(VideoAligner.AlignmentError, BaseException)
     assert kcmc_amd.LoResVideoAligner.SPATIAL_DOWNSAMPLE_RATE == 2
     assert (VideoAligner.RANSAC_MAX_TRIALS, VideoAligner.RANDOM_SEED, VideoAligner.N_KP_FRAME_SKIP) == (1000, 42, 3)
+
+
+def test_percentile_restatement_matches_numpy():
+    """stages._numpy_linear_percentile (the host half of the device percentile, VA:481)
+    equals np.percentile exactly, for the reference's 99.99 and other quantiles."""
+    from kcmc_amd.stages import _numpy_linear_percentile
+
+    rng = np.random.default_rng(0)
+    for _ in range(2000):
+        n = int(rng.integers(1, 4000))
+        a = rng.integers(0, int(rng.choice([2, 10, 300, 65536])), n).astype(np.uint16)
+        q = float(rng.choice([99.99, 50.0, 0.0, 100.0, 12.5, rng.uniform(0, 100)]))
+        s = np.sort(a)
+        assert _numpy_linear_percentile(n, q, lambda r: int(s[r])) == np.percentile(a, q)
+
+
+def test_max_scale_lut_matches_reference_expression():
+    from kcmc_amd.stages import max_scale_lut
+
+    g = load_golden("preprocess_golden.npz")
+    for k in range(int(g["n_cases"])):
+        imgs, b = g[f"p{k}_images"], float(g[f"p{k}_brightest"])
+        assert np.array_equal(max_scale_lut(b)[imgs], g[f"p{k}_u8"])

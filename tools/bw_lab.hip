@@ -30,15 +30,27 @@ __global__ __launch_bounds__(256) void copy_unroll(const uint4* __restrict__ a, 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t i = base + (size_t)u * blockDim.x;
-      if (i < n) v[u] = NT ? __builtin_nontemporal_load(a + i) : a[i];
+      if (i < n) {
+        if (NT) {
+          const uint32_t* p = reinterpret_cast<const uint32_t*>(a + i);
+          v[u] = make_uint4(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1),
+                            __builtin_nontemporal_load(p + 2), __builtin_nontemporal_load(p + 3));
+        } else {
+          v[u] = a[i];
+        }
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t i = base + (size_t)u * blockDim.x;
       if (i < n) {
-        if (NT)
-          __builtin_nontemporal_store(v[u], b + i);
-        else
+        if (NT) {
+          uint32_t* p = reinterpret_cast<uint32_t*>(b + i);
+          __builtin_nontemporal_store(v[u].x, p);
+          __builtin_nontemporal_store(v[u].y, p + 1);
+          __builtin_nontemporal_store(v[u].z, p + 2);
+          __builtin_nontemporal_store(v[u].w, p + 3);
+        } else
           b[i] = v[u];
       }
     }
