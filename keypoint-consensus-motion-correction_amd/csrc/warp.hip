@@ -319,7 +319,8 @@ __device__ __forceinline__ void output_rows(const uint16_t* stile, const Box& bo
     }
     uint16_t* drow = Dst + ((size_t)y * W + x) * C;
     if (pair_store) {
-      *reinterpret_cast<uint32_t*>(drow) = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+      // streaming store: the aligned frame is written once and not re-read by this kernel
+      __builtin_nontemporal_store((uint32_t)o[0] | ((uint32_t)o[1] << 16), reinterpret_cast<uint32_t*>(drow));
     } else {
 #pragma unroll
       for (int q = 0; q < 2; ++q)
@@ -590,7 +591,8 @@ __device__ __forceinline__ void persp_rows(const uint16_t* stile, const Box& box
     }
     uint16_t* drow = Dst + ((size_t)y * W + x) * C;
     if (pair_store) {
-      *reinterpret_cast<uint32_t*>(drow) = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+      // streaming store: the aligned frame is written once and not re-read by this kernel
+      __builtin_nontemporal_store((uint32_t)o[0] | ((uint32_t)o[1] << 16), reinterpret_cast<uint32_t*>(drow));
     } else {
 #pragma unroll
       for (int q = 0; q < 2; ++q)
