@@ -231,6 +231,28 @@ def cpu_baseline(bc: BenchConfig, ks, n_sample: int):
     }
 
 
+def end_to_end(bc: BenchConfig, inp, cfg, dev, world: int, reps: int = 3):
+    """PCIe-inclusive rate: the frames start and end in pinned host memory (analysis on
+    the device-resident keypoints as in the hot path, then H2D / warp / D2H streamed in
+    64-frame slabs).  Detection is excluded, as everywhere in this bench."""
+    F = inp.frames.shape[0]
+    host_in = inp.frames.cpu().pin_memory()
+    host_out = torch.empty_like(host_in).pin_memory()
+    pipeline.align_streamed(host_in, inp, cfg, out_host=host_out)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pipeline.align_streamed(host_in, inp, cfg, out_host=host_out)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / reps
+    frame_bytes = host_in[0].numel() * host_in.element_size()
+    return {"value": round(F * world / el, 1), "unit": "frames/s", "ms_per_pass": round(1e3 * el, 3),
+            "pcie_GBps_each_way": round(F * frame_bytes / el / 1e9, 2),
+            "note": "frames in pinned host memory, H2D + analysis + warp + D2H; detection excluded"}
+
+
 def load_traffic(config: str):
     """HBM bytes per warp launch from the committed rocprofv3 PMC pass of this config
     (tools/pmc_warp.sh + tools/pmc_summary.py), if present."""
@@ -253,6 +275,9 @@ def main():
                     help="BASELINE workload (c2 = configs[1], the headline line)")
     ap.add_argument("--frames", type=int, default=None, help="frames per GPU (default: the config's)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="frames in the CPU-baseline sample (0: skip)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also time the PCIe-inclusive path: frames in pinned host memory, streamed through "
+                         "the warp in slabs (pipeline.align_streamed); reported as `end_to_end`, not `value`")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
@@ -357,6 +382,8 @@ def main():
             "avg_launch_ms": round(warp_ms, 4),
         },
     }
+    if args.e2e:
+        result["end_to_end"] = end_to_end(bc, inp, cfg, dev, world)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         result["cpu_baseline"] = cpu_baseline(bc, ks, args.cpu_sample)
     if rank == 0:

@@ -45,6 +45,22 @@ struct WarpCfg {
   static constexpr int kRowPasses = ROW_PASSES;  // staging passes of 8 rows x 32 chunks
 };
 using BlockCfg = WarpCfg<56, 10240, 9>;  // 20 KB box, box rows <= 72 (7 workgroups per CU)
+// Multi-channel frames (RGB / RGBA, config 4): 3-4x the bytes per box pixel, so shorter
+// tiles keep the interleaved box in a 32 KB LDS budget (box rows <= 32).
+using ChanCfg = WarpCfg<24, 16384, 4>;
+
+template <int C>
+struct CfgFor {
+  using type = BlockCfg;
+};
+template <>
+struct CfgFor<3> {
+  using type = ChanCfg;
+};
+template <>
+struct CfgFor<4> {
+  using type = ChanCfg;
+};
 
 __device__ __forceinline__ int cv_round(double v) { return (int)__builtin_rint(v); }
 
@@ -186,7 +202,27 @@ __device__ __forceinline__ void stage_land(uint16_t* stile, const Box& box, int 
   }
 }
 
-// Element-wise staging (C > 1 or W % 8 != 0).
+// Staging of a C-channel box with 16-byte chunks of the interleaved rows (W % 8 == 0:
+// ax0 and W are multiples of 8 pixels, so a chunk is entirely inside or outside the
+// image row and zero-filling whole chunks is exactly BORDER_CONSTANT).
+template <int C>
+__device__ __forceinline__ void stage_vec_c(const uint16_t* __restrict__ S, uint16_t* stile, const Box& box, int H,
+                                            int W, int tid) {
+  const int cpr = box.pitch * C / 8;  // chunks per staged row
+  const int total = box.rows * cpr;
+  const int rowe = W * C;
+  for (int q = tid; q < total; q += kThreads) {
+    const int r = q / cpr, cc = q - r * cpr;
+    const int gy = box.sy0 + r;
+    const int e = box.ax0 * C + 8 * cc;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if ((unsigned)gy < (unsigned)H && e >= 0 && e < rowe)
+      v = *reinterpret_cast<const uint4*>(S + (size_t)gy * rowe + e);
+    *reinterpret_cast<uint4*>(&stile[r * box.pitch * C + 8 * cc]) = v;
+  }
+}
+
+// Element-wise staging (W % 8 != 0).
 template <int C>
 __device__ __forceinline__ void stage_scalar(const uint16_t* __restrict__ S, uint16_t* stile, const Box& box, int H,
                                              int W, int tid) {
@@ -321,6 +357,12 @@ __device__ __forceinline__ void output_rows(const uint16_t* stile, const Box& bo
     if (pair_store) {
       // streaming store: the aligned frame is written once and not re-read by this kernel
       __builtin_nontemporal_store((uint32_t)o[0] | ((uint32_t)o[1] << 16), reinterpret_cast<uint32_t*>(drow));
+    } else if (C >= 3 && x + 2 <= W) {
+      // two whole pixels: 6 (RGB) or 8 (RGBA) channels as 4-byte stores (x even -> aligned)
+#pragma unroll
+      for (int k = 0; k < C; ++k)
+        __builtin_nontemporal_store((uint32_t)o[2 * k] | ((uint32_t)o[2 * k + 1] << 16),
+                                    reinterpret_cast<uint32_t*>(drow) + k);
     } else {
 #pragma unroll
       for (int q = 0; q < 2; ++q)
@@ -403,6 +445,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
   if (box.mode == 0) {
     if (vec_stage) {
       if (VARIANT != 2) stage_land<Cfg>(stile, box, tid, chunk);
+    } else if (C > 1 && (W & 7) == 0) {
+      stage_vec_c<C>(S, stile, box, H, W, tid);
     } else {
       stage_scalar<C>(S, stile, box, H, W, tid);
     }
@@ -418,7 +462,7 @@ size_t warp_workspace_bytes(int n_frames, int H, int W) {
 }
 
 // Plan + tile launches on `s`; ws holds warp_workspace_bytes<Cfg>(n_frames, H, W) bytes.
-template <int C, class Cfg = BlockCfg, int VARIANT = 0>
+template <int C, class Cfg = typename CfgFor<C>::type, int VARIANT = 0>
 void launch_warp(const uint16_t* src, uint16_t* dst, const double* M, int n_frames, int H, int W, int inverse_map,
                  void* ws, hipStream_t s) {
   const int ntx = ceil_div(W, kTileW), nty = ceil_div(H, Cfg::kTileH);
@@ -593,6 +637,12 @@ __device__ __forceinline__ void persp_rows(const uint16_t* stile, const Box& box
     if (pair_store) {
       // streaming store: the aligned frame is written once and not re-read by this kernel
       __builtin_nontemporal_store((uint32_t)o[0] | ((uint32_t)o[1] << 16), reinterpret_cast<uint32_t*>(drow));
+    } else if (C >= 3 && x + 2 <= W) {
+      // two whole pixels: 6 (RGB) or 8 (RGBA) channels as 4-byte stores (x even -> aligned)
+#pragma unroll
+      for (int k = 0; k < C; ++k)
+        __builtin_nontemporal_store((uint32_t)o[2 * k] | ((uint32_t)o[2 * k + 1] << 16),
+                                    reinterpret_cast<uint32_t*>(drow) + k);
     } else {
 #pragma unroll
       for (int q = 0; q < 2; ++q)
@@ -628,6 +678,8 @@ warp_perspective_u16_kernel(const uint16_t* __restrict__ src, uint16_t* __restri
   if (box.mode == 0) {
     if (vec_stage)
       stage_land<Cfg>(stile, box, tid, chunk);
+    else if (C > 1 && (W & 7) == 0)
+      stage_vec_c<C>(S, stile, box, H, W, tid);
     else
       stage_scalar<C>(S, stile, box, H, W, tid);
   }
@@ -646,7 +698,7 @@ size_t persp_workspace_bytes(int n_frames, int H, int W) {
   return tiles * sizeof(TilePlan) + (size_t)n_frames * 9 * sizeof(double);
 }
 
-template <int C, class Cfg = BlockCfg>
+template <int C, class Cfg = typename CfgFor<C>::type>
 void launch_persp(const uint16_t* src, uint16_t* dst, const double* M, int n_frames, int H, int W, int inverse_map,
                   void* ws, hipStream_t s) {
   const int ntx = ceil_div(W, kTileW), nty = ceil_div(H, Cfg::kTileH);
@@ -677,11 +729,12 @@ extern "C" int kcmc_warp_perspective_u16(kcmc_ctx* ctx, const uint16_t* src, uin
   if (n_frames > 65535) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_perspective_u16: at most 65535 frames per call");
   if (C != 1 && C != 3 && C != 4) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_perspective_u16: C must be 1, 3 or 4");
   if (src == dst) return fail(KCMC_EINVAL, "kcmc_warp_perspective_u16: in-place warp is not supported");
-  if ((long long)ceil_div(W, kTileW) * ceil_div(H, BlockCfg::kTileH) * n_frames >= (1ll << 31))
+  if ((long long)ceil_div(W, kTileW) * ceil_div(H, ChanCfg::kTileH) * n_frames >= (1ll << 31))
     return fail(KCMC_EUNSUPPORTED, "kcmc_warp_perspective_u16: too many tiles in one call");
   hipStream_t s = (hipStream_t)stream;
   void* ws = nullptr;
-  KCMC_TRY(workspace_alloc(ctx, &ws, persp_workspace_bytes<BlockCfg>(n_frames, H, W), s));
+  const size_t wsb = C == 1 ? persp_workspace_bytes<BlockCfg>(n_frames, H, W) : persp_workspace_bytes<ChanCfg>(n_frames, H, W);
+  KCMC_TRY(workspace_alloc(ctx, &ws, wsb, s));
   switch (C) {
     case 1:
       launch_persp<1>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
@@ -708,11 +761,12 @@ extern "C" int kcmc_warp_affine_u16(kcmc_ctx* ctx, const uint16_t* src, uint16_t
   if (n_frames > 65535) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: at most 65535 frames per call");
   if (C != 1 && C != 3 && C != 4) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: C must be 1, 3 or 4");
   if (src == dst) return fail(KCMC_EINVAL, "kcmc_warp_affine_u16: in-place warp is not supported");
-  if ((long long)ceil_div(W, kTileW) * ceil_div(H, BlockCfg::kTileH) * n_frames >= (1ll << 31))
+  if ((long long)ceil_div(W, kTileW) * ceil_div(H, ChanCfg::kTileH) * n_frames >= (1ll << 31))
     return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: too many tiles in one call");
   hipStream_t s = (hipStream_t)stream;
   void* ws = nullptr;
-  KCMC_TRY(workspace_alloc(ctx, &ws, warp_workspace_bytes<BlockCfg>(n_frames, H, W), s));
+  const size_t wsb = C == 1 ? warp_workspace_bytes<BlockCfg>(n_frames, H, W) : warp_workspace_bytes<ChanCfg>(n_frames, H, W);
+  KCMC_TRY(workspace_alloc(ctx, &ws, wsb, s));
   switch (C) {
     case 1:
       launch_warp<1>(src, dst, M, n_frames, H, W, inverse_map, ws, s);

@@ -264,3 +264,66 @@ class OverlappedSlabs:
     def synchronize(self) -> None:
         self.analysis.synchronize()
         self.warp.synchronize()
+
+
+def align_streamed(frames_host: torch.Tensor, inp: SlabInputs, cfg: AlignConfig, slab: int = 64,
+                   out_host: Optional[torch.Tensor] = None, logger: Optional[logging.Logger] = None):
+    """The whole hot path for a stack that lives in (pinned) host memory: the end-to-end
+    use of align_images (VA:57-158) when the video does not stay on the device.
+
+    Phase A runs match -> consensus -> RANSAC -> affine post-processing for every frame
+    (only keypoints/descriptors are on the device: ``inp.frames`` is not used and may be
+    an empty placeholder).  Phase B streams the frames through the warp in slabs of
+    ``slab`` frames with three streams and double-buffered device slabs: host->device
+    copy of slab k+1, warp of slab k and device->host copy of slab k-1 overlap, so the
+    rate is bound by PCIe (both directions) rather than HBM.  Returns
+    (out_host, SlabResult without the aligned tensor)."""
+    dev = inp.des_tpl.device
+    F = frames_host.shape[0]
+    if out_host is None:
+        out_host = torch.empty(frames_host.shape, dtype=frames_host.dtype, pin_memory=True)
+    n_tpl = inp.des_tpl.shape[0]
+    match = match_stage(inp, cfg)
+    keep = match.keep_bits.cpu().numpy()
+    cons = consensus_stage(keep, n_tpl, inp.q_off.numel() - 1, cfg, logger)
+    rr = ransac_stage(match, inp.kp_tpl, cons, cfg)
+    affines, skipped, interpolated, eu = postprocess_affines(rr.params.cpu().numpy(), cfg)
+    maps = torch.from_numpy(np.ascontiguousarray(affines[:F], dtype=np.float64)).to(dev)
+
+    shape = (slab,) + tuple(frames_host.shape[1:])
+    bin_ = [torch.empty(shape, dtype=frames_host.dtype, device=dev) for _ in range(2)]
+    bout = [torch.empty(shape, dtype=frames_host.dtype, device=dev) for _ in range(2)]
+    s_in, s_cmp, s_out = (torch.cuda.Stream(dev) for _ in range(3))
+    cur = torch.cuda.current_stream(dev)
+    for s in (s_in, s_cmp, s_out):
+        s.wait_stream(cur)
+    in_ready = [torch.cuda.Event() for _ in range(2)]
+    in_free = [None, None]   # warp done reading bin_[b]
+    out_free = [None, None]  # device->host copy done reading bout[b]
+    for k, f0 in enumerate(range(0, F, slab)):
+        b = k & 1
+        n = min(slab, F - f0)
+        with torch.cuda.stream(s_in):
+            if in_free[b] is not None:
+                s_in.wait_event(in_free[b])
+            bin_[b][:n].copy_(frames_host[f0:f0 + n], non_blocking=True)
+            in_ready[b].record(s_in)
+        with torch.cuda.stream(s_cmp):
+            s_cmp.wait_event(in_ready[b])
+            if out_free[b] is not None:
+                s_cmp.wait_event(out_free[b])
+            warp_frames(bin_[b][:n], maps[f0:f0 + n], out=bout[b][:n])
+            ev = torch.cuda.Event()
+            ev.record(s_cmp)
+            in_free[b] = ev
+        with torch.cuda.stream(s_out):
+            s_out.wait_event(in_free[b])
+            out_host[f0:f0 + n].copy_(bout[b][:n], non_blocking=True)
+            ev2 = torch.cuda.Event()
+            ev2.record(s_out)
+            out_free[b] = ev2
+    for s in (s_in, s_cmp, s_out):
+        cur.wait_stream(s)
+    for t in bin_ + bout:
+        t.record_stream(cur)
+    return out_host, SlabResult(None, affines, eu, skipped, interpolated, match=match, consensus=cons, ransac=rr)

@@ -260,3 +260,23 @@ def test_warp_all_tile_paths_at_1080p(dev):
     out = stages.warp_affine_u16(_t(imgs, dev), _t(np.stack(Ms), dev)).cpu().numpy()
     for f, M in enumerate(Ms):
         assert np.array_equal(out[f], oracle.warp_affine_u16(img, M)), f
+
+
+@pytest.mark.parametrize("shape", [(3, 120, 256, 3), (2, 96, 136, 4), (1, 2160, 3840, 3)])
+def test_warp_multichannel_vector_staging(dev, shape):
+    """C = 3 / 4 with W % 8 == 0: 16-byte staging of interleaved rows into 128 x 24
+    tiles (and, at 4K, tiles on every path)."""
+    rng = np.random.default_rng(shape[1])
+    imgs = rng.integers(0, 65536, shape).astype(np.uint16)
+    F = shape[0]
+    Ms = [synthetic.rigid(np.deg2rad(0.4), 3.7, -2.2), synthetic.rigid(np.deg2rad(-25.0), 40.0, 10.0),
+          np.array([[1.6, 0.02, -30.0], [0.01, 1.6, -20.0]])][:F]
+    Ms = np.stack(Ms)
+    out = stages.warp_affine_u16(_t(imgs, dev), _t(Ms, dev)).cpu().numpy()
+    for f in range(F):
+        assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], Ms[f])), f
+    Hs = np.concatenate([Ms, np.tile([[[0.0, 0.0, 1.0]]], (F, 1, 1))], axis=1)
+    Hs[:, 2, :2] = [2e-5, -1e-5]
+    outp = stages.warp_perspective_u16(_t(imgs, dev), _t(Hs, dev)).cpu().numpy()
+    for f in range(F):
+        assert np.array_equal(outp[f], oracle.warp_perspective_u16(imgs[f], Hs[f])), f

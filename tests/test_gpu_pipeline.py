@@ -150,3 +150,23 @@ def test_overlapped_slabs_equal_align_slab(dev):
         assert np.array_equal(r.affines, g.affines, equal_nan=True)
         assert r.skipped == g.skipped and r.interpolated == g.interpolated
         assert torch.equal(r.aligned, g.aligned)
+
+
+def test_align_streamed_equals_device_resident(dev):
+    """Host-resident frames streamed through the warp in slabs (3 streams, double
+    buffering) give exactly the device-resident slab result."""
+    from kcmc_amd import pipeline, synthetic
+
+    F, H, W = 37, 96, 160
+    ks = synthetic.make_keypoints(F, 120, 32, (H, W), seed=21)
+    base = synthetic.make_texture((H, W), seed=22)
+    frames = torch.from_numpy(np.broadcast_to(base, (F, H, W)).copy())
+    inp = pipeline.SlabInputs(frames.to(dev), torch.from_numpy(ks.des_tpl).to(dev), torch.from_numpy(ks.kp_tpl).to(dev),
+                              torch.from_numpy(ks.des_q).to(dev), torch.from_numpy(ks.kp_q).to(dev),
+                              torch.from_numpy(ks.q_off).to(dev), ks.q_off)
+    cfg = pipeline.AlignConfig(n_kp_global=40)
+    ref = pipeline.align_slab(inp, cfg)
+    out, res = pipeline.align_streamed(frames.pin_memory(), inp, cfg, slab=8)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.numpy(), ref.aligned.cpu().numpy())
+    assert np.array_equal(res.affines, ref.affines)
