@@ -227,6 +227,21 @@ int kcmc_histogram_u16(kcmc_ctx* ctx, const uint16_t* src_dev, unsigned long lon
 int kcmc_lut_u16_to_u8(kcmc_ctx* ctx, const uint16_t* src_dev, unsigned long long n, const uint8_t* lut_dev,
                        uint8_t* dst_dev, kcmc_stream_t stream);
 
+/* ------------------------------------------------------ f1: keypoint detection
+ * The build's exact ORB-style detector (replaces the host OpenCV
+ * detectAndCompute of VA:114-116 / VA:190-192, parity vs OpenCV unpinned): FAST-9
+ * score > threshold, 3x3 NMS, the n_features largest integer-Harris responses
+ * (harris_k), intensity-centroid orientation in 32 bins, steered BRIEF on a 5x5
+ * binomial smoothing.  frames_dev [n_frames, H, W] u8 (e.g. kcmc_lut_u16_to_u8 output);
+ * pattern_dev [32][512][2] i8 and bin_cs_dev [32][2] f64 from kcmc_amd/orb.py;
+ * edge >= 16.  Outputs per frame, in candidate order (64x16 tiles row-major, raster
+ * inside a tile): out_kp_dev [n_frames, n_features, 2] f64 (x, y),
+ * out_des_dev [n_frames, n_features, 32] u8, out_count_dev [n_frames] i32. */
+int kcmc_orb_detect(kcmc_ctx* ctx, const uint8_t* frames_dev, int n_frames, int H, int W, int threshold,
+                    int n_features, double harris_k, int edge, const int8_t* pattern_dev,
+                    const double* bin_cs_dev, double* out_kp_dev, uint8_t* out_des_dev,
+                    int32_t* out_count_dev, kcmc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

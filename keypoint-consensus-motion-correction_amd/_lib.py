@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = (
     "kcmc_warp_perspective_u16",
     "kcmc_histogram_u16",
     "kcmc_lut_u16_to_u8",
+    "kcmc_orb_detect",
 )
 
 KCMC_MODEL_EUCLIDEAN = 0
@@ -87,6 +88,7 @@ _SIGNATURES = {
     "kcmc_warp_perspective_u16": ([P, P, P, P, I, I, I, I, I, P], I),
     "kcmc_histogram_u16": ([P, P, ctypes.c_ulonglong, I, I, P, P], I),
     "kcmc_lut_u16_to_u8": ([P, P, ctypes.c_ulonglong, P, P, P], I),
+    "kcmc_orb_detect": ([P, P, I, I, I, I, I, D, I, P, P, P, P, P, P], I),
 }
 
 

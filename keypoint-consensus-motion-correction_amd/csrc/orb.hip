@@ -1,0 +1,395 @@
+// f1: keypoint detection + description on the device.
+//
+// The reference detects with OpenCV AKAZE/BRISK in the host process and per joblib
+// worker (VA:114-116, VA:190-192); BASELINE config 2 names ORB keypoints.  OpenCV is
+// absent from this image, so the detector is build-defined -- an exact, integer,
+// single-scale ORB-style detector (oracle: kcmc_oracle_orb_detect, bit-identical):
+//   * FAST-9 score: the largest t for which 9 contiguous pixels of the radius-3 circle
+//     are all brighter, or all darker, than the centre by more than t; a corner if
+//     score > threshold;
+//   * 3x3 non-maximum suppression on the score (ties: the first in raster order wins);
+//   * Harris response of the survivors from integer Sobel sums over 7x7,
+//     R = (ab - c^2) - k (a+b)^2 in double;
+//   * the n_features largest R per frame (ties: candidate order), candidates ordered
+//     by 64x16 tile (row-major) then raster order in the tile -- the output order;
+//   * intensity-centroid orientation over the radius-15 disc, binned into 32 bins with
+//     exact cross-product tests against the bin edges;
+//   * steered BRIEF: 256 point pairs of a fixed pattern rotated to the bin's centre
+//     angle (host table), compared on a 5x5 binomial smoothing -> 32-byte descriptors.
+//
+// orb_candidates_kernel  one workgroup per 64x16 tile: image + 4-px halo in LDS, FAST
+//                        scores for the tile + 1-px halo, NMS, Harris, ordered
+//                        compaction of the tile's candidates (block scan).
+// orb_select_kernel      one workgroup per frame: radix-select of the n_features-th
+//                        largest key over all tiles, then ordered compaction per tile.
+// orb_smooth_kernel      5x5 binomial smoothing of the frame.
+// orb_describe_kernel    one wave per keypoint: moments (wave reduction), bin, 4 x 64
+//                        BRIEF comparisons packed with ballots.
+#include <cmath>
+
+#include "kcmc_internal.h"
+
+namespace kcmc {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kTW = 64, kTH = 16;          // candidate tile
+constexpr int kHalo = 4;                   // FAST radius 3 + NMS 1; Harris 3 + Sobel 1
+constexpr int kPW = kTW + 2 * kHalo;       // 72
+constexpr int kPH = kTH + 2 * kHalo;       // 24
+constexpr int kSW = kTW + 2, kSH = kTH + 2;  // scores of the tile + 1-px halo
+constexpr int kSlots = kTW * kTH / 4;      // NMS leaves at most one candidate per 2x2 block
+
+__constant__ int8_t c_circle[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},  {3, 0},  {3, -1}, {2, -2}, {1, -3},
+                                       {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+__device__ __forceinline__ uint64_t order_key(double r) {
+  const uint64_t u = (uint64_t)__double_as_longlong(r);
+  return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+
+// Exclusive block scan of one int per thread (256 threads); returns the total.
+__device__ __forceinline__ int block_excl_scan(int v, int* s_warp, int& excl) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_warp[wave] = x;
+  __syncthreads();
+  int base = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) {
+    const int t = s_warp[w];
+    if (w < wave) base += t;
+    total += t;
+  }
+  __syncthreads();
+  excl = base + x - v;
+  return total;
+}
+
+__global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t* __restrict__ frames, int H, int W,
+                                                                  int threshold, double harris_k, int edge,
+                                                                  uint64_t* __restrict__ cand_key,
+                                                                  uint32_t* __restrict__ cand_pos,
+                                                                  int32_t* __restrict__ cand_cnt) {
+  __shared__ uint8_t img[kPH][kPW];
+  __shared__ int16_t sc[kSH][kSW];
+  __shared__ int s_warp[kThreads / 64];
+  const int ntx = gridDim.x, nty = gridDim.y;
+  const int f = blockIdx.z;
+  const int tile = blockIdx.y * ntx + blockIdx.x;
+  const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH;
+  const int tid = threadIdx.x;
+  const uint8_t* I = frames + (size_t)f * H * W;
+
+  for (int i = tid; i < kPH * kPW; i += kThreads) {
+    const int r = i / kPW, c = i - r * kPW;
+    const int y = y0 - kHalo + r, x = x0 - kHalo + c;
+    img[r][c] = ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) ? I[(size_t)y * W + x] : (uint8_t)0;
+  }
+  __syncthreads();
+  for (int i = tid; i < kSH * kSW; i += kThreads) {
+    const int r = i / kSW, c = i - r * kSW;
+    const int y = y0 - 1 + r, x = x0 - 1 + c;
+    int s = 0;
+    if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3) {
+      const int py = r - 1 + kHalo, px = c - 1 + kHalo;  // position in img
+      const int v = img[py][px];
+      int d[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) d[j] = (int)img[py + c_circle[j][1]][px + c_circle[j][0]] - v;
+      int best = -1000;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        int mb = 1000, md = 1000;
+#pragma unroll
+        for (int m = 0; m < 9; ++m) {
+          const int e = d[(k + m) & 15];
+          mb = min(mb, e);
+          md = min(md, -e);
+        }
+        best = max(best, max(mb, md));
+      }
+      s = best > threshold ? best : 0;
+    }
+    sc[r][c] = (int16_t)s;
+  }
+  __syncthreads();
+
+  // thread t owns tile pixels 4t .. 4t+3 (raster order inside the tile)
+  uint64_t keys[4];
+  int flags = 0, cnt = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = 4 * tid + q;
+    const int r = p / kTW, c = p - r * kTW;
+    const int y = y0 + r, x = x0 + c;
+    keys[q] = 0;
+    if (y < edge || y >= H - edge || x < edge || x >= W - edge) continue;
+    const int s = sc[r + 1][c + 1];
+    if (s == 0) continue;
+    bool keep = true;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        if (dx == 0 && dy == 0) continue;
+        const int o = sc[r + 1 + dy][c + 1 + dx];
+        const bool later = dy > 0 || (dy == 0 && dx > 0);
+        keep = keep && (s > o || (s == o && later));
+      }
+    if (!keep) continue;
+    long long a = 0, b = 0, cc = 0;
+    for (int dy = -3; dy <= 3; ++dy)
+#pragma unroll
+      for (int dx = -3; dx <= 3; ++dx) {
+        const int py = r + kHalo + dy, px = c + kHalo + dx;
+        const int ix = ((int)img[py - 1][px + 1] + 2 * (int)img[py][px + 1] + (int)img[py + 1][px + 1]) -
+                       ((int)img[py - 1][px - 1] + 2 * (int)img[py][px - 1] + (int)img[py + 1][px - 1]);
+        const int iy = ((int)img[py + 1][px - 1] + 2 * (int)img[py + 1][px] + (int)img[py + 1][px + 1]) -
+                       ((int)img[py - 1][px - 1] + 2 * (int)img[py - 1][px] + (int)img[py - 1][px + 1]);
+        a += (long long)ix * ix;
+        b += (long long)iy * iy;
+        cc += (long long)ix * iy;
+      }
+    const double sab = (double)(a + b);
+    keys[q] = order_key((double)(a * b - cc * cc) - harris_k * (sab * sab));
+    flags |= 1 << q;
+    ++cnt;
+  }
+  int excl;
+  const int total = block_excl_scan(cnt, s_warp, excl);
+  const size_t base = ((size_t)f * nty * ntx + tile) * kSlots;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (!(flags >> q & 1)) continue;
+    const int p = 4 * tid + q;
+    const int r = p / kTW, c = p - r * kTW;
+    cand_key[base + excl] = keys[q];
+    cand_pos[base + excl] = ((uint32_t)(y0 + r) << 16) | (uint32_t)(x0 + c);
+    ++excl;
+  }
+  if (tid == 0) cand_cnt[(size_t)f * nty * ntx + tile] = total;
+}
+
+// One workgroup per frame: the n_features-th largest key by 8-bit radix select over all
+// tiles' slots, then the kept candidates compacted tile by tile in candidate order.
+__global__ __launch_bounds__(kThreads) void orb_select_kernel(const uint64_t* __restrict__ cand_key,
+                                                              const uint32_t* __restrict__ cand_pos,
+                                                              const int32_t* __restrict__ cand_cnt, int ntiles,
+                                                              int n_features, double* __restrict__ out_kp_frame,
+                                                              uint32_t* __restrict__ out_pos, int32_t* __restrict__ out_n,
+                                                              int f_base) {
+  __shared__ int hist[256];
+  __shared__ int s_warp[kThreads / 64];
+  __shared__ uint64_t s_prefix;
+  __shared__ int s_rank, s_total;
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint64_t* K = cand_key + (size_t)f * ntiles * kSlots;
+  const uint32_t* Pp = cand_pos + (size_t)f * ntiles * kSlots;
+  const int32_t* Cn = cand_cnt + (size_t)f * ntiles;
+
+  int my = 0;
+  for (int t = tid; t < ntiles; t += kThreads) my += Cn[t];
+  for (int o = 32; o > 0; o >>= 1) my += __shfl_xor(my, o);
+  if ((tid & 63) == 0) s_warp[tid >> 6] = my;
+  __syncthreads();
+  if (tid == 0) s_total = s_warp[0] + s_warp[1] + s_warp[2] + s_warp[3];
+  __syncthreads();
+  const int total = s_total;
+
+  uint64_t T = 0;  // keep key > T, and ties (key == T) up to n_features in candidate order
+  int n_gt = 0;
+  const bool all = total <= n_features;
+  if (!all) {
+    if (tid == 0) {
+      s_prefix = 0;
+      s_rank = n_features;  // the wanted key is the s_rank-th largest among the matching ones
+    }
+    for (int d = 7; d >= 0; --d) {
+      hist[tid] = 0;
+      __syncthreads();
+      const uint64_t prefix = s_prefix;
+      const uint64_t hmask = d == 7 ? 0ull : (~0ull << (8 * (d + 1)));
+      for (int i = tid; i < ntiles * kSlots; i += kThreads) {
+        const int t = i >> 8, s = i & (kSlots - 1);
+        if (s >= Cn[t]) continue;
+        const uint64_t k = K[i];
+        if ((k & hmask) == prefix) atomicAdd(&hist[(k >> (8 * d)) & 255], 1);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int rank = s_rank, acc = 0, dig = 255;
+        for (; dig > 0; --dig) {
+          if (acc + hist[dig] >= rank) break;
+          acc += hist[dig];
+        }
+        s_rank = rank - acc;
+        s_prefix = prefix | ((uint64_t)dig << (8 * d));
+      }
+      __syncthreads();
+    }
+    T = s_prefix;
+    n_gt = n_features - s_rank;  // keys strictly above T
+  }
+  // ordered compaction, one tile (<= 256 slots) per step
+  int out = 0, ties = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cnt = Cn[t];
+    if (cnt == 0) continue;  // uniform across the block
+    const int i = t * kSlots + tid;
+    int keep = 0, tie = 0;
+    if (tid < cnt) {
+      const uint64_t k = K[i];
+      keep = all || k > T;
+      tie = !all && k == T;
+    }
+    int tie_excl;
+    const int tie_total = block_excl_scan(tie, s_warp, tie_excl);
+    if (tie && ties + tie_excl < n_features - n_gt) keep = 1;
+    int ex;
+    const int kept_total = block_excl_scan(keep, s_warp, ex);
+    if (keep) {
+      const uint32_t pp = Pp[i];
+      const size_t o = (size_t)(f_base + f) * n_features + out + ex;
+      out_pos[o] = pp;
+      out_kp_frame[2 * o] = (double)(pp & 0xffffu);
+      out_kp_frame[2 * o + 1] = (double)(pp >> 16);
+    }
+    out += kept_total;
+    ties += tie_total;
+  }
+  if (tid == 0) out_n[f_base + f] = out;
+}
+
+__global__ __launch_bounds__(kThreads) void orb_smooth_kernel(const uint8_t* __restrict__ src, int H, int W,
+                                                              uint8_t* __restrict__ dst) {
+  const size_t n = (size_t)H * W;
+  const int f = blockIdx.y;
+  const uint8_t* I = src + (size_t)f * n;
+  uint8_t* O = dst + (size_t)f * n;
+  for (size_t p = blockIdx.x * (size_t)kThreads + threadIdx.x; p < n; p += (size_t)gridDim.x * kThreads) {
+    const int y = (int)(p / W), x = (int)(p - (size_t)y * W);
+    int v = 0;
+    if (y >= 2 && y < H - 2 && x >= 2 && x < W - 2) {
+      const int w[5] = {1, 4, 6, 4, 1};
+      int s = 0;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const uint8_t* row = I + (size_t)(y + i - 2) * W + x - 2;
+        s += w[i] * ((int)row[0] + 4 * (int)row[1] + 6 * (int)row[2] + 4 * (int)row[3] + (int)row[4]);
+      }
+      v = (s + 128) >> 8;
+    }
+    O[p] = (uint8_t)v;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void orb_describe_kernel(const uint8_t* __restrict__ frames,
+                                                                const uint8_t* __restrict__ smooth, int H, int W,
+                                                                const uint32_t* __restrict__ kp_pos,
+                                                                const int32_t* __restrict__ kp_n, int n_features,
+                                                                const int8_t* __restrict__ pattern,
+                                                                const double* __restrict__ bin_cs, int f_base,
+                                                                uint8_t* __restrict__ out_des) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.y;
+  const int k = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (k >= kp_n[f_base + f]) return;  // wave-uniform
+  const size_t slot = (size_t)(f_base + f) * n_features + k;
+  const uint32_t pp = kp_pos[slot];
+  const int x = (int)(pp & 0xffffu), y = (int)(pp >> 16);
+  const uint8_t* I = frames + (size_t)f * H * W;
+  const uint8_t* S = smooth + (size_t)f * H * W;
+  int m10 = 0, m01 = 0;
+  for (int i = lane; i < 31 * 31; i += 64) {
+    const int dy = i / 31 - 15, dx = i % 31 - 15;
+    if (dx * dx + dy * dy <= 225) {
+      const int v = I[(size_t)(y + dy) * W + (x + dx)];
+      m10 += dx * v;
+      m01 += dy * v;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    m10 += __shfl_xor(m10, o);
+    m01 += __shfl_xor(m01, o);
+  }
+  int bin = 0;
+  if (m10 != 0 || m01 != 0) {
+    int b = (int)floor(atan2((double)m01, (double)m10) / 0.19634954084936207);
+    b &= 31;
+    const int b1 = (b + 1) & 31;
+    const double ck = (double)m01 * bin_cs[2 * b] - (double)m10 * bin_cs[2 * b + 1];
+    const double ck1 = (double)m01 * bin_cs[2 * b1] - (double)m10 * bin_cs[2 * b1 + 1];
+    bin = ck < 0 ? ((b + 31) & 31) : (ck1 >= 0 ? b1 : b);
+  }
+  const int8_t* pt = pattern + (size_t)bin * 512 * 2;
+  uint8_t* d = out_des + slot * 32;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int pi = 64 * r + lane;
+    const int p = S[(size_t)(y + pt[4 * pi + 1]) * W + (x + pt[4 * pi])];
+    const int q = S[(size_t)(y + pt[4 * pi + 3]) * W + (x + pt[4 * pi + 2])];
+    const unsigned long long m = __ballot(p < q);
+    if (lane == 0) {
+#pragma unroll
+      for (int b = 0; b < 8; ++b) d[8 * r + b] = (uint8_t)(m >> (8 * b));
+    }
+  }
+}
+
+}  // namespace
+}  // namespace kcmc
+
+using namespace kcmc;
+
+extern "C" int kcmc_orb_detect(kcmc_ctx* ctx, const uint8_t* frames, int n_frames, int H, int W, int threshold,
+                               int n_features, double harris_k, int edge, const int8_t* pattern, const double* bin_cs,
+                               double* out_kp, uint8_t* out_des, int32_t* out_count, kcmc_stream_t stream) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_orb_detect: ctx is NULL");
+  if (n_frames < 0 || H < 0 || W < 0 || n_features < 0) return fail(KCMC_EINVAL, "kcmc_orb_detect: negative size");
+  if (n_frames == 0) return KCMC_OK;
+  if (!frames || !pattern || !bin_cs || !out_kp || !out_des || !out_count)
+    return fail(KCMC_EINVAL, "kcmc_orb_detect: NULL pointer");
+  if (edge < 16) return fail(KCMC_EINVAL, "kcmc_orb_detect: edge must be >= 16 (orientation disc + BRIEF patch)");
+  if (H > 65535 || W > 65535) return fail(KCMC_EUNSUPPORTED, "kcmc_orb_detect: H, W must be < 65536");
+  if (threshold < 0 || threshold > 255) return fail(KCMC_EINVAL, "kcmc_orb_detect: threshold must be in [0, 255]");
+  hipStream_t s = (hipStream_t)stream;
+  KCMC_TRY(hip_check(hipMemsetAsync(out_count, 0, (size_t)n_frames * sizeof(int32_t), s), "hipMemsetAsync"));
+  if (n_features == 0 || H < 2 * edge + 1 || W < 2 * edge + 1) return KCMC_OK;
+  const int ntx = ceil_div(W, kTW), nty = ceil_div(H, kTH), ntiles = ntx * nty;
+  // frames are processed in batches so that the candidate slots and the smoothed
+  // copy stay a bounded workspace
+  const size_t per_frame = (size_t)ntiles * kSlots * (sizeof(uint64_t) + sizeof(uint32_t)) +
+                           (size_t)ntiles * sizeof(int32_t) + (size_t)H * W;
+  int batch = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_frames, ((size_t)1 << 30) / per_frame));
+  batch = std::min(batch, 65535);
+  void* ws = nullptr;
+  KCMC_TRY(workspace_alloc(ctx, &ws, per_frame * batch + (size_t)n_frames * n_features * sizeof(uint32_t) + 64, s));
+  uint64_t* ckey = static_cast<uint64_t*>(ws);
+  uint32_t* cpos = reinterpret_cast<uint32_t*>(ckey + (size_t)batch * ntiles * kSlots);
+  int32_t* ccnt = reinterpret_cast<int32_t*>(cpos + (size_t)batch * ntiles * kSlots);
+  uint8_t* smooth = reinterpret_cast<uint8_t*>(ccnt + (size_t)batch * ntiles);
+  uint32_t* kpos = reinterpret_cast<uint32_t*>(smooth + (size_t)batch * H * W + 16 - (((size_t)batch * H * W) & 15));
+  int rc = KCMC_OK;
+  for (int f0 = 0; f0 < n_frames && rc == KCMC_OK; f0 += batch) {
+    const int nb = std::min(batch, n_frames - f0);
+    const uint8_t* fr = frames + (size_t)f0 * H * W;
+    hipLaunchKernelGGL(orb_candidates_kernel, dim3(ntx, nty, nb), dim3(kThreads), 0, s, fr, H, W, threshold, harris_k,
+                       edge, ckey, cpos, ccnt);
+    hipLaunchKernelGGL(orb_select_kernel, dim3(nb), dim3(kThreads), 0, s, ckey, cpos, ccnt, ntiles, n_features, out_kp,
+                       kpos, out_count, f0);
+    const unsigned sgrid = (unsigned)std::min<size_t>(((size_t)H * W + kThreads - 1) / kThreads, 1024);
+    hipLaunchKernelGGL(orb_smooth_kernel, dim3(sgrid, nb), dim3(kThreads), 0, s, fr, H, W, smooth);
+    hipLaunchKernelGGL(orb_describe_kernel, dim3(ceil_div(n_features, kThreads / 64), nb), dim3(kThreads), 0, s, fr,
+                       smooth, H, W, kpos, out_count, n_features, pattern, bin_cs, f0, out_des);
+    rc = launch_check("orb kernels");
+  }
+  const int rc2 = workspace_free(ctx, ws, s);
+  return rc != KCMC_OK ? rc : rc2;
+}

@@ -434,3 +434,50 @@ def max_scale_u8(frames: torch.Tensor, brightest: float, out: Optional[torch.Ten
     _lib.check(_lib.load().kcmc_lut_u16_to_u8(_ctx(dev).handle, _ptr(frames), frames.numel(), _ptr(lut), _ptr(out),
                                               _stream(dev)))
     return out
+
+
+# ------------------------------------------------------------ f1: detection
+@dataclass
+class Keypoints:
+    kp: torch.Tensor      # [F, n_features, 2] f64 (x, y); rows >= count[f] undefined
+    des: torch.Tensor     # [F, n_features, 32] u8
+    count: torch.Tensor   # [F] i32
+
+
+def detect_orb(frames_u8: torch.Tensor, params=None) -> Keypoints:
+    """The build's ORB-style detector (csrc/orb.hip) for every frame of a uint8 stack:
+    replaces detector.detectAndCompute (VA:114-116, VA:190-192) on the device."""
+    from . import orb
+
+    params = params or orb.OrbParams()
+    dev = _device_of(frames_u8)
+    _require(frames_u8, "frames_u8", torch.uint8, dev)
+    if frames_u8.dim() == 2:
+        frames_u8 = frames_u8.unsqueeze(0)
+    if frames_u8.dim() != 3:
+        raise ValueError("frames_u8 must be [F, H, W] or [H, W]")
+    F, H, W = frames_u8.shape
+    N = int(params.n_features)
+    res = Keypoints(kp=torch.empty((F, N, 2), dtype=torch.float64, device=dev),
+                    des=torch.empty((F, N, 32), dtype=torch.uint8, device=dev),
+                    count=torch.empty((F,), dtype=torch.int32, device=dev))
+    pattern = torch.from_numpy(orb.rotated_patterns()).to(dev)
+    cs = torch.from_numpy(orb.bin_edges()).to(dev)
+    _lib.check(_lib.load().kcmc_orb_detect(
+        _ctx(dev).handle, _ptr(frames_u8), F, H, W, int(params.fast_threshold), N, float(params.harris_k),
+        int(params.edge), _ptr(pattern), _ptr(cs), _ptr(res.kp), _ptr(res.des), _ptr(res.count), _stream(dev)))
+    return res
+
+
+def keypoints_csr(k: Keypoints):
+    """Per-frame keypoints -> the matcher's CSR layout: (kp [P, 2] f64, des [P, 32] u8,
+    q_off (device i32 [F+1]), q_off_host)."""
+    counts = k.count.cpu().numpy().astype(np.int64)
+    F, N = k.kp.shape[:2]
+    q_off = np.zeros(F + 1, np.int32)
+    q_off[1:] = np.cumsum(counts)
+    rows = torch.from_numpy(np.concatenate([f * N + np.arange(c) for f, c in enumerate(counts)])
+                            if F else np.zeros(0, np.int64)).to(k.kp.device)
+    kp = k.kp.reshape(F * N, 2).index_select(0, rows).contiguous()
+    des = k.des.reshape(F * N, 32).index_select(0, rows).contiguous()
+    return kp, des, torch.from_numpy(q_off).to(k.kp.device), q_off

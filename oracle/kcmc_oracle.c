@@ -649,3 +649,196 @@ int kcmc_oracle_ransac_model(int model, const double* src, const double* dst, in
   free(cur);
   return best_n > 0 ? 0 : 1;
 }
+
+/* ------------------------------------------------------------------------- */
+/* f1 oracle: the build's ORB-style detector (DESIGN.md "f1").  The reference  */
+/* detects with OpenCV AKAZE/BRISK (VA:114-116, VA:190-192) and BASELINE        */
+/* config 2 names ORB keypoints; OpenCV is absent from this image, so the       */
+/* detector is build-defined (parity vs OpenCV unpinned) and exact in integers: */
+/*   FAST-9 score (largest t for which 9 contiguous circle pixels are all        */
+/*   brighter / darker than the centre by more than t), 3x3 non-maximum        */
+/*   suppression (ties: the first in raster order wins), Harris response from   */
+/*   integer Sobel sums over 7x7 (R = (ab - c^2) - k (a+b)^2 in double), the     */
+/*   n_features largest R (ties: candidate order), intensity-centroid           */
+/*   orientation binned to 32 bins with exact cross-product tests, and steered  */
+/*   BRIEF (256 pairs, a rotated table per bin) on a 5x5 binomial smoothing.    */
+/*   Candidate order = 64x16 tiles in row-major order, raster order inside a    */
+/*   tile; the kept keypoints keep that order.                                  */
+/* ------------------------------------------------------------------------- */
+static const int kFastCircle[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},  {3, 0},  {3, -1}, {2, -2}, {1, -3},
+                                       {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+int kcmc_oracle_fast_score(const uint8_t* img, int W, int x, int y) {
+  const int v = img[(size_t)y * W + x];
+  int d[16];
+  for (int j = 0; j < 16; ++j) d[j] = (int)img[(size_t)(y + kFastCircle[j][1]) * W + x + kFastCircle[j][0]] - v;
+  int best = -1000;
+  for (int k = 0; k < 16; ++k) {
+    int mb = 1000, md = 1000;
+    for (int m = 0; m < 9; ++m) {
+      int e = d[(k + m) & 15];
+      if (e < mb) mb = e;
+      if (-e < md) md = -e;
+    }
+    if (mb > best) best = mb;
+    if (md > best) best = md;
+  }
+  return best;
+}
+
+double kcmc_oracle_harris(const uint8_t* img, int W, int x, int y, double k) {
+  long long a = 0, b = 0, c = 0;
+  for (int dy = -3; dy <= 3; ++dy)
+    for (int dx = -3; dx <= 3; ++dx) {
+      const uint8_t* p = img + (size_t)(y + dy) * W + (x + dx);
+      int ix = ((int)p[-W + 1] + 2 * (int)p[1] + (int)p[W + 1]) - ((int)p[-W - 1] + 2 * (int)p[-1] + (int)p[W - 1]);
+      int iy = ((int)p[W - 1] + 2 * (int)p[W] + (int)p[W + 1]) - ((int)p[-W - 1] + 2 * (int)p[-W] + (int)p[-W + 1]);
+      a += (long long)ix * ix;
+      b += (long long)iy * iy;
+      c += (long long)ix * iy;
+    }
+  double s = (double)(a + b);
+  return (double)(a * b - c * c) - k * (s * s);
+}
+
+static uint64_t order_key(double r) {
+  uint64_t u;
+  memcpy(&u, &r, 8);
+  return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+
+/* 5x5 binomial smoothing (weights 1 4 6 4 1 per axis, /256 rounded) at (x, y). */
+static int smooth5(const uint8_t* img, int W, int x, int y) {
+  static const int w[5] = {1, 4, 6, 4, 1};
+  int s = 0;
+  for (int i = 0; i < 5; ++i)
+    for (int j = 0; j < 5; ++j) s += w[i] * w[j] * (int)img[(size_t)(y + i - 2) * W + (x + j - 2)];
+  return (s + 128) >> 8;
+}
+
+int kcmc_oracle_orientation_bin(const uint8_t* img, int W, int x, int y, const double* cs /* [32][2] */) {
+  int m10 = 0, m01 = 0;
+  for (int dy = -15; dy <= 15; ++dy)
+    for (int dx = -15; dx <= 15; ++dx) {
+      if (dx * dx + dy * dy > 225) continue;
+      int v = img[(size_t)(y + dy) * W + (x + dx)];
+      m10 += dx * v;
+      m01 += dy * v;
+    }
+  if (m10 == 0 && m01 == 0) return 0;
+  const double a = 0.19634954084936207; /* 2 pi / 32 */
+  int k = (int)floor(atan2((double)m01, (double)m10) / a);
+  k &= 31;
+  double ck = (double)m01 * cs[2 * k] - (double)m10 * cs[2 * k + 1];
+  int k1 = (k + 1) & 31;
+  double ck1 = (double)m01 * cs[2 * k1] - (double)m10 * cs[2 * k1 + 1];
+  if (ck < 0)
+    k = (k + 31) & 31;
+  else if (ck1 >= 0)
+    k = k1;
+  return k;
+}
+
+/* One frame.  pattern [32 bins][512 points][2] int8 (x, y) = the rotated BRIEF pairs
+ * (point 2i and 2i+1 form pair i), cs [32][2] = cos / sin of the bin edges.
+ * out_kp [n_features][2] f64 (x, y), out_des [n_features][32] u8.  Returns the count. */
+int kcmc_oracle_orb_detect(const uint8_t* img, int H, int W, int threshold, int n_features, double harris_k,
+                           int edge, const int8_t* pattern, const double* cs, double* out_kp, uint8_t* out_des) {
+  if (H <= 0 || W <= 0) return 0;
+  int* score = (int*)calloc((size_t)H * W, sizeof(int));
+  size_t cap = (size_t)H * W / 4 + 16, nc = 0;
+  uint64_t* key = (uint64_t*)malloc(cap * sizeof(uint64_t));
+  int* pos = (int*)malloc(cap * 2 * sizeof(int));
+  if (!score || !key || !pos) {
+    free(score);
+    free(key);
+    free(pos);
+    return -1;
+  }
+  for (int y = 3; y < H - 3; ++y)
+    for (int x = 3; x < W - 3; ++x) {
+      int s = kcmc_oracle_fast_score(img, W, x, y);
+      score[(size_t)y * W + x] = s > threshold ? s : 0;
+    }
+  const int TW = 64, TH = 16;
+  for (int ty = 0; ty < H; ty += TH)
+    for (int tx = 0; tx < W; tx += TW)
+      for (int y = ty; y < ty + TH && y < H; ++y)
+        for (int x = tx; x < tx + TW && x < W; ++x) {
+          if (y < edge || y >= H - edge || x < edge || x >= W - edge) continue;
+          int s = score[(size_t)y * W + x];
+          if (s == 0) continue;
+          int keep = 1;
+          for (int dy = -1; dy <= 1 && keep; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) {
+              if (!dx && !dy) continue;
+              int q = score[(size_t)(y + dy) * W + (x + dx)];
+              int later = dy > 0 || (dy == 0 && dx > 0);
+              if (!(s > q || (s == q && later))) {
+                keep = 0;
+                break;
+              }
+            }
+          if (!keep) continue;
+          key[nc] = order_key(kcmc_oracle_harris(img, W, x, y, harris_k));
+          pos[2 * nc] = x;
+          pos[2 * nc + 1] = y;
+          ++nc;
+        }
+  /* the n_features largest keys; ties in candidate order */
+  uint64_t T = 0;
+  size_t n_gt = 0;
+  if ((size_t)n_features < nc) {
+    /* T = the n_features-th largest key */
+    uint64_t lo = 0, hi = ~0ull;
+    while (lo < hi) { /* largest T with count(key >= T) >= n_features */
+      uint64_t mid = lo + (hi - lo) / 2 + 1;
+      size_t c = 0;
+      for (size_t i = 0; i < nc; ++i) c += key[i] >= mid;
+      if (c >= (size_t)n_features)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    T = lo;
+    for (size_t i = 0; i < nc; ++i) n_gt += key[i] > T;
+  }
+  uint8_t* sm = (uint8_t*)calloc((size_t)H * W, 1);
+  int n_out = 0;
+  size_t ties = 0;
+  for (size_t i = 0; i < nc && sm; ++i) {
+    int take;
+    if ((size_t)n_features >= nc)
+      take = 1;
+    else if (key[i] > T)
+      take = 1;
+    else if (key[i] == T && ties < (size_t)n_features - n_gt) {
+      take = 1;
+      ++ties;
+    } else
+      take = 0;
+    if (!take) continue;
+    int x = pos[2 * i], y = pos[2 * i + 1];
+    int bin = kcmc_oracle_orientation_bin(img, W, x, y, cs);
+    const int8_t* pt = pattern + (size_t)bin * 512 * 2;
+    uint8_t* d = out_des + (size_t)n_out * 32;
+    for (int b = 0; b < 32; ++b) {
+      int val = 0;
+      for (int j = 0; j < 8; ++j) {
+        int pi = 8 * b + j;
+        int p = smooth5(img, W, x + pt[4 * pi], y + pt[4 * pi + 1]);
+        int q = smooth5(img, W, x + pt[4 * pi + 2], y + pt[4 * pi + 3]);
+        val |= (p < q) << j;
+      }
+      d[b] = (uint8_t)val;
+    }
+    out_kp[2 * n_out] = x;
+    out_kp[2 * n_out + 1] = y;
+    ++n_out;
+  }
+  free(sm);
+  free(score);
+  free(key);
+  free(pos);
+  return n_out;
+}

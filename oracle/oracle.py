@@ -60,6 +60,11 @@ def lib() -> ctypes.CDLL:
         L.kcmc_oracle_pairwise_sum.restype = ctypes.c_double
         L.kcmc_oracle_ransac_rigid.argtypes = [P, P, i, P, i, ctypes.c_double, P, P, P, P]
         L.kcmc_oracle_knn2_l2f32.argtypes = [P, i, P, i, i, P, P]
+        L.kcmc_oracle_orb_detect.argtypes = [P, i, i, i, i, ctypes.c_double, i, P, P, P, P]
+        L.kcmc_oracle_fast_score.argtypes = [P, i, i, i]
+        L.kcmc_oracle_harris.argtypes = [P, i, i, i, ctypes.c_double]
+        L.kcmc_oracle_harris.restype = ctypes.c_double
+        L.kcmc_oracle_orientation_bin.argtypes = [P, i, i, i, P]
         L.kcmc_oracle_ransac_model.argtypes = [i, P, P, i, P, i, ctypes.c_double, P, P, P, P]
         L.kcmc_oracle_warp_perspective_u16.argtypes = [P, i, i, i, P, i, P, i, i]
         L.kcmc_oracle_invert_perspective.argtypes = [P, P]
@@ -421,3 +426,20 @@ def warp_perspective_u16(img: np.ndarray, M: np.ndarray, dsize=None, inverse_map
     rc = lib().kcmc_oracle_warp_perspective_u16(_p(src), H, W, C, _p(M9), int(inverse_map), _p(out), dH, dW)
     assert rc == 0
     return out
+
+
+# ------------------------------------------------------------ f1: detection
+def orb_detect(img: np.ndarray, n_features: int = 500, threshold: int = 20, harris_k: float = 0.04, edge: int = 16,
+               pattern: np.ndarray = None, bin_cs: np.ndarray = None):
+    """The build's ORB-style detector on one uint8 image (kcmc_oracle_orb_detect):
+    returns (kp [n, 2] f64 (x, y), des [n, 32] u8) in candidate order."""
+    a = np.ascontiguousarray(img, np.uint8)
+    H, W = a.shape
+    pat = np.ascontiguousarray(pattern, np.int8)
+    cs = np.ascontiguousarray(bin_cs, np.float64)
+    kp = np.empty((max(n_features, 1), 2), np.float64)
+    des = np.empty((max(n_features, 1), 32), np.uint8)
+    n = lib().kcmc_oracle_orb_detect(_p(a), H, W, threshold, n_features, float(harris_k), edge, _p(pat), _p(cs),
+                                     _p(kp), _p(des))
+    assert n >= 0
+    return kp[:n].copy(), des[:n].copy()

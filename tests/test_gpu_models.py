@@ -307,3 +307,55 @@ def test_brightest_px_matches_numpy(dev, shape, hi):
     b = np.percentile(imgs, 99.99)
     ref = np.clip(imgs / b * 255, a_min=0, a_max=255).astype(np.uint8)
     assert np.array_equal(stages.max_scale_u8(t, b).cpu().numpy(), ref)
+
+
+# ------------------------------------------------------------ f1: detection
+def _texture_u8(rng, H, W, cell=4, noise=12):
+    lo = rng.integers(0, 256, (H // cell + 2, W // cell + 2)).astype(np.float64)
+    img = np.kron(lo, np.ones((cell, cell)))[:H, :W] + rng.normal(0, noise, (H, W))
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+@pytest.mark.parametrize("shape,nf", [((3, 120, 200), 500), ((2, 256, 320), 40), ((1, 1080, 1920), 500)])
+def test_orb_detect_matches_oracle(dev, shape, nf):
+    from kcmc_amd import orb
+
+    rng = np.random.default_rng(shape[1] + nf)
+    F, H, W = shape
+    imgs = np.stack([_texture_u8(rng, H, W) for _ in range(F)])
+    if F >= 2:
+        imgs[1, :, : W // 2] = 100  # a flat half: no corners there
+    if F == 3:
+        imgs[2] = np.tile(_texture_u8(rng, 40, 40), (3, 5))[:H, :W]  # repeated tiles: equal Harris -> ties
+    k = stages.detect_orb(_t(imgs, dev), orb.OrbParams(n_features=nf))
+    kp, des, cnt = k.kp.cpu().numpy(), k.des.cpu().numpy(), k.count.cpu().numpy()
+    for f in range(F):
+        rkp, rdes = oracle.orb_detect(imgs[f], n_features=nf, pattern=orb.rotated_patterns(), bin_cs=orb.bin_edges())
+        assert cnt[f] == len(rkp), (f, cnt[f], len(rkp))
+        assert np.array_equal(kp[f, :cnt[f]], rkp), f
+        assert np.array_equal(des[f, :cnt[f]], rdes), f
+        assert cnt[f] > 0
+    flat = stages.detect_orb(_t(np.full((1, 64, 64), 7, np.uint8), dev))
+    assert flat.count.cpu().numpy()[0] == 0
+
+
+def test_orb_keypoints_feed_the_matcher(dev):
+    """Detect on a frame and on its shifted copy, match through the reference's
+    matcher + filters, and recover the shift with RANSAC: the GPU front end end to end."""
+    from kcmc_amd import orb, pipeline
+
+    rng = np.random.default_rng(5)
+    H, W = 240, 320
+    base = _texture_u8(rng, H + 20, W + 20)
+    tpl = base[10:10 + H, 10:10 + W]
+    frames = np.stack([base[10 + dy:10 + dy + H, 10 + dx:10 + dx + W] for dy, dx in ((0, 0), (3, -2), (-4, 5))])
+    kt = stages.detect_orb(_t(tpl, dev))
+    kq = stages.detect_orb(_t(frames, dev))
+    n_t = int(kt.count.cpu()[0])
+    kp_q, des_q, q_off, q_off_host = stages.keypoints_csr(kq)
+    inp = pipeline.SlabInputs(_t(frames.astype(np.uint16), dev), kt.des[0, :n_t].contiguous(),
+                              kt.kp[0, :n_t].contiguous(), des_q, kp_q, q_off, q_off_host)
+    res = pipeline.align_slab(inp, pipeline.AlignConfig(n_kp_global=60), keep_intermediates=True)
+    # frame content at (x, y) is the template at (x + dx, y + dy): frame->template map translates by (dx, dy)
+    for f, (dy, dx) in enumerate(((0, 0), (3, -2), (-4, 5))):
+        np.testing.assert_allclose(res.affines[f][:, 2], [dx, dy], atol=1e-6)
