@@ -231,6 +231,27 @@ def cpu_baseline(bc: BenchConfig, ks, n_sample: int):
     }
 
 
+def with_detection(inp, cfg, dev, world: int, reps: int = 3):
+    """Device-resident frames -> aligned frames including the front end the hot path
+    excludes: exact percentile normalisation (f2) and the build's ORB-style detector
+    (f1, 500 keypoints per frame) on the synthetic video, then match / consensus /
+    RANSAC / warp as in `value`."""
+    out = torch.empty_like(inp.frames)
+    res = pipeline.align_frames(inp.frames, cfg, out=out)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res = pipeline.align_frames(inp.frames, cfg, out=out)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / reps
+    F = inp.frames.shape[0]
+    return {"value": round(F * world / el, 1), "unit": "frames/s", "ms_per_pass": round(1e3 * el, 3),
+            "template_keypoints": res.extras["n_template_keypoints"], "skipped_frames": len(res.skipped),
+            "note": "normalisation + ORB-style detection + match + consensus + RANSAC + warp, frames on the device"}
+
+
 def end_to_end(bc: BenchConfig, inp, cfg, dev, world: int, reps: int = 3):
     """PCIe-inclusive rate: the frames start and end in pinned host memory (analysis on
     the device-resident keypoints as in the hot path, then H2D / warp / D2H streamed in
@@ -278,6 +299,9 @@ def main():
     ap.add_argument("--e2e", action="store_true",
                     help="also time the PCIe-inclusive path: frames in pinned host memory, streamed through "
                          "the warp in slabs (pipeline.align_streamed); reported as `end_to_end`, not `value`")
+    ap.add_argument("--detect", action="store_true",
+                    help="also time align from raw uint16 frames on the device: normalisation + ORB-style "
+                         "detection + the hot path (pipeline.align_frames); reported as `with_detection`")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
@@ -384,6 +408,8 @@ def main():
     }
     if args.e2e:
         result["end_to_end"] = end_to_end(bc, inp, cfg, dev, world)
+    if args.detect and bc.C == 1:
+        result["with_detection"] = with_detection(inp, cfg, dev, world)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         result["cpu_baseline"] = cpu_baseline(bc, ks, args.cpu_sample)
     if rank == 0:

@@ -327,3 +327,43 @@ def align_streamed(frames_host: torch.Tensor, inp: SlabInputs, cfg: AlignConfig,
     for t in bin_ + bout:
         t.record_stream(cur)
     return out_host, SlabResult(None, affines, eu, skipped, interpolated, match=match, consensus=cons, ransac=rr)
+
+
+def detect_slab(frames: torch.Tensor, cfg: AlignConfig, template_index: Optional[int] = None,
+                template: Optional[torch.Tensor] = None, orb_params=None, percentile: float = 99.99):
+    """The front end of align_images (VA:93-123) on the device for a uint16 stack:
+    normalisation (f2: exact 99.99th percentile + max-scale) and the build's
+    ORB-style detector (f1) on the template and on every sample frame.  Returns
+    (SlabInputs for align_slab, brightest)."""
+    if frames.dim() != 3:
+        raise ValueError("detection needs a grayscale stack [F, H, W]")
+    if cfg.frame_downsample_rate != 1 or cfg.spatial_rate != 1:
+        raise ValueError("device detection needs frame_downsample_rate == 1 and spatial_rate == 1 (pyrDown not built)")
+    F = frames.shape[0]
+    brightest = stages.brightest_px(frames, percentile)
+    u8 = stages.max_scale_u8(frames, brightest)
+    if template is None:
+        ti = int(F * 0.5) if template_index is None else int(template_index)
+        tpl_u8 = u8[ti:ti + 1]
+    else:
+        tpl_u8 = stages.max_scale_u8(template.reshape(1, *template.shape[-2:]).contiguous(), brightest)
+    kt = stages.detect_orb(tpl_u8, orb_params)
+    kq = stages.detect_orb(u8, orb_params)
+    n_t = int(kt.count.cpu()[0])
+    kp_q, des_q, q_off, q_off_host = stages.keypoints_csr(kq)
+    inp = SlabInputs(frames, kt.des[0, :n_t].contiguous(), kt.kp[0, :n_t].contiguous(), des_q, kp_q, q_off,
+                     q_off_host)
+    return inp, brightest
+
+
+def align_frames(frames: torch.Tensor, cfg: AlignConfig, template_index: Optional[int] = None,
+                 orb_params=None, out: Optional[torch.Tensor] = None,
+                 logger: Optional[logging.Logger] = None) -> SlabResult:
+    """align_images (VA:57-158) entirely on the device for a device-resident uint16 stack:
+    normalisation, detection, matching, consensus (host, native), RANSAC, gap filling
+    (host) and warp."""
+    inp, brightest = detect_slab(frames, cfg, template_index, orb_params=orb_params)
+    res = align_slab(inp, cfg, logger=logger, out=out)
+    res.extras["brightest"] = brightest
+    res.extras["n_template_keypoints"] = int(inp.des_tpl.shape[0])
+    return res

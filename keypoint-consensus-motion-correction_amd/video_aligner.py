@@ -50,6 +50,35 @@ def _cv2_factory(name: str) -> Callable:
     return make
 
 
+class _CvKeyPoint:
+    __slots__ = ("pt",)
+
+    def __init__(self, x: float, y: float):
+        self.pt = (x, y)
+
+
+class GpuOrbDetector:
+    """The build's ORB-style detector (csrc/orb.hip) behind the OpenCV
+    detector interface the reference uses (VA:114-116, VA:190-192):
+    ``detectAndCompute(img_u8, mask) -> (keypoints with .pt, uint8 [n, 32] descriptors)``.
+    ``align_images`` recognises it and detects on the whole device-resident stack at once."""
+
+    def __init__(self, params=None):
+        from . import orb
+
+        self.params = params or orb.OrbParams()
+
+    def detectAndCompute(self, image, mask=None):  # noqa: N802 (OpenCV's name)
+        if mask is not None:
+            raise NotImplementedError("detection masks are not supported by the GPU detector")
+        dev = torch.device("cuda", torch.cuda.current_device())
+        img = image if isinstance(image, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(image, np.uint8))
+        k = stages.detect_orb(img.to(dev).reshape(1, *img.shape[-2:]).contiguous(), self.params)
+        n = int(k.count.cpu()[0])
+        kp = k.kp[0, :n].cpu().numpy()
+        return [_CvKeyPoint(float(x), float(y)) for x, y in kp], k.des[0, :n].cpu().numpy()
+
+
 def _as_numpy(x) -> np.ndarray:
     return x.cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
 
@@ -63,6 +92,8 @@ class VideoAligner:
     DETECTOR_CONSTRUCTOR_DICT = {
         "akaze": _cv2_factory("AKAZE_create"),
         "brisk": _cv2_factory("BRISK_create"),
+        # New: the build's exact ORB-style detector on the GPU (no OpenCV needed).
+        "orb": GpuOrbDetector,
     }
     N_KP_GLOBAL_MIN = 5
     N_KP_FRAME_SKIP = 3
@@ -150,16 +181,32 @@ class VideoAligner:
         dev = self._device()
         frames = images if on_device else torch.from_numpy(np.ascontiguousarray(images_np)).to(dev)
         brightest_px = self._get_brightest_px(frames)
-        images_i8 = self._max_scale_images(frames, None, brightest_px, np.uint8)[0].cpu().numpy()
+        u8_dev = self._max_scale_images(frames, None, brightest_px, np.uint8)[0]
         _, template_i8 = self._max_scale_images(None, template, brightest_px, np.uint8)
         frame_downsample_rate = max(1, frame_rate // self.FRAME_SAMPLE_RATE)
-        images_sample, template = self._downsample(images_i8, template_i8, frame_downsample_rate,
-                                                   self.SPATIAL_DOWNSAMPLE_RATE)
+        detector = self.DETECTOR_CONSTRUCTOR_DICT[detector_algorithm]()
+        on_gpu = (isinstance(detector, GpuOrbDetector) and frame_downsample_rate == 1
+                  and self.SPATIAL_DOWNSAMPLE_RATE == 1 and frames.dim() == 3)
+        if not on_gpu:
+            images_i8 = u8_dev.cpu().numpy()
+            images_sample, template = self._downsample(images_i8, template_i8, frame_downsample_rate,
+                                                       self.SPATIAL_DOWNSAMPLE_RATE)
         self.logger.info(f"normalized frames in: {round(time.time() - t_start)} s")
 
         self.logger.info("identifying keypoints...")
         t_start = time.time()
-        detector = self.DETECTOR_CONSTRUCTOR_DICT[detector_algorithm]()
+        if on_gpu:  # f1: detection of the whole stack on the device
+            kt = stages.detect_orb(torch.from_numpy(np.ascontiguousarray(template_i8)).to(dev)[None], detector.params)
+            kq = stages.detect_orb(u8_dev, detector.params)
+            n_t = int(kt.count.cpu()[0])
+            self._kp_template = kt.kp[0, :n_t].cpu().numpy()
+            self._des_template = kt.des[0, :n_t].cpu().numpy()
+            kp_q, des_q, q_off, q_off_host = stages.keypoints_csr(kq)
+            inp = _pl.SlabInputs(frames, kt.des[0, :n_t].contiguous(), kt.kp[0, :n_t].contiguous(), des_q, kp_q,
+                                 q_off, q_off_host)
+            self.logger.info(f"identified keypoints in: {round(time.time() - t_start)} s")
+            aligned, eu, skipped = self._align_inputs(inp, n_kp_global, frame_downsample_rate, patch)
+            return (aligned if on_device else aligned.cpu().numpy()), eu, skipped
         kp_t, des_t = detector.detectAndCompute(template, None)
         self._kp_template = np.array([p.pt for p in kp_t])
         self._des_template = des_t
@@ -213,6 +260,9 @@ class VideoAligner:
             q_off=torch.from_numpy(q_off).to(dev),
             q_off_host=q_off,
         )
+        return self._align_inputs(inp, n_kp_global, rate, patch, to_host=to_host)
+
+    def _align_inputs(self, inp, n_kp_global, rate, patch, to_host: bool = False):
         cfg = self._config(n_kp_global, rate)
         self.logger.info("generating keypoint consensus...")
         t_start = time.time()

@@ -170,3 +170,22 @@ def test_align_streamed_equals_device_resident(dev):
     torch.cuda.synchronize()
     assert np.array_equal(out.numpy(), ref.aligned.cpu().numpy())
     assert np.array_equal(res.affines, ref.affines)
+
+
+def test_align_images_with_gpu_orb_detector(dev):
+    """align_images from raw uint16 frames with the build's GPU detector: normalisation,
+    detection, matching, consensus, RANSAC and warp all on the device; the recovered
+    translations are the synthetic jitter (integer shifts of a textured scene)."""
+    rng = np.random.default_rng(31)
+    H, W, F = 200, 260, 8
+    lo = rng.integers(0, 60000, (H // 4 + 8, W // 4 + 8)).astype(np.float64)
+    scene = np.clip(np.kron(lo, np.ones((4, 4))) + rng.normal(0, 800, (H + 32, W + 32)), 0, 65535).astype(np.uint16)
+    shifts = [(int(a), int(b)) for a, b in rng.integers(-6, 7, (F, 2))]
+    shifts[F // 2] = (0, 0)  # the template frame
+    imgs = np.stack([scene[16 + dy:16 + dy + H, 16 + dx:16 + dx + W] for dy, dx in shifts])
+    aligned, eu, skipped = VideoAligner().align_images(imgs, n_kp_global=60, detector_algorithm="orb", frame_rate=30)
+    assert skipped == [] and aligned.shape == imgs.shape and aligned.dtype == np.uint16
+    np.testing.assert_allclose(eu[:, 0], [dx for dy, dx in shifts], atol=1e-6)
+    np.testing.assert_allclose(eu[:, 1], [dy for dy, dx in shifts], atol=1e-6)
+    res = pipeline.align_frames(torch.from_numpy(imgs).to(dev), pipeline.AlignConfig(n_kp_global=60))
+    assert np.array_equal(res.aligned.cpu().numpy(), aligned)
