@@ -20,11 +20,12 @@
 // orb_candidates_kernel  one workgroup per 64x16 tile: image + 4-px halo in LDS, FAST
 //                        scores for the tile + 1-px halo, NMS, Harris, ordered
 //                        compaction of the tile's candidates (block scan).
-// orb_select_kernel      one workgroup per frame: radix-select of the n_features-th
-//                        largest key over all tiles, then ordered compaction per tile.
-// orb_smooth_kernel      5x5 binomial smoothing of the frame.
+// orb_offsets_kernel +   per frame: tile prefix offsets, then one wave per tile copies
+// orb_gather_kernel      its candidates into the frame's compact list (candidate order).
+// orb_select_kernel      one workgroup per frame: radix select of the n_features-th
+//                        largest key, ordered compaction of the kept candidates.
 // orb_describe_kernel    one wave per keypoint: moments (wave reduction), bin, 4 x 64
-//                        BRIEF comparisons packed with ballots.
+//                        BRIEF comparisons of on-the-fly smoothed samples (ballots).
 #include <cmath>
 
 #include "kcmc_internal.h"
@@ -99,6 +100,15 @@ __global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t*
     if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3) {
       const int py = r - 1 + kHalo, px = c - 1 + kHalo;  // position in img
       const int v = img[py][px];
+      // a 9-pixel arc covers at least two of the four compass pixels (0, 4, 8, 12):
+      // fewer than two beyond the threshold on the same side -> not a corner (score 0)
+      const int n0 = img[py + 3][px], n4 = img[py][px + 3], n8 = img[py - 3][px], n12 = img[py][px - 3];
+      const int hi = (n0 > v + threshold) + (n4 > v + threshold) + (n8 > v + threshold) + (n12 > v + threshold);
+      const int lo = (n0 < v - threshold) + (n4 < v - threshold) + (n8 < v - threshold) + (n12 < v - threshold);
+      if (hi < 2 && lo < 2) {
+        sc[r][c] = 0;
+        continue;
+      }
       int d[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) d[j] = (int)img[py + c_circle[j][1]][px + c_circle[j][0]] - v;
@@ -176,49 +186,77 @@ __global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t*
   if (tid == 0) cand_cnt[(size_t)f * nty * ntx + tile] = total;
 }
 
-// One workgroup per frame: the n_features-th largest key by 8-bit radix select over all
-// tiles' slots, then the kept candidates compacted tile by tile in candidate order.
-__global__ __launch_bounds__(kThreads) void orb_select_kernel(const uint64_t* __restrict__ cand_key,
+// Per frame, one wave per tile (in tile order): the tile's candidates are appended to
+// the frame's compact list at the tile's prefix offset, keeping candidate order.
+__global__ __launch_bounds__(kThreads) void orb_gather_kernel(const uint64_t* __restrict__ cand_key,
                                                               const uint32_t* __restrict__ cand_pos,
-                                                              const int32_t* __restrict__ cand_cnt, int ntiles,
-                                                              int n_features, double* __restrict__ out_kp_frame,
-                                                              uint32_t* __restrict__ out_pos, int32_t* __restrict__ out_n,
-                                                              int f_base) {
+                                                              const int32_t* __restrict__ cand_cnt,
+                                                              const int32_t* __restrict__ tile_off, int ntiles,
+                                                              uint64_t* __restrict__ list_key,
+                                                              uint32_t* __restrict__ list_pos) {
+  const int f = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const size_t fb = (size_t)f * ntiles;
+  for (int t = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); t < ntiles; t += gridDim.x * (kThreads / 64)) {
+    const int cnt = cand_cnt[fb + t];
+    const int off = tile_off[fb + t];
+    for (int s = lane; s < cnt; s += 64) {
+      list_key[fb * kSlots + off + s] = cand_key[(fb + t) * kSlots + s];
+      list_pos[fb * kSlots + off + s] = cand_pos[(fb + t) * kSlots + s];
+    }
+  }
+}
+
+// Per frame (one workgroup): exclusive prefix of the tile counts -> tile offsets, total.
+__global__ __launch_bounds__(kThreads) void orb_offsets_kernel(const int32_t* __restrict__ cand_cnt, int ntiles,
+                                                               int32_t* __restrict__ tile_off,
+                                                               int32_t* __restrict__ total) {
+  __shared__ int s_warp[kThreads / 64];
+  const int f = blockIdx.x;
+  int carry = 0;
+  for (int t0 = 0; t0 < ntiles; t0 += kThreads) {
+    const int t = t0 + threadIdx.x;
+    const int c = t < ntiles ? cand_cnt[(size_t)f * ntiles + t] : 0;
+    int ex;
+    const int tot = block_excl_scan(c, s_warp, ex);
+    if (t < ntiles) tile_off[(size_t)f * ntiles + t] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) total[f] = carry;
+}
+
+// One workgroup per frame: the n_features-th largest key T of the compact list by 8-bit
+// radix select, then the kept candidates (key > T, and the first ties) compacted in
+// list order.
+__global__ __launch_bounds__(kThreads) void orb_select_kernel(const uint64_t* __restrict__ list_key,
+                                                              const uint32_t* __restrict__ list_pos,
+                                                              const int32_t* __restrict__ total_n, int ntiles,
+                                                              int n_features, double* __restrict__ out_kp,
+                                                              uint32_t* __restrict__ out_pos,
+                                                              int32_t* __restrict__ out_n, int f_base) {
   __shared__ int hist[256];
   __shared__ int s_warp[kThreads / 64];
   __shared__ uint64_t s_prefix;
-  __shared__ int s_rank, s_total;
+  __shared__ int s_rank;
   const int f = blockIdx.x;
   const int tid = threadIdx.x;
-  const uint64_t* K = cand_key + (size_t)f * ntiles * kSlots;
-  const uint32_t* Pp = cand_pos + (size_t)f * ntiles * kSlots;
-  const int32_t* Cn = cand_cnt + (size_t)f * ntiles;
-
-  int my = 0;
-  for (int t = tid; t < ntiles; t += kThreads) my += Cn[t];
-  for (int o = 32; o > 0; o >>= 1) my += __shfl_xor(my, o);
-  if ((tid & 63) == 0) s_warp[tid >> 6] = my;
-  __syncthreads();
-  if (tid == 0) s_total = s_warp[0] + s_warp[1] + s_warp[2] + s_warp[3];
-  __syncthreads();
-  const int total = s_total;
-
-  uint64_t T = 0;  // keep key > T, and ties (key == T) up to n_features in candidate order
-  int n_gt = 0;
+  const uint64_t* K = list_key + (size_t)f * ntiles * kSlots;
+  const uint32_t* Pp = list_pos + (size_t)f * ntiles * kSlots;
+  const int total = total_n[f];
   const bool all = total <= n_features;
+  uint64_t T = 0;
+  int n_gt = 0;
   if (!all) {
     if (tid == 0) {
       s_prefix = 0;
-      s_rank = n_features;  // the wanted key is the s_rank-th largest among the matching ones
+      s_rank = n_features;
     }
     for (int d = 7; d >= 0; --d) {
       hist[tid] = 0;
       __syncthreads();
       const uint64_t prefix = s_prefix;
       const uint64_t hmask = d == 7 ? 0ull : (~0ull << (8 * (d + 1)));
-      for (int i = tid; i < ntiles * kSlots; i += kThreads) {
-        const int t = i >> 8, s = i & (kSlots - 1);
-        if (s >= Cn[t]) continue;
+      for (int i = tid; i < total; i += kThreads) {
         const uint64_t k = K[i];
         if ((k & hmask) == prefix) atomicAdd(&hist[(k >> (8 * d)) & 255], 1);
       }
@@ -237,61 +275,49 @@ __global__ __launch_bounds__(kThreads) void orb_select_kernel(const uint64_t* __
     T = s_prefix;
     n_gt = n_features - s_rank;  // keys strictly above T
   }
-  // ordered compaction, one tile (<= 256 slots) per step
   int out = 0, ties = 0;
-  for (int t = 0; t < ntiles; ++t) {
-    const int cnt = Cn[t];
-    if (cnt == 0) continue;  // uniform across the block
-    const int i = t * kSlots + tid;
+  for (int i0 = 0; i0 < total; i0 += kThreads) {
+    const int i = i0 + tid;
     int keep = 0, tie = 0;
-    if (tid < cnt) {
+    if (i < total) {
       const uint64_t k = K[i];
       keep = all || k > T;
       tie = !all && k == T;
     }
-    int tie_excl;
-    const int tie_total = block_excl_scan(tie, s_warp, tie_excl);
-    if (tie && ties + tie_excl < n_features - n_gt) keep = 1;
+    int tie_ex;
+    const int tie_tot = block_excl_scan(tie, s_warp, tie_ex);
+    if (tie && ties + tie_ex < n_features - n_gt) keep = 1;
     int ex;
-    const int kept_total = block_excl_scan(keep, s_warp, ex);
+    const int kept = block_excl_scan(keep, s_warp, ex);
     if (keep) {
       const uint32_t pp = Pp[i];
       const size_t o = (size_t)(f_base + f) * n_features + out + ex;
       out_pos[o] = pp;
-      out_kp_frame[2 * o] = (double)(pp & 0xffffu);
-      out_kp_frame[2 * o + 1] = (double)(pp >> 16);
+      out_kp[2 * o] = (double)(pp & 0xffffu);
+      out_kp[2 * o + 1] = (double)(pp >> 16);
     }
-    out += kept_total;
-    ties += tie_total;
+    out += kept;
+    ties += tie_tot;
   }
   if (tid == 0) out_n[f_base + f] = out;
 }
 
-__global__ __launch_bounds__(kThreads) void orb_smooth_kernel(const uint8_t* __restrict__ src, int H, int W,
-                                                              uint8_t* __restrict__ dst) {
-  const size_t n = (size_t)H * W;
-  const int f = blockIdx.y;
-  const uint8_t* I = src + (size_t)f * n;
-  uint8_t* O = dst + (size_t)f * n;
-  for (size_t p = blockIdx.x * (size_t)kThreads + threadIdx.x; p < n; p += (size_t)gridDim.x * kThreads) {
-    const int y = (int)(p / W), x = (int)(p - (size_t)y * W);
-    int v = 0;
-    if (y >= 2 && y < H - 2 && x >= 2 && x < W - 2) {
-      const int w[5] = {1, 4, 6, 4, 1};
-      int s = 0;
+// 5x5 binomial smoothing at one point: (sum w_i w_j I + 128) >> 8, w = 1 4 6 4 1.
+__device__ __forceinline__ int smooth5(const uint8_t* __restrict__ I, int W, int x, int y) {
+  int s = 0;
+  const int w[5] = {1, 4, 6, 4, 1};
 #pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        const uint8_t* row = I + (size_t)(y + i - 2) * W + x - 2;
-        s += w[i] * ((int)row[0] + 4 * (int)row[1] + 6 * (int)row[2] + 4 * (int)row[3] + (int)row[4]);
-      }
-      v = (s + 128) >> 8;
-    }
-    O[p] = (uint8_t)v;
+  for (int i = 0; i < 5; ++i) {
+    const uint8_t* row = I + (size_t)(y + i - 2) * W + x - 2;
+    s += w[i] * ((int)row[0] + 4 * (int)row[1] + 6 * (int)row[2] + 4 * (int)row[3] + (int)row[4]);
   }
+  return (s + 128) >> 8;
 }
 
-__global__ __launch_bounds__(kThreads) void orb_describe_kernel(const uint8_t* __restrict__ frames,
-                                                                const uint8_t* __restrict__ smooth, int H, int W,
+// One wave per keypoint: intensity-centroid moments (wave reduction), exact bin, then
+// 4 x 64 BRIEF comparisons of on-the-fly smoothed samples packed with ballots (the
+// 31x31 patch stays in L1, cheaper than smoothing whole frames for 500 keypoints).
+__global__ __launch_bounds__(kThreads) void orb_describe_kernel(const uint8_t* __restrict__ frames, int H, int W,
                                                                 const uint32_t* __restrict__ kp_pos,
                                                                 const int32_t* __restrict__ kp_n, int n_features,
                                                                 const int8_t* __restrict__ pattern,
@@ -305,7 +331,6 @@ __global__ __launch_bounds__(kThreads) void orb_describe_kernel(const uint8_t* _
   const uint32_t pp = kp_pos[slot];
   const int x = (int)(pp & 0xffffu), y = (int)(pp >> 16);
   const uint8_t* I = frames + (size_t)f * H * W;
-  const uint8_t* S = smooth + (size_t)f * H * W;
   int m10 = 0, m01 = 0;
   for (int i = lane; i < 31 * 31; i += 64) {
     const int dy = i / 31 - 15, dx = i % 31 - 15;
@@ -333,8 +358,8 @@ __global__ __launch_bounds__(kThreads) void orb_describe_kernel(const uint8_t* _
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int pi = 64 * r + lane;
-    const int p = S[(size_t)(y + pt[4 * pi + 1]) * W + (x + pt[4 * pi])];
-    const int q = S[(size_t)(y + pt[4 * pi + 3]) * W + (x + pt[4 * pi + 2])];
+    const int p = smooth5(I, W, x + pt[4 * pi], y + pt[4 * pi + 1]);
+    const int q = smooth5(I, W, x + pt[4 * pi + 2], y + pt[4 * pi + 3]);
     const unsigned long long m = __ballot(p < q);
     if (lane == 0) {
 #pragma unroll
@@ -363,31 +388,34 @@ extern "C" int kcmc_orb_detect(kcmc_ctx* ctx, const uint8_t* frames, int n_frame
   KCMC_TRY(hip_check(hipMemsetAsync(out_count, 0, (size_t)n_frames * sizeof(int32_t), s), "hipMemsetAsync"));
   if (n_features == 0 || H < 2 * edge + 1 || W < 2 * edge + 1) return KCMC_OK;
   const int ntx = ceil_div(W, kTW), nty = ceil_div(H, kTH), ntiles = ntx * nty;
-  // frames are processed in batches so that the candidate slots and the smoothed
-  // copy stay a bounded workspace
-  const size_t per_frame = (size_t)ntiles * kSlots * (sizeof(uint64_t) + sizeof(uint32_t)) +
-                           (size_t)ntiles * sizeof(int32_t) + (size_t)H * W;
+  // frames are processed in batches so that the candidate slots stay a bounded workspace
+  const size_t slots = (size_t)ntiles * kSlots;
+  const size_t per_frame = 2 * slots * (sizeof(uint64_t) + sizeof(uint32_t)) + (size_t)ntiles * 2 * sizeof(int32_t) + 4;
   int batch = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_frames, ((size_t)1 << 30) / per_frame));
   batch = std::min(batch, 65535);
   void* ws = nullptr;
   KCMC_TRY(workspace_alloc(ctx, &ws, per_frame * batch + (size_t)n_frames * n_features * sizeof(uint32_t) + 64, s));
   uint64_t* ckey = static_cast<uint64_t*>(ws);
-  uint32_t* cpos = reinterpret_cast<uint32_t*>(ckey + (size_t)batch * ntiles * kSlots);
-  int32_t* ccnt = reinterpret_cast<int32_t*>(cpos + (size_t)batch * ntiles * kSlots);
-  uint8_t* smooth = reinterpret_cast<uint8_t*>(ccnt + (size_t)batch * ntiles);
-  uint32_t* kpos = reinterpret_cast<uint32_t*>(smooth + (size_t)batch * H * W + 16 - (((size_t)batch * H * W) & 15));
+  uint64_t* lkey = ckey + (size_t)batch * slots;
+  uint32_t* cpos = reinterpret_cast<uint32_t*>(lkey + (size_t)batch * slots);
+  uint32_t* lpos = cpos + (size_t)batch * slots;
+  int32_t* ccnt = reinterpret_cast<int32_t*>(lpos + (size_t)batch * slots);
+  int32_t* toff = ccnt + (size_t)batch * ntiles;
+  int32_t* ctot = toff + (size_t)batch * ntiles;
+  uint32_t* kpos = reinterpret_cast<uint32_t*>(ctot + batch);
   int rc = KCMC_OK;
   for (int f0 = 0; f0 < n_frames && rc == KCMC_OK; f0 += batch) {
     const int nb = std::min(batch, n_frames - f0);
     const uint8_t* fr = frames + (size_t)f0 * H * W;
     hipLaunchKernelGGL(orb_candidates_kernel, dim3(ntx, nty, nb), dim3(kThreads), 0, s, fr, H, W, threshold, harris_k,
                        edge, ckey, cpos, ccnt);
-    hipLaunchKernelGGL(orb_select_kernel, dim3(nb), dim3(kThreads), 0, s, ckey, cpos, ccnt, ntiles, n_features, out_kp,
+    hipLaunchKernelGGL(orb_offsets_kernel, dim3(nb), dim3(kThreads), 0, s, ccnt, ntiles, toff, ctot);
+    hipLaunchKernelGGL(orb_gather_kernel, dim3(ceil_div(ntiles, 4 * 8), nb), dim3(kThreads), 0, s, ckey, cpos, ccnt,
+                       toff, ntiles, lkey, lpos);
+    hipLaunchKernelGGL(orb_select_kernel, dim3(nb), dim3(kThreads), 0, s, lkey, lpos, ctot, ntiles, n_features, out_kp,
                        kpos, out_count, f0);
-    const unsigned sgrid = (unsigned)std::min<size_t>(((size_t)H * W + kThreads - 1) / kThreads, 1024);
-    hipLaunchKernelGGL(orb_smooth_kernel, dim3(sgrid, nb), dim3(kThreads), 0, s, fr, H, W, smooth);
-    hipLaunchKernelGGL(orb_describe_kernel, dim3(ceil_div(n_features, kThreads / 64), nb), dim3(kThreads), 0, s, fr,
-                       smooth, H, W, kpos, out_count, n_features, pattern, bin_cs, f0, out_des);
+    hipLaunchKernelGGL(orb_describe_kernel, dim3(ceil_div(n_features, kThreads / 64), nb), dim3(kThreads), 0, s, fr, H,
+                       W, kpos, out_count, n_features, pattern, bin_cs, f0, out_des);
     rc = launch_check("orb kernels");
   }
   const int rc2 = workspace_free(ctx, ws, s);
