@@ -22,13 +22,17 @@ namespace {
 constexpr int kThreads = 256;
 
 // bins[(v >> shift) & 255] over the values with (v >> 8) == match (match < 0: all).
+// Video values crowd into a few coarse bins, so same-address LDS atomics would
+// serialise: each wave keeps 8 sub-histograms (lane & 7), 32 per workgroup (32 KB).
+constexpr int kReplicas = 8;
+
 __global__ __launch_bounds__(kThreads) void hist256_u16_kernel(const uint16_t* __restrict__ src, size_t n, int shift,
                                                                int match, unsigned long long* __restrict__ out) {
-  __shared__ uint32_t h[4][256];  // one sub-histogram per wave
+  __shared__ uint32_t h[kThreads / 64 * kReplicas][256];
   const int tid = threadIdx.x, wave = tid >> 6;
-  for (int i = tid; i < 4 * 256; i += kThreads) (&h[0][0])[i] = 0u;
+  for (int i = tid; i < kThreads / 64 * kReplicas * 256; i += kThreads) (&h[0][0])[i] = 0u;
   __syncthreads();
-  uint32_t* hw = h[wave];
+  uint32_t* hw = h[wave * kReplicas + (tid & (kReplicas - 1))];
   const size_t n8 = n / 8;
   const uint4* s8 = reinterpret_cast<const uint4*>(src);
   const size_t stride = (size_t)gridDim.x * kThreads;
@@ -52,7 +56,8 @@ __global__ __launch_bounds__(kThreads) void hist256_u16_kernel(const uint16_t* _
   }
   __syncthreads();
   for (int b = tid; b < 256; b += kThreads) {
-    const unsigned long long c = (unsigned long long)h[0][b] + h[1][b] + h[2][b] + h[3][b];
+    unsigned long long c = 0;
+    for (int r = 0; r < kThreads / 64 * kReplicas; ++r) c += h[r][b];
     if (c) atomicAdd(&out[b], c);
   }
 }
