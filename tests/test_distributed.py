@@ -19,7 +19,7 @@ from kcmc_amd import distributed as kdist, pipeline, synthetic
 F_PER_RANK, N_TPL, D, HW = 6, 80, 32, (64, 96)
 
 
-def _oracle_stages():
+def _oracle_stages(model="euclidean"):
     import oracle
 
     def match(inp, cfg):
@@ -37,22 +37,26 @@ def _oracle_stages():
 
     def ransac(kp_ordered, kp_tpl, pt_off, pt_idx, cfg):
         kq, kt = kp_ordered.numpy(), kp_tpl.numpy()
-        out = np.full((len(pt_off) - 1, 2, 3), np.nan)
+        out = np.full((len(pt_off) - 1,) + ((3, 3) if model == "projective" else (2, 3)), np.nan)
         for f in range(len(pt_off) - 1):
             L = pt_idx[pt_off[f]:pt_off[f + 1]]
-            if len(L) >= cfg.n_kp_frame_skip:
-                out[f] = oracle.ransac_rigid(kq[f][L], kt[L])[0]
+            if len(L) >= cfg.effective_frame_skip:
+                if model == "euclidean":
+                    out[f] = oracle.ransac_rigid(kq[f][L], kt[L])[0]
+                else:
+                    out[f] = oracle.ransac_model(kq[f][L], kt[L], model)[0][: out.shape[1]]
         return torch.from_numpy(out)
 
     def warp(frames, affines):
         fr = frames.numpy()
-        return torch.from_numpy(np.stack([oracle.warp_affine_u16(fr[f], affines[f]) for f in range(len(fr))]))
+        fn = oracle.warp_perspective_u16 if model == "projective" else oracle.warp_affine_u16
+        return torch.from_numpy(np.stack([fn(fr[f], affines[f]) for f in range(len(fr))]))
 
     return kdist.SlabStages(match, ransac, warp)
 
 
-def _slab(rank, n_frames):
-    ks = synthetic.make_keypoints(n_frames, N_TPL, D, HW, seed=5, frame_seed=rank)
+def _slab(rank, n_frames, model="euclidean"):
+    ks = synthetic.make_keypoints(n_frames, N_TPL, D, HW, seed=5, frame_seed=rank, model=model)
     base = synthetic.make_texture(HW, seed=1)
     frames = torch.from_numpy(np.broadcast_to(base, (n_frames,) + HW).copy())
     return pipeline.SlabInputs(frames, torch.from_numpy(ks.des_tpl), torch.from_numpy(ks.kp_tpl),
@@ -60,16 +64,16 @@ def _slab(rank, n_frames):
                                torch.from_numpy(ks.q_off), ks.q_off)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, model):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    inp = _slab(rank, F_PER_RANK + rank)  # uneven slabs on purpose
+    inp = _slab(rank, F_PER_RANK + rank, model)  # uneven slabs on purpose
     if rank != 0:  # the template comes from rank 0 by broadcast
         inp.des_tpl.zero_()
         inp.kp_tpl.zero_()
     kdist.broadcast_template(inp.des_tpl, inp.kp_tpl)
-    cfg = pipeline.AlignConfig(n_kp_global=20)
-    res = kdist.align_sharded(inp, cfg, impl=_oracle_stages())
+    cfg = pipeline.AlignConfig(n_kp_global=20, ransac_model=model)
+    res = kdist.align_sharded(inp, cfg, impl=_oracle_stages(model))
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), aligned=res.aligned.numpy(), affines=res.affines,
              euclid=res.euclidean, skipped=np.array(res.skipped), interp=np.array(res.interpolated))
     dist.destroy_process_group()
@@ -84,14 +88,15 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_sharded_pipeline_matches_single_process(tmp_path):
+@pytest.mark.parametrize("model", ["euclidean", "affine", "projective"])
+def test_sharded_pipeline_matches_single_process(tmp_path, model):
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), model), nprocs=world, join=True)
     r = [np.load(os.path.join(tmp_path, f"rank{k}.npz")) for k in range(world)]
     # single-process reference over the concatenated slabs, same stages
-    slabs = [_slab(k, F_PER_RANK + k) for k in range(world)]
-    st = _oracle_stages()
-    cfg = pipeline.AlignConfig(n_kp_global=20)
+    slabs = [_slab(k, F_PER_RANK + k, model) for k in range(world)]
+    st = _oracle_stages(model)
+    cfg = pipeline.AlignConfig(n_kp_global=20, ransac_model=model)
     kb, kq = zip(*[st.match(s, cfg) for s in slabs])
     keep = torch.cat(kb).numpy()
     cons = pipeline.consensus_stage(keep, N_TPL, keep.shape[0], cfg)
