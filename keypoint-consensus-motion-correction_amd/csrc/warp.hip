@@ -22,9 +22,16 @@
 // zoom-out or rotation) gather from global memory instead; tiles whose box misses the
 // image store zeros.
 //
+// One-channel frames with W % 8 == 0 and a box that fits a fixed 144-pixel LDS pitch (the
+// near-identity maps of motion correction) take a leaner form of the same path (mode 3,
+// fast_rows): scalar per-row origins from a per-frame table, immediate-offset taps, buffer
+// stores, and a per-tile choice of blend from the staged values (exact integer blend with
+// no range check when every value is < 16384; OpenCV's float blend on packed fp32 for
+// bright boxes).
+//
 // Two launches: warp_plan_kernel (one thread per tile) inverts the map in fp64 and
-// derives each tile's source box, so that the tile kernel starts with scalar loads of
-// its plan and issues its staging loads immediately; warp_affine_u16_kernel then makes
+// derives each tile's source box and the frame's row-origin table, so that the tile
+// kernel starts with scalar loads of its plan and issues its staging loads immediately; warp_affine_u16_kernel then makes
 // one tile per workgroup, latency hidden by the other resident workgroups (a persistent
 // double-buffered variant measured 25% slower).
 #include <climits>
@@ -60,6 +67,20 @@ struct CfgFor<3> {
 template <>
 struct CfgFor<4> {
   using type = ChanCfg;
+};
+
+// Fast staged path (mode 3; one channel, W % 8 == 0, the near-identity maps of motion
+// correction): the box is staged at a fixed LDS pitch, so the lower tap row is an
+// immediate offset of the upper one, and the per-row source origins come from a per-frame
+// table through scalar loads.  Boxes wider than kFastPitch or taller than kFastRows take
+// the general staged path (mode 0).
+constexpr int kFastPitch = 144;           // pixels: 128-px tile + up to ~8 deg / 6 % zoom
+constexpr int kFastChunks = kFastPitch / 8;  // 16-byte chunks per staged row
+template <class Cfg>
+struct Fast {
+  static constexpr int kRows = (Cfg::kLdsElems - 8) / kFastPitch;  // the last 16 bytes: per-wave flags
+  static constexpr int kFlagWord = Cfg::kLdsElems / 2 - 4;          // uint32 index of the flags
+  static constexpr int kPasses = (kRows * kFastChunks + kThreads - 1) / kThreads;
 };
 
 __device__ __forceinline__ int cv_round(double v) { return (int)__builtin_rint(v); }
@@ -243,6 +264,125 @@ __device__ __forceinline__ uint16_t round_q10(uint32_t S) {
 
 __device__ __forceinline__ uint32_t tap(const uint16_t* stile, int i) { return stile[i]; }
 
+
+// Fast-path staging: chunk q = tid + 256k of the box in row-major order at kFastChunks
+// chunks per row (LDS offset 16q); chunks right of the box's own pitch are left unwritten
+// (never read).
+template <class Cfg>
+__device__ __forceinline__ void fast_stage_issue(const uint16_t* __restrict__ S, int ax0, int sy0, int cpr, int rows,
+                                                 int H, int W, int tid, uint4 (&chunk)[Fast<Cfg>::kPasses]) {
+#pragma unroll
+  for (int k = 0; k < Fast<Cfg>::kPasses; ++k) {
+    const int q = tid + kThreads * k;
+    const int r = q / kFastChunks, c = q - r * kFastChunks;
+    const int gy = sy0 + r, gx = ax0 + 8 * c;
+    chunk[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (r < rows && c < cpr && (unsigned)gx < (unsigned)W && (unsigned)gy < (unsigned)H)
+      chunk[k] = *reinterpret_cast<const uint4*>(S + (size_t)gy * W + gx);
+  }
+}
+
+template <class Cfg>
+__device__ __forceinline__ void fast_stage_land(uint16_t* stile, int cpr, int rows, int tid,
+                                                const uint4 (&chunk)[Fast<Cfg>::kPasses]) {
+#pragma unroll
+  for (int k = 0; k < Fast<Cfg>::kPasses; ++k) {
+    const int q = tid + kThreads * k;
+    const int r = q / kFastChunks, c = q - r * kFastChunks;
+    if (r < rows && c < cpr) reinterpret_cast<uint4*>(stile)[q] = chunk[k];
+  }
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// OpenCV's float evaluation of remapBilinear's blend, ((v00 w0 + v01 w1) + v10 w2) + v11 w3
+// with separately rounded products and w_k = K_k / 1024 exactly (the 2^-10 scaling commutes
+// with every rounding), then cvRound: packed fp32 over the lane's two pixels; returns the
+// two results in the low 16 bits of each float.
+__device__ __forceinline__ f32x2 blend_float2(const uint32_t (&v)[2][4], const uint32_t (&fx)[2],
+                                              const uint32_t (&fy)[2]) {
+  const f32x2 fxf = {(float)fx[0], (float)fx[1]}, fyf = {(float)fy[0], (float)fy[1]};
+  const f32x2 axf = 32.0f - fxf, ayf = 32.0f - fyf;
+  const f32x2 t0 = {(float)v[0][0], (float)v[1][0]}, t1 = {(float)v[0][1], (float)v[1][1]};
+  const f32x2 t2 = {(float)v[0][2], (float)v[1][2]}, t3 = {(float)v[0][3], (float)v[1][3]};
+  const f32x2 sum = ((t0 * (ayf * axf) + t1 * (ayf * fxf)) + t2 * (fyf * axf)) + t3 * (fyf * fxf);
+  // cvRound(sum / 1024): one rounding of the exact sum * 2^-10 + 1.5 * 2^23
+  f32x2 q;
+  q[0] = __builtin_fmaf(sum[0], 0x1p-10f, 0x1.8p23f);
+  q[1] = __builtin_fmaf(sum[1], 0x1p-10f, 0x1.8p23f);
+  return q;
+}
+
+// Blend of a mode-3 tile, chosen once per tile from its staged box:
+enum FastBlend {
+  kDark = 0,    // every staged value < 16384: S = sum v_k K_k < 2^24, so the exact separable
+                // integer evaluation of output_rows IS OpenCV's float result; no range check
+  kMixed = 1,   // some bright values: per output row (wave-uniform), the integer blend when
+                // all the row's taps are < 16384, blend_float2 otherwise
+  kBright = 2,  // bright regions over much of the box: blend_float2 throughout
+};
+// kBright above this fraction of bright staged chunks: a float row costs ~1.25x an integer
+// row, and a kMixed row pays ~10 % for its tap test (tools/warp_lab at config 2: dark
+// 2.85 ms, all-bright 3.56 ms).
+constexpr int kBrightShare = 3;  // bright chunks * kBrightShare > box chunks -> kBright
+
+// Output rows of a mode-3 tile, with the per-row overheads of output_rows removed: row
+// origins are scalar, the lower tap row is an immediate LDS offset, the store is a buffer
+// store with the row offset in soffset.
+template <class Cfg, int BLEND>
+__device__ __forceinline__ void fast_rows(const uint16_t* stile, const int2* __restrict__ rt, int ox, int oy,
+                                          uint16_t* __restrict__ Dst, int H, int W, int xb, int yb, int wave, int lane,
+                                          const int (&ad)[2], const int (&bd)[2]) {
+  const uint32_t xoff = 2u * (uint32_t)(xb + 2 * lane);  // byte offset of the lane's pixel pair
+  const bool store_ok = xb + 2 * lane + 2 <= W;          // W is even here
+  const __amdgpu_buffer_rsrc_t dst_rsrc = __builtin_amdgcn_make_buffer_rsrc(Dst, 0, 2 * H * W, 0x00020000);
+  int2 org[Cfg::kTileH / 4];  // all row origins up front (scalar loads; the table is padded)
+#pragma unroll
+  for (int i = 0; i < Cfg::kTileH / 4; ++i) org[i] = rt[i];
+#pragma unroll
+  for (int i = 0; i < Cfg::kTileH / 4; ++i) {
+    const int y = yb + wave + 4 * i;  // wave-uniform
+    if (y >= H) break;
+    const int X0 = org[i].x - ox, Y0 = org[i].y - oy;
+    uint32_t v[2][4], fx[2], fy[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int tX = X0 + ad[p], tY = Y0 + bd[p];
+      fx[p] = (tX >> 5) & 31;
+      fy[p] = (tY >> 5) & 31;
+      const uint16_t* t = stile + __umul24((uint32_t)(tY >> 10), (uint32_t)kFastPitch) + (uint32_t)(tX >> 10);
+      v[p][0] = t[0];
+      v[p][1] = t[1];
+      v[p][2] = t[kFastPitch];
+      v[p][3] = t[kFastPitch + 1];
+    }
+    bool use_float = BLEND == kBright;
+    if constexpr (BLEND == kMixed) {
+      const uint32_t taps = (v[0][0] | v[0][1] | v[0][2]) | (v[0][3] | v[1][0] | v[1][1]) | (v[1][2] | v[1][3]);
+      use_float = __builtin_amdgcn_ballot_w64((taps & 0xc000u) != 0) != 0;  // wave-uniform
+    }
+    f32x2 q;
+    if (use_float) {
+      q = blend_float2(v, fx, fy);
+    } else {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const uint32_t ax = 32 - fx[p], ay = 32 - fy[p];
+        uint32_t h0 = __umul24(v[p][0], ax) + __umul24(v[p][1], fx[p]);
+        uint32_t h1 = __umul24(v[p][2], ax) + __umul24(v[p][3], fx[p]);
+        asm volatile("" : "+v"(h0), "+v"(h1));  // keep the separable form (see output_rows)
+        q[p] = (float)(__umul24(h0, ay) + __umul24(h1, fy[p]));
+      }
+      // rint(S / 1024) in the low bits: fl(S) + 1.5 * 2^33 rounds (half to even) to a
+      // multiple of 1024, the float's unit in the last place there
+      q += 0x1.8p33f;
+    }
+    const uint32_t out = __builtin_amdgcn_perm(__float_as_uint(q[1]), __float_as_uint(q[0]), 0x05040100u);
+    // aux 2 = nontemporal: the aligned frame is written once and not re-read here
+    if (store_ok) __builtin_amdgcn_raw_buffer_store_b32(out, dst_rsrc, xoff, 2 * y * W, 2);
+  }
+}
+
 // Per-tile plan made by warp_plan_kernel.
 struct TilePlan {
   int mode, ax0, sy0;
@@ -265,15 +405,20 @@ __device__ __forceinline__ Box unpack(const TilePlan& t) {
 // in fixed point, so the fractional bits are unchanged): coordinates are box-relative.
 // Columns past the frame edge reuse the last valid column's coordinates so that their
 // (never stored) taps stay inside the box.
-template <class Cfg>
-__device__ __forceinline__ void lane_coords(const double* __restrict__ M, int xb, int yb, int W, int wave, int lane,
-                                            int ox, int oy, int (&ad)[2], int (&bd)[2], int& X0v, int& Y0v) {
+__device__ __forceinline__ void lane_cols(const double* __restrict__ M, int xb, int W, int lane, int (&ad)[2],
+                                          int (&bd)[2]) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int x = min(xb + 2 * lane + q, W - 1);
     ad[q] = cv_round(M[0] * x * 1024);
     bd[q] = cv_round(M[3] * x * 1024);
   }
+}
+
+template <class Cfg>
+__device__ __forceinline__ void lane_coords(const double* __restrict__ M, int xb, int yb, int W, int wave, int lane,
+                                            int ox, int oy, int (&ad)[2], int (&bd)[2], int& X0v, int& Y0v) {
+  lane_cols(M, xb, W, lane, ad, bd);
   const int y = yb + wave + 4 * min(lane, Cfg::kTileH / 4 - 1);
   X0v = cv_round((M[1] * y + M[2]) * 1024) + 16 - ox * 1024;
   Y0v = cv_round((M[4] * y + M[5]) * 1024) + 16 - oy * 1024;
@@ -398,20 +543,31 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
 // ------------------------------------------------------------------------- plan
 // One thread per tile (tile id = (f * nty + ty) * ntx + tx): the fp64 map inversion
 // (written once per frame to minv) and the tile's source box.
+// Also the frame's row-origin table for the fast path: rowtab[f][y & 3][y >> 2] =
+// (X0(y), Y0(y)) = (cvRound((M1*y + M2)*1024) + 16, cvRound((M4*y + M5)*1024) + 16), so
+// that a wave's rows y = yb + wave + 4i are consecutive entries; the tiles of a tile row
+// share its rows.
 template <int C, class Cfg>
 __global__ __launch_bounds__(256) void warp_plan_kernel(const double* __restrict__ Mall, int n_frames, int H, int W,
                                                         int inverse_map, int ntx, int nty,
-                                                        TilePlan* __restrict__ plan, double* __restrict__ minv) {
+                                                        TilePlan* __restrict__ plan, double* __restrict__ minv,
+                                                        int2* __restrict__ rowtab, int hq) {
   const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (t >= (long long)ntx * nty * n_frames) return;
   const int f = (int)(t / (ntx * nty)), t2 = (int)(t - (long long)f * ntx * nty);
-  const int xb = (t2 % ntx) * kTileW, yb = (t2 / ntx) * Cfg::kTileH;
+  const int tx = t2 % ntx, xb = tx * kTileW, yb = (t2 / ntx) * Cfg::kTileH;
   double M[6];
   load_map(Mall, f, inverse_map, M);
   if (t2 == 0)
     for (int k = 0; k < 6; ++k) minv[6 * (size_t)f + k] = M[k];
-  const Box b = source_box<Cfg, C>(M, xb, yb, H, W);
+  Box b = source_box<Cfg, C>(M, xb, yb, H, W);
+  if (C == 1 && (W & 7) == 0 && b.mode == 0 && b.pitch <= kFastPitch && b.rows <= Fast<Cfg>::kRows) b.mode = 3;
   plan[t] = TilePlan{b.mode, b.ax0, b.sy0, b.pitch | (b.rows << 16)};
+  for (int j = tx; j < Cfg::kTileH && yb + j < H; j += ntx) {
+    const int y = yb + j;
+    rowtab[((size_t)f * 4 + (y & 3)) * hq + (y >> 2)] =
+        make_int2(cv_round((M[1] * y + M[2]) * 1024) + 16, cv_round((M[4] * y + M[5]) * 1024) + 16);
+  }
 }
 
 // ------------------------------------------------------------ one tile per workgroup
@@ -423,7 +579,7 @@ __global__ __launch_bounds__(256) void warp_plan_kernel(const double* __restrict
 template <int C, class Cfg = BlockCfg, int VARIANT = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-access-mode"))) void warp_affine_u16_kernel(
     const uint16_t* __restrict__ src, uint16_t* __restrict__ dst, const TilePlan* __restrict__ plan,
-    const double* __restrict__ minv, int H, int W) {
+    const double* __restrict__ minv, const int2* __restrict__ rowtab, int hq, int H, int W) {
   __shared__ __attribute__((aligned(16))) uint16_t stile[Cfg::kLdsElems];
   const int ntx = gridDim.x, nty = gridDim.y;
   const int tile = xcd_remap(blockIdx.x + ntx * (blockIdx.y + nty * blockIdx.z), ntx * nty * gridDim.z);
@@ -435,7 +591,38 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
   const uint16_t* S = src + (size_t)f * H * W * C;
   uint16_t* Dst = dst + (size_t)f * H * W * C;
 
-  const Box box = unpack(plan[tile]);
+  Box box = unpack(plan[tile]);
+  if constexpr (C == 1 && VARIANT == 0) {
+    if (box.mode == 3) {
+      const int cpr = box.pitch >> 3;
+      uint4 fchunk[Fast<Cfg>::kPasses];
+      fast_stage_issue<Cfg>(S, box.ax0, box.sy0, cpr, box.rows, H, W, tid, fchunk);  // loads first
+      int ad[2], bd[2];
+      lane_cols(minv + 6 * (size_t)f, xb, W, lane, ad, bd);
+      fast_stage_land<Cfg>(stile, cpr, box.rows, tid, fchunk);
+      // bright (>= 16384) staged chunks of the box, counted per wave into the flag words
+      uint32_t nb = 0;
+#pragma unroll
+      for (int k = 0; k < Fast<Cfg>::kPasses; ++k)
+        nb += __builtin_popcountll(__builtin_amdgcn_ballot_w64(
+            ((fchunk[k].x | fchunk[k].y | fchunk[k].z | fchunk[k].w) & 0xc000c000u) != 0));
+      uint32_t* flags = reinterpret_cast<uint32_t*>(stile) + Fast<Cfg>::kFlagWord;
+      if (lane == 0) flags[wave] = nb;
+      __syncthreads();
+      const uint4 fl = *reinterpret_cast<const uint4*>(flags);
+      const uint32_t bright = fl.x + fl.y + fl.z + fl.w;
+      const int2* rt = rowtab + ((size_t)f * 4 + wave) * hq + (yb >> 2);
+      const int ox = box.ax0 * 1024, oy = box.sy0 * 1024;
+      if (bright == 0)
+        fast_rows<Cfg, kDark>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+      else if ((int)bright * kBrightShare <= box.rows * (box.pitch >> 3))
+        fast_rows<Cfg, kMixed>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+      else
+        fast_rows<Cfg, kBright>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+      return;
+    }
+  }
+  if (box.mode == 3) box.mode = 0;  // lab ablations: the general staged path
   const bool vec_stage = (C == 1) && ((W & 7) == 0);
   uint4 chunk[Cfg::kRowPasses];
   if (box.mode == 0 && vec_stage && VARIANT != 2) stage_issue<Cfg>(S, box, H, W, tid, chunk);  // loads first
@@ -455,10 +642,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
   output_tile<Cfg, C>(VARIANT == 1 ? 1 : box.mode, stile, box, S, Dst, H, W, xb, yb, wave, lane, ad, bd, X0v, Y0v);
 }
 
+// Row-origin table entries per (frame, y & 3): padded so that a wave's scalar loads of
+// its kTileH / 4 entries stay inside the frame's block.
+inline int rowtab_hq(int H) { return ceil_div(H, 4) + 16; }
+
 template <class Cfg>
 size_t warp_workspace_bytes(int n_frames, int H, int W) {
   const size_t tiles = (size_t)ceil_div(W, kTileW) * ceil_div(H, Cfg::kTileH) * n_frames;
-  return tiles * sizeof(TilePlan) + (size_t)n_frames * 6 * sizeof(double);
+  return tiles * sizeof(TilePlan) + (size_t)n_frames * 6 * sizeof(double) +
+         (size_t)n_frames * 4 * rowtab_hq(H) * sizeof(int2);
 }
 
 // Plan + tile launches on `s`; ws holds warp_workspace_bytes<Cfg>(n_frames, H, W) bytes.
@@ -468,11 +660,13 @@ void launch_warp(const uint16_t* src, uint16_t* dst, const double* M, int n_fram
   const int ntx = ceil_div(W, kTileW), nty = ceil_div(H, Cfg::kTileH);
   const long long tiles = (long long)ntx * nty * n_frames;
   double* minv = static_cast<double*>(ws);
-  TilePlan* plan = reinterpret_cast<TilePlan*>(minv + 6 * (size_t)n_frames);
+  int2* rowtab = reinterpret_cast<int2*>(minv + 6 * (size_t)n_frames);
+  const int hq = rowtab_hq(H);
+  TilePlan* plan = reinterpret_cast<TilePlan*>(rowtab + (size_t)n_frames * 4 * hq);
   hipLaunchKernelGGL((warp_plan_kernel<C, Cfg>), dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, s, M, n_frames,
-                     H, W, inverse_map, ntx, nty, plan, minv);
+                     H, W, inverse_map, ntx, nty, plan, minv, rowtab, hq);
   hipLaunchKernelGGL((warp_affine_u16_kernel<C, Cfg, VARIANT>), dim3(ntx, nty, n_frames), dim3(kThreads), 0, s, src,
-                     dst, plan, minv, H, W);
+                     dst, plan, minv, rowtab, hq, H, W);
 }
 
 // ================================================================ warpPerspective

@@ -225,6 +225,30 @@ def test_warp_matches_oracle(dev, shape):
         assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], Ms[f])), f
 
 
+@pytest.mark.parametrize("values", ["14bit", "hot", "blobs", "edge16384"])
+def test_warp_fast_path_value_ranges(dev, values):
+    # the fixed-pitch staged path picks its blend per tile: exact integer for boxes below
+    # 16384, packed-fp32 OpenCV evaluation otherwise; mix both within one frame
+    F, H, W = 3, 240, 512
+    rng = np.random.default_rng(77)
+    if values == "14bit":
+        imgs = rng.integers(0, 16384, (F, H, W))
+    elif values == "hot":  # isolated bright pixels: the per-row mixed blend
+        imgs = rng.integers(0, 16384, (F, H, W))
+        imgs[rng.random((F, H, W)) < 2e-4] = 65535
+    elif values == "blobs":
+        imgs = rng.integers(0, 8192, (F, H, W))
+        blk = rng.random((F, H // 32 + 1, W // 32 + 1)) < 0.15
+        imgs = np.where(np.repeat(np.repeat(blk, 32, 1), 32, 2)[:, :H, :W], imgs + 36000, imgs)
+    else:  # straddle the 2^24 boundary of the integer blend sum
+        imgs = rng.integers(16370, 16400, (F, H, W))
+    imgs = imgs.astype(np.uint16)
+    Ms = np.stack([synthetic.rigid(rng.normal(0, 0.02), rng.normal(0, 5), rng.normal(0, 5)) for _ in range(F)])
+    out = stages.warp_affine_u16(_t(imgs, dev), _t(Ms, dev)).cpu().numpy()
+    for f in range(F):
+        assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], Ms[f])), f
+
+
 def test_warp_identity_inverse_map_and_extreme_maps(dev):
     rng = np.random.default_rng(31)
     imgs = rng.integers(0, 65536, (4, 33, 45)).astype(np.uint16)
