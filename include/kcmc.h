@@ -242,6 +242,15 @@ int kcmc_orb_detect(kcmc_ctx* ctx, const uint8_t* frames_dev, int n_frames, int 
                     const double* bin_cs_dev, double* out_kp_dev, uint8_t* out_des_dev,
                     int32_t* out_count_dev, kcmc_stream_t stream);
 
+/* ----------------------------------------------------- f4: spatial downsample
+ * cv2.pyrDown(frame, dstsize=(dst_w, dst_h)) of every uint8 frame (replaces the per-frame
+ * host calls of VideoAligner._downsample, VA:501-503): 5x5 binomial (1,4,6,4,1)^2 / 256,
+ * BORDER_REFLECT_101, (sum + 128) >> 8.  src_dev [n_frames, H, W] u8, dst_dev
+ * [n_frames, dst_h, dst_w] u8, both 4-byte aligned.  KCMC_EINVAL (OpenCV's assertion)
+ * unless |2 dst_w - W| <= 2 and |2 dst_h - H| <= 2. */
+int kcmc_pyr_down_u8(kcmc_ctx* ctx, const uint8_t* src_dev, int n_frames, int H, int W, uint8_t* dst_dev,
+                     int dst_h, int dst_w, kcmc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -41,6 +41,7 @@ EXPORTED_SYMBOLS = (
     "kcmc_histogram_u16",
     "kcmc_lut_u16_to_u8",
     "kcmc_orb_detect",
+    "kcmc_pyr_down_u8",
 )
 
 KCMC_MODEL_EUCLIDEAN = 0
@@ -89,6 +90,7 @@ _SIGNATURES = {
     "kcmc_histogram_u16": ([P, P, ctypes.c_ulonglong, I, I, P, P], I),
     "kcmc_lut_u16_to_u8": ([P, P, ctypes.c_ulonglong, P, P, P], I),
     "kcmc_orb_detect": ([P, P, I, I, I, I, I, D, I, P, P, P, P, P, P], I),
+    "kcmc_pyr_down_u8": ([P, P, I, I, I, P, I, I, P], I),
 }
 
 

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import logging
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional
+from typing import Callable, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -329,6 +329,22 @@ def align_streamed(frames_host: torch.Tensor, inp: SlabInputs, cfg: AlignConfig,
     return out_host, SlabResult(None, affines, eu, skipped, interpolated, match=match, consensus=cons, ransac=rr)
 
 
+def downsample_u8(frames_u8: torch.Tensor, template_u8: torch.Tensor, frame_downsample_rate: int,
+                  spatial_downsample_rate) -> Tuple[torch.Tensor, torch.Tensor]:
+    """VideoAligner._downsample (VA:494-506) on the device: every rate-th frame and, only
+    when the rate is not 1, cv2.pyrDown of the sample frames and the template
+    (stages.pyr_down_u8) with the reference's dstsize = tuple(shape // spatial rate), which
+    OpenCV reads as (width, height) -- so non-square frames fail its size assertion just
+    as the reference does."""
+    rate = int(frame_downsample_rate)
+    if rate == 1:
+        return frames_u8, template_u8
+    H, W = frames_u8.shape[-2:]
+    dsize = (int(H // spatial_downsample_rate), int(W // spatial_downsample_rate))
+    return (stages.pyr_down_u8(frames_u8[::rate].contiguous(), dsize),
+            stages.pyr_down_u8(template_u8.reshape(1, H, W).contiguous(), dsize))
+
+
 def detect_slab(frames: torch.Tensor, cfg: AlignConfig, template_index: Optional[int] = None,
                 template: Optional[torch.Tensor] = None, orb_params=None, percentile: float = 99.99):
     """The front end of align_images (VA:93-123) on the device for a uint16 stack:
@@ -337,8 +353,6 @@ def detect_slab(frames: torch.Tensor, cfg: AlignConfig, template_index: Optional
     (SlabInputs for align_slab, brightest)."""
     if frames.dim() != 3:
         raise ValueError("detection needs a grayscale stack [F, H, W]")
-    if cfg.frame_downsample_rate != 1 or cfg.spatial_rate != 1:
-        raise ValueError("device detection needs frame_downsample_rate == 1 and spatial_rate == 1 (pyrDown not built)")
     F = frames.shape[0]
     brightest = stages.brightest_px(frames, percentile)
     u8 = stages.max_scale_u8(frames, brightest)
@@ -347,6 +361,7 @@ def detect_slab(frames: torch.Tensor, cfg: AlignConfig, template_index: Optional
         tpl_u8 = u8[ti:ti + 1]
     else:
         tpl_u8 = stages.max_scale_u8(template.reshape(1, *template.shape[-2:]).contiguous(), brightest)
+    u8, tpl_u8 = downsample_u8(u8, tpl_u8, cfg.frame_downsample_rate, cfg.spatial_rate)
     kt = stages.detect_orb(tpl_u8, orb_params)
     kq = stages.detect_orb(u8, orb_params)
     n_t = int(kt.count.cpu()[0])

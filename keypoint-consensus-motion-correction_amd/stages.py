@@ -436,6 +436,34 @@ def max_scale_u8(frames: torch.Tensor, brightest: float, out: Optional[torch.Ten
     return out
 
 
+# ------------------------------------------------------------ f4: pyrDown
+def pyr_down_u8(frames_u8: torch.Tensor, dstsize=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """cv2.pyrDown(frame, dstsize=dstsize) of every frame of a uint8 stack [F, H, W]
+    (VA:501-503) on the device.  dstsize is (width, height) like OpenCV; None or an
+    empty size gives ((W + 1) // 2, (H + 1) // 2).  ValueError where OpenCV's size
+    assertion (|2 w - W| <= 2, |2 h - H| <= 2) fails."""
+    dev = _device_of(frames_u8)
+    _require(frames_u8, "frames_u8", torch.uint8, dev)
+    if frames_u8.dim() != 3:
+        raise ValueError("frames_u8 must be [F, H, W]")
+    F, H, W = frames_u8.shape
+    if H == 0 or W == 0:
+        raise ValueError("pyrDown: ssize.width > 0 && ssize.height > 0")
+    dw, dh = ((W + 1) // 2, (H + 1) // 2) if dstsize is None or min(dstsize) <= 0 else (int(dstsize[0]), int(dstsize[1]))
+    if abs(2 * dw - W) > 2 or abs(2 * dh - H) > 2:
+        raise ValueError("pyrDown: std::abs(dsize.width*2 - ssize.width) <= 2 && "
+                         "std::abs(dsize.height*2 - ssize.height) <= 2")
+    if out is None:
+        out = torch.empty((F, dh, dw), dtype=torch.uint8, device=dev)
+    else:
+        _require(out, "out", torch.uint8, dev)
+        if tuple(out.shape) != (F, dh, dw):
+            raise ValueError("out must be [F, dst_h, dst_w]")
+    _lib.check(_lib.load().kcmc_pyr_down_u8(_ctx(dev).handle, _ptr(frames_u8), F, H, W, _ptr(out), dh, dw,
+                                            _stream(dev)))
+    return out
+
+
 # ------------------------------------------------------------ f1: detection
 @dataclass
 class Keypoints:

@@ -185,8 +185,7 @@ class VideoAligner:
         _, template_i8 = self._max_scale_images(None, template, brightest_px, np.uint8)
         frame_downsample_rate = max(1, frame_rate // self.FRAME_SAMPLE_RATE)
         detector = self.DETECTOR_CONSTRUCTOR_DICT[detector_algorithm]()
-        on_gpu = (isinstance(detector, GpuOrbDetector) and frame_downsample_rate == 1
-                  and self.SPATIAL_DOWNSAMPLE_RATE == 1 and frames.dim() == 3)
+        on_gpu = isinstance(detector, GpuOrbDetector) and frames.dim() == 3
         if not on_gpu:
             images_i8 = u8_dev.cpu().numpy()
             images_sample, template = self._downsample(images_i8, template_i8, frame_downsample_rate,
@@ -195,9 +194,11 @@ class VideoAligner:
 
         self.logger.info("identifying keypoints...")
         t_start = time.time()
-        if on_gpu:  # f1: detection of the whole stack on the device
-            kt = stages.detect_orb(torch.from_numpy(np.ascontiguousarray(template_i8)).to(dev)[None], detector.params)
-            kq = stages.detect_orb(u8_dev, detector.params)
+        if on_gpu:  # f1: detection of the whole stack on the device (f4: downsample there too)
+            sample_dev, tpl_dev = _pl.downsample_u8(u8_dev, torch.from_numpy(np.ascontiguousarray(template_i8)).to(dev)[None],
+                                                    frame_downsample_rate, self.SPATIAL_DOWNSAMPLE_RATE)
+            kt = stages.detect_orb(tpl_dev, detector.params)
+            kq = stages.detect_orb(sample_dev, detector.params)
             n_t = int(kt.count.cpu()[0])
             self._kp_template = kt.kp[0, :n_t].cpu().numpy()
             self._des_template = kt.des[0, :n_t].cpu().numpy()
@@ -428,19 +429,16 @@ class VideoAligner:
     @staticmethod
     def _downsample(images: np.ndarray, template: np.ndarray, frame_downsample_rate: int,
                     spatial_downsample_rate: Union[float, int]) -> Tuple[np.ndarray, np.ndarray]:
-        """VA:494-506 (OpenCV pyrDown when frame_downsample_rate != 1)."""
-        images_sample = images[::frame_downsample_rate]
-        dst_size = tuple(np.array(images_sample[0].shape) // spatial_downsample_rate)
-        if frame_downsample_rate != 1:
-            try:
-                import cv2  # type: ignore
-            except ImportError as e:
-                raise RuntimeError("frame_rate >= 2*FRAME_SAMPLE_RATE needs cv2.pyrDown (OpenCV absent)") from e
-            images_sample = [cv2.pyrDown(frame, dstsize=dst_size) for frame in images_sample]
-            template = cv2.pyrDown(template, dstsize=dst_size)
-            images_sample = np.stack(images_sample).astype(np.uint8)
-            template = template.astype(np.uint8)
-        return images_sample, template
+        """VA:494-506: every rate-th frame and, when the rate is not 1, cv2.pyrDown of the
+        sample frames and the template -- here the device kernel (stages.pyr_down_u8, via
+        pipeline.downsample_u8) with the reference's dstsize quirk kept."""
+        if int(frame_downsample_rate) == 1:
+            return images[::1], template
+        dev = VideoAligner._device()
+        f = torch.from_numpy(np.ascontiguousarray(images, np.uint8)).to(dev)
+        t = torch.from_numpy(np.ascontiguousarray(template, np.uint8)).to(dev)[None]
+        s, t = _pl.downsample_u8(f, t, frame_downsample_rate, spatial_downsample_rate)
+        return s.cpu().numpy(), t[0].cpu().numpy()
 
 
 class LoResVideoAligner(VideoAligner):

@@ -842,3 +842,33 @@ int kcmc_oracle_orb_detect(const uint8_t* img, int H, int W, int threshold, int 
   free(pos);
   return n_out;
 }
+
+/* ----------------------------------------------------------------- f4: pyrDown
+ * cv2.pyrDown(src, dstsize) for one uint8 frame (VA:501-503; OpenCV 4.x
+ * imgproc/src/pyramids.cpp pyrDown_ with FixPtCast<uchar, 8>, BORDER_REFLECT_101):
+ * the ring buffer holds the horizontal 1-4-6-4-1 sums of the reflected source rows
+ * 2y-2 .. 2y+2 (tabL / tabR reflect the border columns), the vertical pass applies the
+ * same weights and rounds with (sum + 128) >> 8.  Returns -1 when OpenCV's assertion
+ * |2 dw - W| <= 2 && |2 dh - H| <= 2 fails. */
+static int reflect101(int p, int len) {
+  if (len == 1) return 0;
+  while ((unsigned)p >= (unsigned)len) p = p < 0 ? -p : 2 * len - 2 - p;
+  return p;
+}
+
+int kcmc_oracle_pyr_down_u8(const uint8_t* src, int H, int W, uint8_t* dst, int DH, int DW) {
+  static const int k[5] = {1, 4, 6, 4, 1};
+  if (H <= 0 || W <= 0 || abs(DW * 2 - W) > 2 || abs(DH * 2 - H) > 2) return -1;
+  for (int y = 0; y < DH; ++y)
+    for (int x = 0; x < DW; ++x) {
+      int acc = 0;
+      for (int i = 0; i < 5; ++i) {
+        const uint8_t* row = src + (size_t)reflect101(2 * y + i - 2, H) * W;
+        int h = 0;
+        for (int j = 0; j < 5; ++j) h += k[j] * row[reflect101(2 * x + j - 2, W)];
+        acc += k[i] * h;
+      }
+      dst[(size_t)y * DW + x] = (uint8_t)((acc + 128) >> 8);
+    }
+  return 0;
+}

@@ -68,6 +68,7 @@ def lib() -> ctypes.CDLL:
         L.kcmc_oracle_ransac_model.argtypes = [i, P, P, i, P, i, ctypes.c_double, P, P, P, P]
         L.kcmc_oracle_warp_perspective_u16.argtypes = [P, i, i, i, P, i, P, i, i]
         L.kcmc_oracle_invert_perspective.argtypes = [P, P]
+        L.kcmc_oracle_pyr_down_u8.argtypes = [P, i, i, P, i, i]
         L.kcmc_oracle_invert_perspective.restype = i
         _LIB = L
     return _LIB
@@ -382,6 +383,22 @@ def invert_affine(M: np.ndarray) -> np.ndarray:
     out = np.empty(6, np.float64)
     lib().kcmc_oracle_invert_affine(_p(M), _p(out))
     return out.reshape(2, 3)
+
+
+def pyr_down_u8(img: np.ndarray, dstsize=None) -> np.ndarray:
+    """``cv2.pyrDown(img, dstsize=dstsize)`` on a uint8 [H, W] frame (VA:501-503).
+
+    ``dstsize`` is (width, height) like OpenCV; empty/None -> ((W+1)//2, (H+1)//2).
+    Raises ValueError where OpenCV's size assertion fails.
+    """
+    src = np.ascontiguousarray(img, np.uint8)
+    H, W = src.shape
+    dW, dH = ((W + 1) // 2, (H + 1) // 2) if dstsize is None or min(dstsize) <= 0 else dstsize
+    out = np.empty((dH, dW), np.uint8)
+    if lib().kcmc_oracle_pyr_down_u8(_p(src), H, W, _p(out), int(dH), int(dW)) != 0:
+        raise ValueError("pyrDown: std::abs(dsize.width*2 - ssize.width) <= 2 && "
+                         "std::abs(dsize.height*2 - ssize.height) <= 2")
+    return out
 
 
 def warp_affine_u16(img: np.ndarray, M: np.ndarray, dsize=None, inverse_map: bool = False) -> np.ndarray:
