@@ -22,42 +22,54 @@ namespace {
 constexpr int kThreads = 256;
 
 // bins[(v >> shift) & 255] over the values with (v >> 8) == match (match < 0: all).
-// Video values crowd into a few coarse bins, so same-address LDS atomics would
-// serialise: each wave keeps 8 sub-histograms (lane & 7), 32 per workgroup (32 KB).
-constexpr int kReplicas = 8;
+// Video values crowd into a few coarse bins, so the LDS atomics must not collide: one
+// sub-histogram per lane index (64 per workgroup, shared by the 4 waves, which issue their
+// atomics at different times), rows padded to 257 words so that bin b of lane l sits in
+// bank (l + b) % 64 -- the 64 atomics of one wave instruction hit 64 distinct banks
+// whatever the values.  65.8 KB of LDS: two workgroups per CU.  The fine pass (match >= 0)
+// counts only the values of one coarse bin -- few, for the 99.99th percentile -- and
+// keeps 8 sub-histograms (8 KB) for occupancy instead.
+constexpr int kRow = 257;
 
+template <int R>
 __global__ __launch_bounds__(kThreads) void hist256_u16_kernel(const uint16_t* __restrict__ src, size_t n, int shift,
                                                                int match, unsigned long long* __restrict__ out) {
-  __shared__ uint32_t h[kThreads / 64 * kReplicas][256];
-  const int tid = threadIdx.x, wave = tid >> 6;
-  for (int i = tid; i < kThreads / 64 * kReplicas * 256; i += kThreads) (&h[0][0])[i] = 0u;
+  __shared__ uint32_t h[R * kRow];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < R * kRow; i += kThreads) h[i] = 0u;
   __syncthreads();
-  uint32_t* hw = h[wave * kReplicas + (tid & (kReplicas - 1))];
+  uint32_t* hl = h + (tid & (R - 1)) * kRow;
   const size_t n8 = n / 8;
   const uint4* s8 = reinterpret_cast<const uint4*>(src);
   const size_t stride = (size_t)gridDim.x * kThreads;
-  for (size_t i = blockIdx.x * (size_t)kThreads + tid; i < n8; i += stride) {
-    const uint4 q = s8[i];
+  auto count8 = [&](const uint4& q) {
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const uint32_t v = (w[k] >> (16 * p)) & 0xffffu;
-        if (match < 0 || (int)(v >> 8) == match) atomicAdd(&hw[(v >> shift) & 255u], 1u);
+        if (match < 0 || (int)(v >> 8) == match) atomicAdd(&hl[(v >> shift) & 255u], 1u);
       }
     }
+  };
+  size_t i = blockIdx.x * (size_t)kThreads + tid;
+  for (; i + stride < n8; i += 2 * stride) {  // two 16-byte loads in flight per thread
+    const uint4 a = s8[i], b = s8[i + stride];
+    count8(a);
+    count8(b);
   }
+  if (i < n8) count8(s8[i]);
   if (blockIdx.x == 0) {  // tail (n % 8 values)
-    for (size_t i = n8 * 8 + tid; i < n; i += kThreads) {
-      const uint32_t v = src[i];
-      if (match < 0 || (int)(v >> 8) == match) atomicAdd(&hw[(v >> shift) & 255u], 1u);
+    for (size_t t = n8 * 8 + tid; t < n; t += kThreads) {
+      const uint32_t v = src[t];
+      if (match < 0 || (int)(v >> 8) == match) atomicAdd(&hl[(v >> shift) & 255u], 1u);
     }
   }
   __syncthreads();
   for (int b = tid; b < 256; b += kThreads) {
     unsigned long long c = 0;
-    for (int r = 0; r < kThreads / 64 * kReplicas; ++r) c += h[r][b];
+    for (int r = 0; r < R; ++r) c += h[r * kRow + b];
     if (c) atomicAdd(&out[b], c);
   }
 }
@@ -90,9 +102,9 @@ __global__ __launch_bounds__(kThreads) void lut_u16_to_u8_kernel(const uint16_t*
     for (size_t i = n16 * 16 + tid; i < n; i += kThreads) dst[i] = t[src[i]];
 }
 
-int grid_for(size_t work_items) {
+int grid_for(size_t work_items, size_t cap = 4096) {
   size_t g = (work_items + kThreads - 1) / kThreads;
-  if (g > 4096) g = 4096;  // grid-stride beyond 16 workgroups per CU
+  if (g > cap) g = cap;  // grid-stride beyond that
   return g < 1 ? 1 : (int)g;
 }
 
@@ -111,8 +123,12 @@ extern "C" int kcmc_histogram_u16(kcmc_ctx* ctx, const uint16_t* src, unsigned l
   hipStream_t s = (hipStream_t)stream;
   KCMC_TRY(hip_check(hipMemsetAsync(out_hist, 0, 256 * sizeof(unsigned long long), s), "hipMemsetAsync"));
   if (n == 0) return KCMC_OK;
-  hipLaunchKernelGGL(hist256_u16_kernel, dim3(grid_for(n / 8 + 1)), dim3(kThreads), 0, s, src, (size_t)n, shift, match,
-                     out_hist);
+  if (match < 0)  // 2 resident workgroups per CU (LDS): a few waves of them
+    hipLaunchKernelGGL(hist256_u16_kernel<64>, dim3(grid_for(n / 8 + 1, 2048)), dim3(kThreads), 0, s, src, (size_t)n,
+                       shift, match, out_hist);
+  else
+    hipLaunchKernelGGL(hist256_u16_kernel<8>, dim3(grid_for(n / 8 + 1, 4096)), dim3(kThreads), 0, s, src, (size_t)n,
+                       shift, match, out_hist);
   return launch_check("hist256_u16_kernel");
 }
 

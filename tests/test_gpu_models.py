@@ -309,6 +309,17 @@ def test_brightest_px_matches_numpy(dev, shape, hi):
     assert np.array_equal(stages.max_scale_u8(t, b).cpu().numpy(), ref)
 
 
+def test_brightest_px_concentrated_values(dev):
+    # the bench texture: most values in a few coarse bins (the histogram's worst case for
+    # atomic collisions), plus a stack where every value is identical
+    imgs = np.stack([synthetic.make_texture((360, 480), seed=s) for s in range(4)])
+    t = _t(imgs, dev)
+    for q in (99.99, 50.0, 1.0):
+        assert stages.brightest_px(t, q) == np.percentile(imgs, q), q
+    same = np.full((3, 64, 64), 2047, np.uint16)
+    assert stages.brightest_px(_t(same, dev), 99.99) == 2047.0
+
+
 # ------------------------------------------------------------ f1: detection
 def _texture_u8(rng, H, W, cell=4, noise=12):
     lo = rng.integers(0, 256, (H // cell + 2, W // cell + 2)).astype(np.float64)
