@@ -18,8 +18,9 @@
 //     angle (host table), compared on a 5x5 binomial smoothing -> 32-byte descriptors.
 //
 // orb_candidates_kernel  one workgroup per 64x16 tile: image + 4-px halo in LDS, FAST
-//                        scores for the tile + 1-px halo, NMS, Harris, ordered
-//                        compaction of the tile's candidates (block scan).
+//                        scores for the tile + 1-px halo, NMS, Harris -- each step on
+//                        the compacted survivors of the previous one (block scans), so
+//                        the candidates keep raster order inside the tile.
 // orb_offsets_kernel +   per frame: tile prefix offsets, then one wave per tile copies
 // orb_gather_kernel      its candidates into the frame's compact list (candidate order).
 // orb_select_kernel      one workgroup per frame: radix select of the n_features-th
@@ -72,13 +73,51 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_warp, int& excl) {
   return total;
 }
 
+// FAST-9 score of one pixel (max over the 16 contiguous 9-pixel arcs of the smaller
+// threshold margin, positive or negative side): running minima over 2, 4, 8 then 9
+// neighbours on the circle, both sides at once.
+__device__ __forceinline__ int fast_score9(const uint8_t (*img)[kPW], int py, int px) {
+  const int v = img[py][px];
+  int d[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) d[j] = (int)img[py + c_circle[j][1]][px + c_circle[j][0]] - v;
+  int lo2[16], hi2[16], lo4[16], hi4[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    lo2[j] = min(d[j], d[(j + 1) & 15]);
+    hi2[j] = max(d[j], d[(j + 1) & 15]);
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    lo4[j] = min(lo2[j], lo2[(j + 2) & 15]);
+    hi4[j] = max(hi2[j], hi2[(j + 2) & 15]);
+  }
+  int best = -1000;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int mb = min(min(lo4[k], lo4[(k + 4) & 15]), d[(k + 8) & 15]);   // min of d over the arc
+    const int Md = max(max(hi4[k], hi4[(k + 4) & 15]), d[(k + 8) & 15]);  // max of d over the arc
+    best = max(best, max(mb, -Md));
+  }
+  return best;
+}
+
+// One workgroup per 64x16 tile.  Candidates are sparse, so every expensive step runs on
+// a compacted list instead of on all pixels (a wave would otherwise pay for its single
+// candidate with 63 idle lanes): (1) stage the image + 4-px halo; (2) the compass
+// pre-test on the tile + 1-px halo, survivors listed; (3) FAST scores of the listed
+// pixels; (4) 3x3 NMS of the tile pixels, survivors listed in raster order; (5) integer
+// Harris of the listed candidates, 8 lanes per candidate (one 7-pixel window row each,
+// shuffle reduction); (6) the keys and positions stored in list (= raster) order.
 __global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t* __restrict__ frames, int H, int W,
                                                                   int threshold, double harris_k, int edge,
                                                                   uint64_t* __restrict__ cand_key,
                                                                   uint32_t* __restrict__ cand_pos,
                                                                   int32_t* __restrict__ cand_cnt) {
-  __shared__ uint8_t img[kPH][kPW];
+  __shared__ __attribute__((aligned(16))) uint8_t img[kPH][kPW];
   __shared__ int16_t sc[kSH][kSW];
+  __shared__ uint16_t plist[kSH * kSW];  // pre-test survivors (score-region index)
+  __shared__ uint16_t nlist[kTW * kTH];  // NMS survivors (tile pixel index, raster order)
   __shared__ int s_warp[kThreads / 64];
   const int ntx = gridDim.x, nty = gridDim.y;
   const int f = blockIdx.z;
@@ -87,58 +126,67 @@ __global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t*
   const int tid = threadIdx.x;
   const uint8_t* I = frames + (size_t)f * H * W;
 
-  for (int i = tid; i < kPH * kPW; i += kThreads) {
-    const int r = i / kPW, c = i - r * kPW;
-    const int y = y0 - kHalo + r, x = x0 - kHalo + c;
-    img[r][c] = ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) ? I[(size_t)y * W + x] : (uint8_t)0;
-  }
-  __syncthreads();
-  for (int i = tid; i < kSH * kSW; i += kThreads) {
-    const int r = i / kSW, c = i - r * kSW;
-    const int y = y0 - 1 + r, x = x0 - 1 + c;
-    int s = 0;
-    if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3) {
-      const int py = r - 1 + kHalo, px = c - 1 + kHalo;  // position in img
-      const int v = img[py][px];
-      // a 9-pixel arc covers at least two of the four compass pixels (0, 4, 8, 12):
-      // fewer than two beyond the threshold on the same side -> not a corner (score 0)
-      const int n0 = img[py + 3][px], n4 = img[py][px + 3], n8 = img[py - 3][px], n12 = img[py][px - 3];
-      const int hi = (n0 > v + threshold) + (n4 > v + threshold) + (n8 > v + threshold) + (n12 > v + threshold);
-      const int lo = (n0 < v - threshold) + (n4 < v - threshold) + (n8 < v - threshold) + (n12 < v - threshold);
-      if (hi < 2 && lo < 2) {
-        sc[r][c] = 0;
-        continue;
-      }
-      int d[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) d[j] = (int)img[py + c_circle[j][1]][px + c_circle[j][0]] - v;
-      int best = -1000;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        int mb = 1000, md = 1000;
-#pragma unroll
-        for (int m = 0; m < 9; ++m) {
-          const int e = d[(k + m) & 15];
-          mb = min(mb, e);
-          md = min(md, -e);
-        }
-        best = max(best, max(mb, md));
-      }
-      s = best > threshold ? best : 0;
+  // (1) staging: 4-byte words where the row is aligned (x0 - 4 is a multiple of 4)
+  if ((W & 3) == 0) {
+    for (int i = tid; i < kPH * (kPW / 4); i += kThreads) {
+      const int r = i / (kPW / 4), c = 4 * (i - r * (kPW / 4));
+      const int y = y0 - kHalo + r, x = x0 - kHalo + c;
+      uint32_t v = 0;
+      if ((unsigned)y < (unsigned)H && x >= 0 && x + 4 <= W) v = *reinterpret_cast<const uint32_t*>(I + (size_t)y * W + x);
+      *reinterpret_cast<uint32_t*>(&img[r][c]) = v;
     }
-    sc[r][c] = (int16_t)s;
+  } else {
+    for (int i = tid; i < kPH * kPW; i += kThreads) {
+      const int r = i / kPW, c = i - r * kPW;
+      const int y = y0 - kHalo + r, x = x0 - kHalo + c;
+      img[r][c] = ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) ? I[(size_t)y * W + x] : (uint8_t)0;
+    }
   }
   __syncthreads();
 
-  // thread t owns tile pixels 4t .. 4t+3 (raster order inside the tile)
-  uint64_t keys[4];
-  int flags = 0, cnt = 0;
+  // (2) compass pre-test: a 9-pixel arc covers at least two of the four compass pixels
+  // (0, 4, 8, 12), so fewer than two beyond the threshold on the same side -> score 0
+  constexpr int kItems = (kSH * kSW + kThreads - 1) / kThreads;
+  uint32_t pass = 0;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    const int i = tid + kThreads * k;
+    if (i >= kSH * kSW) break;
+    const int r = i / kSW, c = i - r * kSW;
+    const int y = y0 - 1 + r, x = x0 - 1 + c;
+    sc[r][c] = 0;
+    if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3) {
+      const int py = r - 1 + kHalo, px = c - 1 + kHalo;
+      const int v = img[py][px];
+      const int n0 = img[py + 3][px], n4 = img[py][px + 3], n8 = img[py - 3][px], n12 = img[py][px - 3];
+      const int hi = (n0 > v + threshold) + (n4 > v + threshold) + (n8 > v + threshold) + (n12 > v + threshold);
+      const int lo = (n0 < v - threshold) + (n4 < v - threshold) + (n8 < v - threshold) + (n12 < v - threshold);
+      if (hi >= 2 || lo >= 2) pass |= 1u << k;
+    }
+  }
+  int excl;
+  const int npass = block_excl_scan(__builtin_popcount(pass), s_warp, excl);
+#pragma unroll
+  for (int k = 0; k < kItems; ++k)
+    if (pass >> k & 1) plist[excl++] = (uint16_t)(tid + kThreads * k);
+  __syncthreads();
+
+  // (3) FAST scores of the listed pixels
+  for (int j = tid; j < npass; j += kThreads) {
+    const int i = plist[j];
+    const int r = i / kSW, c = i - r * kSW;
+    const int s = fast_score9(img, r - 1 + kHalo, c - 1 + kHalo);
+    sc[r][c] = (int16_t)(s > threshold ? s : 0);
+  }
+  __syncthreads();
+
+  // (4) NMS; thread t owns tile pixels 4t .. 4t+3 (raster order inside the tile)
+  int flags = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int p = 4 * tid + q;
     const int r = p / kTW, c = p - r * kTW;
     const int y = y0 + r, x = x0 + c;
-    keys[q] = 0;
     if (y < edge || y >= H - edge || x < edge || x >= W - edge) continue;
     const int s = sc[r + 1][c + 1];
     if (s == 0) continue;
@@ -152,36 +200,53 @@ __global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t*
         const bool later = dy > 0 || (dy == 0 && dx > 0);
         keep = keep && (s > o || (s == o && later));
       }
-    if (!keep) continue;
-    long long a = 0, b = 0, cc = 0;
-    for (int dy = -3; dy <= 3; ++dy)
-#pragma unroll
-      for (int dx = -3; dx <= 3; ++dx) {
-        const int py = r + kHalo + dy, px = c + kHalo + dx;
-        const int ix = ((int)img[py - 1][px + 1] + 2 * (int)img[py][px + 1] + (int)img[py + 1][px + 1]) -
-                       ((int)img[py - 1][px - 1] + 2 * (int)img[py][px - 1] + (int)img[py + 1][px - 1]);
-        const int iy = ((int)img[py + 1][px - 1] + 2 * (int)img[py + 1][px] + (int)img[py + 1][px + 1]) -
-                       ((int)img[py - 1][px - 1] + 2 * (int)img[py - 1][px] + (int)img[py - 1][px + 1]);
-        a += (long long)ix * ix;
-        b += (long long)iy * iy;
-        cc += (long long)ix * iy;
-      }
-    const double sab = (double)(a + b);
-    keys[q] = order_key((double)(a * b - cc * cc) - harris_k * (sab * sab));
-    flags |= 1 << q;
-    ++cnt;
+    if (keep) flags |= 1 << q;
   }
-  int excl;
-  const int total = block_excl_scan(cnt, s_warp, excl);
-  const size_t base = ((size_t)f * nty * ntx + tile) * kSlots;
+  const int total = block_excl_scan(__builtin_popcount(flags), s_warp, excl);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    if (!(flags >> q & 1)) continue;
-    const int p = 4 * tid + q;
-    const int r = p / kTW, c = p - r * kTW;
-    cand_key[base + excl] = keys[q];
-    cand_pos[base + excl] = ((uint32_t)(y0 + r) << 16) | (uint32_t)(x0 + c);
-    ++excl;
+  for (int q = 0; q < 4; ++q)
+    if (flags >> q & 1) nlist[excl++] = (uint16_t)(4 * tid + q);
+  __syncthreads();
+
+  // (5) Harris over the 7x7 window of Sobel gradients, 8 lanes per candidate (lane row
+  // 0..6 sums its window row, lane 7 idles), then (6) the stores in list order
+  const size_t base = ((size_t)f * nty * ntx + tile) * kSlots;
+  const int grp = tid >> 3, row = tid & 7;
+  for (int j0 = 0; j0 < total; j0 += kThreads / 8) {
+    const int j = j0 + grp;
+    int a = 0, b = 0, cc = 0;
+    int p = 0;
+    if (j < total) {
+      p = nlist[j];
+      if (row < 7) {
+        const int r = p / kTW, c = p - r * kTW;
+        const int py = r + kHalo + row - 3;
+#pragma unroll
+        for (int dx = -3; dx <= 3; ++dx) {
+          const int px = c + kHalo + dx;
+          const int ix = ((int)img[py - 1][px + 1] + 2 * (int)img[py][px + 1] + (int)img[py + 1][px + 1]) -
+                         ((int)img[py - 1][px - 1] + 2 * (int)img[py][px - 1] + (int)img[py + 1][px - 1]);
+          const int iy = ((int)img[py + 1][px - 1] + 2 * (int)img[py + 1][px] + (int)img[py + 1][px + 1]) -
+                         ((int)img[py - 1][px - 1] + 2 * (int)img[py - 1][px] + (int)img[py - 1][px + 1]);
+          a += ix * ix;  // |ix|, |iy| <= 1020: 49 terms stay below 2^31
+          b += iy * iy;
+          cc += ix * iy;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      a += __shfl_xor(a, o);
+      b += __shfl_xor(b, o);
+      cc += __shfl_xor(cc, o);
+    }
+    if (j < total && row == 0) {
+      const long long A = a, B = b, C = cc;
+      const double sab = (double)(A + B);
+      const int r = p / kTW, c = p - r * kTW;
+      cand_key[base + j] = order_key((double)(A * B - C * C) - harris_k * (sab * sab));
+      cand_pos[base + j] = ((uint32_t)(y0 + r) << 16) | (uint32_t)(x0 + c);
+    }
   }
   if (tid == 0) cand_cnt[(size_t)f * nty * ntx + tile] = total;
 }
