@@ -14,7 +14,11 @@ int launch_check(const char* w) { return hip_check(hipGetLastError(), w); }
 int workspace_alloc(kcmc_ctx*, void**, size_t, hipStream_t) { return KCMC_EUNSUPPORTED; }
 int workspace_free(kcmc_ctx*, void*, hipStream_t) { return KCMC_EUNSUPPORTED; }
 }  // namespace kcmc
-#include "../keypoint-consensus-motion-correction_amd/csrc/warp.hip"
+// -DWARP_SRC='"path"' builds the lab against another version of warp.hip (A/B on one box)
+#ifndef WARP_SRC
+#define WARP_SRC "../keypoint-consensus-motion-correction_amd/csrc/warp.hip"
+#endif
+#include WARP_SRC
 
 __global__ void copy_kernel(const uint4* __restrict__ a, uint4* __restrict__ b, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) b[i] = a[i];
