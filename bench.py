@@ -172,61 +172,73 @@ def run_step(inp, cfg, out, timer=None, world=1, counts=None):
     return cons, rr
 
 
-def cpu_baseline(bc: BenchConfig, ks, n_sample: int):
-    """The oracle restatement of the reference CPU path on a bounded sample (1 thread):
-    C knnMatch + the reference's numpy filters, CPython consensus, the numpy/LAPACK
-    restatement of skimage 0.18.3 ransac (per-trial SVD, like the reference), C warp."""
+def _cpu_pool(procs: int, initargs):
+    """`procs` spawned worker processes (oracle/cpu_baseline_workers.py).  The children
+    must not re-run this script's imports (torch, the HIP library), so the main module's
+    __file__ is hidden from multiprocessing while they start."""
+    import multiprocessing as mp
+
+    import cpu_baseline_workers as W  # noqa: F401  (oracle/, on sys.path)
+
+    main = sys.modules["__main__"]
+    saved = main.__dict__.pop("__file__", None)
+    try:
+        pool = mp.get_context("spawn").Pool(procs, initializer=W.init, initargs=initargs)
+        pool.map(W.ping, range(procs))
+    finally:
+        if saved is not None:
+            main.__file__ = saved
+    return pool
+
+
+def cpu_baseline(bc: BenchConfig, ks, n_sample: int, procs: int):
+    """The oracle restatement of the reference CPU path on a bounded sample, structured
+    like the reference: the per-frame stages (C knnMatch + the reference's numpy filters;
+    the numpy/LAPACK restatement of skimage 0.18.3 ransac with per-trial SVD; C warp) in
+    `procs` single-threaded worker processes over frame chunks (the reference's joblib
+    pool, VA:460-465), CPython consensus in the parent."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # cpu_baseline leg: the oracle is what is timed here
+    import cpu_baseline_workers as W
     from threadpoolctl import threadpool_limits
 
     base = make_texture(bc)
-    skip = {"euclidean": 3, "affine": 4, "projective": 5}[bc.model]
+    initargs = (ks.des_tpl, ks.kp_tpl, ks.des_q, ks.kp_q, ks.q_off, base, bc.model, bc.descriptor)
+    procs = max(1, min(procs, n_sample))
+    chunks = [c.tolist() for c in np.array_split(np.arange(n_sample), procs)]
     with threadpool_limits(1):
+        if procs == 1:
+            W.init(*initargs)
+            run = lambda fn, args: [fn(a) for a in args]  # noqa: E731
+            pool = None
+        else:
+            pool = _cpu_pool(procs, initargs)
+            run = pool.map
         t0 = time.perf_counter()
-        sets, kqs = [], []
-        for f in range(n_sample):
-            a, b = ks.q_off[f], ks.q_off[f + 1]
-            knn = oracle.knn2_l2f32 if bc.descriptor == "f32" else oracle.knn2_l2u8
-            idx, dist = knn(ks.des_tpl, ks.des_q[a:b])
-            s, kq, _ = oracle.filter_matches(idx, dist, ks.kp_tpl, ks.kp_q[a:b])
-            sets.append(s)
-            kqs.append(kq)
+        res = run(W.match_chunk, chunks)
+        sets = [s for r in res for s, _ in r]
+        kqs = [kq for r in res for _, kq in r]
         t1 = time.perf_counter()
         cons, _, _ = oracle.consensus(sets, bc.n_kp_global)
         lists = oracle.lookup(cons, sets)
         t2 = time.perf_counter()
-        affs = []
-        for f in range(n_sample):
-            L = lists[f]
-            if len(L) < skip:
-                affs.append(np.full((2, 3) if bc.model != "projective" else (3, 3), np.nan))
-                continue
-            if bc.model == "euclidean":
-                p, _ = oracle.ransac_rigid_skimage(kqs[f][L], ks.kp_tpl[L])
-            else:
-                p, _ = oracle.ransac_model_skimage(kqs[f][L], ks.kp_tpl[L], bc.model)
-                p = p[:2] if bc.model == "affine" else p
-            affs.append(p)
+        run(W.ransac_warp_chunk, [[(kqs[f], lists[f]) for f in c] for c in chunks])
         t3 = time.perf_counter()
-        for f in range(n_sample):
-            if bc.model == "projective":
-                oracle.warp_perspective_u16(base, affs[f])
-            else:
-                oracle.warp_affine_u16(base, affs[f])
-        t4 = time.perf_counter()
-    total = t4 - t0
+        if pool is not None:
+            pool.close()
+            pool.join()
+    total = t3 - t0
     return {
         "value": n_sample / total,
         "unit": "aligned frames/s",
-        "cores": 1,
+        "cores": procs,
         "kind": "port",
         "sample": (f"{n_sample} frames of {bc.name} ({bc.H}x{bc.W}x{bc.C} u16, n_tpl={bc.n_tpl}, D={bc.D}, "
-                   f"n_kp_global={bc.n_kp_global}, {bc.model}), 1 thread: "
-                   f"match {1e3 * (t1 - t0) / n_sample:.1f} ms/frame (C oracle knnMatch + reference numpy filters), "
-                   f"consensus {1e3 * (t2 - t1):.1f} ms (CPython set/Counter), "
-                   f"RANSAC {1e3 * (t3 - t2) / n_sample:.1f} ms/frame (numpy/LAPACK restatement of skimage 0.18.3, "
-                   f"1000 trials), warp {1e3 * (t4 - t3) / n_sample:.1f} ms/frame (C oracle)"),
+                   f"n_kp_global={bc.n_kp_global}, {bc.model}), {procs} single-threaded worker process(es) "
+                   f"like the reference's joblib pool: match {1e3 * (t1 - t0):.0f} ms "
+                   f"(C oracle knnMatch + reference numpy filters), consensus {1e3 * (t2 - t1):.1f} ms "
+                   f"(CPython set/Counter, parent), RANSAC + warp {1e3 * (t3 - t2):.0f} ms "
+                   f"(numpy/LAPACK restatement of skimage 0.18.3 with 1000 trials; C warp)"),
         "seconds": total,
     }
 
@@ -296,6 +308,8 @@ def main():
                     help="BASELINE workload (c2 = configs[1], the headline line)")
     ap.add_argument("--frames", type=int, default=None, help="frames per GPU (default: the config's)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="frames in the CPU-baseline sample (0: skip)")
+    ap.add_argument("--cpu-procs", type=int, default=8,
+                    help="worker processes of the CPU baseline (the reference's per-core pool)")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the PCIe-inclusive path: frames in pinned host memory, streamed through "
                          "the warp in slabs (pipeline.align_streamed); reported as `end_to_end`, not `value`")
@@ -309,7 +323,7 @@ def main():
     if args.frames is None:
         args.frames = bc.frames_per_gpu
     if args.cpu_sample is None:
-        args.cpu_sample = bc.cpu_sample
+        args.cpu_sample = bc.cpu_sample * max(1, args.cpu_procs) // 2
 
     rank, world, local = kdist.init_from_env("nccl")
     if world != args.gpus:
@@ -411,7 +425,7 @@ def main():
     if args.detect and bc.C == 1:
         result["with_detection"] = with_detection(inp, cfg, dev, world)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        result["cpu_baseline"] = cpu_baseline(bc, ks, args.cpu_sample)
+        result["cpu_baseline"] = cpu_baseline(bc, ks, args.cpu_sample, args.cpu_procs)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
