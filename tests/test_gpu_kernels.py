@@ -208,7 +208,8 @@ def test_ransac_gather_mode_matches_contiguous(dev):
 
 
 # ------------------------------------------------------------------------ K3
-@pytest.mark.parametrize("shape", [(1, 5, 7), (3, 64, 128), (2, 67, 131), (2, 130, 257), (1, 1080, 1920)])
+@pytest.mark.parametrize("shape", [(1, 5, 7), (3, 64, 128), (2, 67, 131), (2, 130, 257), (2, 90, 200), (1, 57, 136),
+                                   (1, 1080, 1920)])
 def test_warp_matches_oracle(dev, shape):
     F, H, W = shape
     rng = np.random.default_rng(H * W)
