@@ -367,40 +367,69 @@ __global__ __launch_bounds__(kThreads) void orb_select_kernel(const uint64_t* __
   if (tid == 0) out_n[f_base + f] = out;
 }
 
-// 5x5 binomial smoothing at one point: (sum w_i w_j I + 128) >> 8, w = 1 4 6 4 1.
-__device__ __forceinline__ int smooth5(const uint8_t* __restrict__ I, int W, int x, int y) {
+// The keypoint's 31x31 patch in LDS: moments use the radius-15 disc, BRIEF samples lie
+// within radius 13 of the keypoint and their 5x5 smoothing adds 2.
+constexpr int kPatch = 31, kPatchWords = 9;  // rows of 36 bytes from the 4-aligned column
+
+__device__ __forceinline__ int patch_at(const uint8_t* P, int ofs, int dx, int dy) {
+  return P[(dy + 15) * (4 * kPatchWords) + ofs + dx + 15];
+}
+
+// 5x5 binomial smoothing at one patch point: (sum w_i w_j I + 128) >> 8, w = 1 4 6 4 1.
+__device__ __forceinline__ int smooth5_patch(const uint8_t* P, int ofs, int dx, int dy) {
   int s = 0;
   const int w[5] = {1, 4, 6, 4, 1};
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    const uint8_t* row = I + (size_t)(y + i - 2) * W + x - 2;
+    const uint8_t* row = P + (dy + i - 2 + 15) * (4 * kPatchWords) + ofs + dx - 2 + 15;
     s += w[i] * ((int)row[0] + 4 * (int)row[1] + 6 * (int)row[2] + 4 * (int)row[3] + (int)row[4]);
   }
   return (s + 128) >> 8;
 }
 
-// One wave per keypoint: intensity-centroid moments (wave reduction), exact bin, then
-// 4 x 64 BRIEF comparisons of on-the-fly smoothed samples packed with ballots (the
-// 31x31 patch stays in L1, cheaper than smoothing whole frames for 500 keypoints).
+// One wave per keypoint: the 31x31 patch is staged into the wave's LDS slice with
+// coalesced 4-byte loads (scattered byte loads of the patch kept the texture units busy
+// for ~3400 cycles per keypoint), then intensity-centroid moments (wave reduction),
+// exact bin, and 4 x 64 BRIEF comparisons of smoothed samples packed with ballots.
 __global__ __launch_bounds__(kThreads) void orb_describe_kernel(const uint8_t* __restrict__ frames, int H, int W,
                                                                 const uint32_t* __restrict__ kp_pos,
                                                                 const int32_t* __restrict__ kp_n, int n_features,
                                                                 const int8_t* __restrict__ pattern,
                                                                 const double* __restrict__ bin_cs, int f_base,
                                                                 uint8_t* __restrict__ out_des) {
-  const int lane = threadIdx.x & 63;
+  __shared__ uint32_t patch[kThreads / 64][kPatch * kPatchWords];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int f = blockIdx.y;
-  const int k = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  if (k >= kp_n[f_base + f]) return;  // wave-uniform
+  const int k = blockIdx.x * (kThreads / 64) + wave;
+  if (k >= kp_n[f_base + f]) return;  // wave-uniform; no block barriers below
   const size_t slot = (size_t)(f_base + f) * n_features + k;
   const uint32_t pp = kp_pos[slot];
   const int x = (int)(pp & 0xffffu), y = (int)(pp >> 16);
   const uint8_t* I = frames + (size_t)f * H * W;
+  // rows y-15 .. y+15, bytes from bx = (x-15) & ~3 (x >= edge >= 16); the last word may
+  // run up to 3 bytes past the row end, into the next row (y + 15 < H - 1)
+  const int bx = (x - 15) & ~3, ofs = (x - 15) - bx;
+  uint32_t* Pw = patch[wave];
+  for (int i = lane; i < kPatch * kPatchWords; i += 64) {
+    const int r = i / kPatchWords, c = i - r * kPatchWords;
+    const uint8_t* src = I + (size_t)(y - 15 + r) * W + bx + 4 * c;
+    uint32_t v;
+    if ((W & 3) == 0) {
+      v = *reinterpret_cast<const uint32_t*>(src);
+    } else {
+      v = 0;
+      for (int b = 0; b < 4; ++b)
+        if (bx + 4 * c + b < W) v |= (uint32_t)src[b] << (8 * b);
+    }
+    Pw[i] = v;
+  }
+  __builtin_amdgcn_wave_barrier();  // one wave writes and reads its slice: in order, no block barrier
+  const uint8_t* P = reinterpret_cast<const uint8_t*>(Pw);
   int m10 = 0, m01 = 0;
   for (int i = lane; i < 31 * 31; i += 64) {
     const int dy = i / 31 - 15, dx = i % 31 - 15;
     if (dx * dx + dy * dy <= 225) {
-      const int v = I[(size_t)(y + dy) * W + (x + dx)];
+      const int v = patch_at(P, ofs, dx, dy);
       m10 += dx * v;
       m01 += dy * v;
     }
@@ -423,8 +452,8 @@ __global__ __launch_bounds__(kThreads) void orb_describe_kernel(const uint8_t* _
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int pi = 64 * r + lane;
-    const int p = smooth5(I, W, x + pt[4 * pi], y + pt[4 * pi + 1]);
-    const int q = smooth5(I, W, x + pt[4 * pi + 2], y + pt[4 * pi + 3]);
+    const int p = smooth5_patch(P, ofs, pt[4 * pi], pt[4 * pi + 1]);
+    const int q = smooth5_patch(P, ofs, pt[4 * pi + 2], pt[4 * pi + 3]);
     const unsigned long long m = __ballot(p < q);
     if (lane == 0) {
 #pragma unroll
