@@ -325,9 +325,14 @@ def main():
     if args.cpu_sample is None:
         args.cpu_sample = bc.cpu_sample * max(1, args.cpu_procs) // 2
 
-    rank, world, local = kdist.init_from_env("nccl")
+    # KCMC_BENCH_BACKEND=gloo + KCMC_BENCH_ONE_DEVICE=1: rehearsal of the multi-rank
+    # path with every rank on cuda:0 (a 1-GPU box cannot host two RCCL ranks)
+    backend = os.environ.get("KCMC_BENCH_BACKEND", "nccl")
+    rank, world, local = kdist.init_from_env(backend)
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if os.environ.get("KCMC_BENCH_ONE_DEVICE") == "1":
+        local = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     t_setup = time.perf_counter()

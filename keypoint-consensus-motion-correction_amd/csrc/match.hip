@@ -5,17 +5,22 @@
 //
 // knn2_l2u8_kernel -- one workgroup = 256 template rows x one frame.
 //   The distance is an exact integer contraction, so it runs on the int8 matrix
-//   cores: with x = a - 128 and y = b - 128 (int8), SSD = |x|^2 + |y|^2 - 2 x.y and
-//   x.y comes from v_mfma_i32_32x32x32_i8.  A operand = 32 frame descriptors (rows j),
-//   B operand = 32 template descriptors (columns i), so each lane owns one template
-//   column and 16 frame rows of the 32x32 tile and keeps a running top-2 in
-//   registers.  The top-2 runs on packed keys (ssd << jb | j): for D <= 64 bytes
-//   sqrtf is strictly increasing on the integer SSD range, so integer
-//   keys order exactly like OpenCV's float distances, and the low bits make ties go
-//   to the lower frame index like OpenCV's K-insertion.  4 VALU ops per distance
-//   (key = tk + qk - g*2^(jb+1); min; med3).  Frame descriptors are staged through
-//   LDS in 256-row chunks (converted to int8, zero-padded to DP, rows padded by 16 B
-//   so the ds_read_b128 fragment reads are bank-conflict free).
+//   cores.  With x = a - 128 (template) and y = 127 - b (frame), both int8,
+//   a - b = x + y + 1, so SSD = T + Q + 2 x.y with T = sum(x^2 + 2x) + D per template
+//   row and Q = sum(y^2 + 2y) per frame row.  v_mfma_i32_32x32x32_i8 runs the K loop
+//   twice over the same fragments with the accumulator initialised to T, so it
+//   returns T + 2 x.y directly.  A operand = 32 frame descriptors (rows j), B operand
+//   = 32 template descriptors (columns i): each lane owns one template column and 16
+//   frame rows of the 32x32 tile and keeps a running top-2 in registers.
+//   The top-2 runs on 32-bit keys (ssd << 8 | j - q0) local to a 256-row chunk of
+//   frame descriptors (ssd <= 64 * 255^2 < 2^22): for D <= 64 bytes sqrtf is strictly
+//   increasing on the integer SSD range, so integer keys order exactly
+//   like OpenCV's float distances, and the low bits make ties go to the lower frame
+//   index like OpenCV's K-insertion.  3 VALU ops per distance after the accumulator
+//   read: key = acc << 8 + qk (v_lshl_add), b2 = med3(b1, b2, key), b1 = min(b1, key).
+//   Each chunk's top-2 is merged into a 64-bit (ssd << 32 | j) top-2.  Frame
+//   descriptors are staged through LDS (converted to int8, zero-padded to DP, rows
+//   padded by 16 B so the ds_read_b128 fragment reads are bank-conflict free).
 //
 // match_filter_kernel -- one workgroup per frame: VA:196-214 in float64 with the
 //   reference's exact operation order (no FMA contraction; file built with
@@ -34,52 +39,55 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int kThreads = 256;
 constexpr int kBlocksPerWave = 2;                         // 32-row template blocks per wave
 constexpr int kTplPerWG = (kThreads / 64) * kBlocksPerWave * 32;  // 256
-constexpr int kQChunk = 256;                              // frame descriptors per LDS chunk
+constexpr int kQChunk = 256;                              // frame descriptors per LDS chunk (8-bit local index)
+constexpr uint32_t kNoKey = 0xffffffffu;                  // chunk keys of real rows are < 2^30
+constexpr uint32_t kPad = 0xc0000000u;                    // key base of the padding rows of a tile
+constexpr unsigned long long kNoKey64 = ~0ull;
 
-template <bool WIDE>
-struct KeyT;
-template <>
-struct KeyT<false> {
-  using T = uint32_t;
-  static constexpr T kMax = 0xffffffffu;
-};
-template <>
-struct KeyT<true> {
-  using T = unsigned long long;
-  static constexpr T kMax = ~0ull;
-};
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 
-__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b) { return a < b ? a : b; }
+// b1 <= b2 always; new b2 = median(b1, b2, key), new b1 = min(b1, key).
+__device__ __forceinline__ void top2_insert(uint32_t& b1, uint32_t& b2, uint32_t key) {
+  b2 = med3_u32(b1, b2, key);
+  b1 = b1 < key ? b1 : key;
+}
 
-template <typename K>
-__device__ __forceinline__ void top2_insert(K& b1, K& b2, K key) {
-  // b1 <= b2 always; new b2 = median(b1, b2, key), new b1 = min(b1, key).
-  K hi = b1 > key ? b1 : key;
+__device__ __forceinline__ void top2_insert64(unsigned long long& b1, unsigned long long& b2, unsigned long long key) {
+  const unsigned long long hi = b1 > key ? b1 : key;
   b2 = b2 < hi ? b2 : hi;
   b1 = b1 < key ? b1 : key;
 }
 
-// Signed-byte view of 4 consecutive descriptor bytes at column `col` (zero past D).
-__device__ __forceinline__ uint32_t load4_signed(const uint8_t* row, int col, int D) {
+// 4 consecutive descriptor bytes at column `col`, each XORed with `x` (0x80: a - 128,
+// 0x7f: 127 - b as int8), zero past D.
+__device__ __forceinline__ uint32_t load4_xor(const uint8_t* row, int col, int D, uint32_t x) {
   uint32_t w = 0;
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
-    uint32_t v = (col + b < D) ? (uint32_t)(row[col + b] ^ 0x80u) : 0u;
+    uint32_t v = (col + b < D) ? (uint32_t)(row[col + b] ^ x) : 0u;
     w |= v << (8 * b);
   }
   return w;
 }
 
-template <int DP, bool WIDE>
+// sum(v^2 + 2v) over the four int8 lanes of w, accumulated into acc
+__device__ __forceinline__ int sq2(uint32_t w, int acc) {
+  acc = __builtin_amdgcn_sdot4((int)w, (int)w, acc, false);
+  return __builtin_amdgcn_sdot4((int)w, 0x02020202, acc, false);
+}
+
+template <int DP>
 __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
     const uint8_t* __restrict__ des_tpl, int n_tpl, int D, const uint8_t* __restrict__ des_q,
-    const int32_t* __restrict__ q_off, int jb, int32_t* __restrict__ out_idx,
-    float* __restrict__ out_dist) {
-  using K = typename KeyT<WIDE>::T;
+    const int32_t* __restrict__ q_off, int32_t* __restrict__ out_idx, float* __restrict__ out_dist) {
   constexpr int KSTEPS = DP / 32;
   constexpr int ROWB = DP + 16;  // padded LDS row stride (bytes)
   __shared__ __attribute__((aligned(16))) uint8_t qbuf[kQChunk * ROWB];
-  __shared__ __attribute__((aligned(16))) K qkey[kQChunk];
+  __shared__ uint32_t qkey[kQChunk];
 
   const int f = blockIdx.y;
   const int tid = threadIdx.x;
@@ -89,11 +97,10 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
   const int h = lane >> 5;   // k-half of the fragment / row group of the output
   const int q_begin = q_off[f];
   const int n_q = q_off[f + 1] - q_begin;
-  const K jmask = (K)((1ull << jb) - 1ull);
 
-  // ---- template fragments (B operand) and their squared norms, kept in registers
+  // ---- template fragments (B operand) and T = sum(x^2 + 2x) + D, kept in registers
   v4i bfrag[kBlocksPerWave][KSTEPS];
-  K tk[kBlocksPerWave];
+  int tk[kBlocksPerWave];
   int tpl_row[kBlocksPerWave];
 #pragma unroll
   for (int b = 0; b < kBlocksPerWave; ++b) {
@@ -106,25 +113,25 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
       if (i < n_tpl) {
         const uint8_t* row = des_tpl + (size_t)i * D;
 #pragma unroll
-        for (int d = 0; d < 4; ++d) w[d] = load4_signed(row, 32 * kk + 16 * h + 4 * d, D);
+        for (int d = 0; d < 4; ++d) w[d] = load4_xor(row, 32 * kk + 16 * h + 4 * d, D, 0x80u);
       }
 #pragma unroll
-      for (int d = 0; d < 4; ++d) na = __builtin_amdgcn_sdot4((int)w[d], (int)w[d], na, false);
+      for (int d = 0; d < 4; ++d) na = sq2(w[d], na);
       bfrag[b][kk] = v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
     }
     na += __shfl_xor(na, 32);
-    tk[b] = WIDE ? (K)na : ((K)na << jb);
+    tk[b] = na + D;
   }
 
-  K best1[kBlocksPerWave], best2[kBlocksPerWave];
+  unsigned long long g1[kBlocksPerWave], g2[kBlocksPerWave];
 #pragma unroll
-  for (int b = 0; b < kBlocksPerWave; ++b) best1[b] = best2[b] = KeyT<WIDE>::kMax;
+  for (int b = 0; b < kBlocksPerWave; ++b) g1[b] = g2[b] = kNoKey64;
 
   for (int q0 = 0; q0 < n_q; q0 += kQChunk) {
     const int cnt = min(kQChunk, n_q - q0);
     const int rows = (cnt + 31) & ~31;
     __syncthreads();  // previous chunk fully consumed
-    // ---- stage frame descriptors [q0, q0+cnt) as int8, zero-padded to DP columns
+    // ---- stage frame descriptors [q0, q0+cnt) as int8 127 - b, zero-padded to DP columns
     const uint8_t* base = des_q + (size_t)(q_begin + q0) * D;
     for (int e = tid; e < rows * (DP / 4); e += kThreads) {
       const int r = e / (DP / 4);
@@ -132,24 +139,27 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
       uint32_t w = 0;
       if (r < cnt) {
         if ((D & 3) == 0) {
-          w = (col < D) ? (*reinterpret_cast<const uint32_t*>(base + (size_t)r * D + col) ^ 0x80808080u) : 0u;
+          w = (col < D) ? (*reinterpret_cast<const uint32_t*>(base + (size_t)r * D + col) ^ 0x7f7f7f7fu) : 0u;
         } else {
-          w = load4_signed(base + (size_t)r * D, col, D);
+          w = load4_xor(base + (size_t)r * D, col, D, 0x7fu);
         }
       }
       *reinterpret_cast<uint32_t*>(&qbuf[r * ROWB + col]) = w;
     }
     __syncthreads();
-    // ---- per-row key part: |y|^2 << jb | j
+    // ---- per-row key part: Q << 8 | (j - q0)  (Q >= -D may be negative: modular)
     for (int r = tid; r < rows; r += kThreads) {
       int nb = 0;
       const uint32_t* rw = reinterpret_cast<const uint32_t*>(&qbuf[r * ROWB]);
 #pragma unroll
-      for (int d = 0; d < DP / 4; ++d) nb = __builtin_amdgcn_sdot4((int)rw[d], (int)rw[d], nb, false);
-      const K j = (K)(q0 + r);
-      qkey[r] = WIDE ? (((K)nb << 32) | j) : (((K)nb << jb) | j);
+      for (int d = 0; d < DP / 4; ++d) nb = sq2(rw[d], nb);
+      // rows past cnt (zero descriptors, so acc = T < 2^21) get keys in [kPad, kPad + 2^29)
+      qkey[r] = r < cnt ? (((uint32_t)nb << 8) | (uint32_t)r) : kPad;
     }
     __syncthreads();
+    uint32_t b1[kBlocksPerWave], b2[kBlocksPerWave];
+#pragma unroll
+    for (int b = 0; b < kBlocksPerWave; ++b) b1[b] = b2[b] = kNoKey;
     // ---- MFMA tiles of 32 frame rows
     for (int t0 = 0; t0 < rows; t0 += 32) {
       v4i afrag[KSTEPS];
@@ -157,66 +167,58 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
       for (int kk = 0; kk < KSTEPS; ++kk)
         afrag[kk] = *reinterpret_cast<const v4i*>(&qbuf[(t0 + c) * ROWB + 32 * kk + 16 * h]);
       // rows of this lane's 16 accumulators: t0 + (r&3) + 8*(r>>2) + 4*h
-      K qk[16];
+      uint32_t qk[16];
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int s = 0; s < 4; ++s) qk[4 * g + s] = qkey[t0 + 8 * g + 4 * h + s];
-      const bool partial = (t0 + 32 > cnt);
 #pragma unroll
       for (int b = 0; b < kBlocksPerWave; ++b) {
-        v16i acc = {0};
+        v16i acc;
 #pragma unroll
-        for (int kk = 0; kk < KSTEPS; ++kk)
-          acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag[kk], bfrag[b][kk], acc, 0, 0, 0);
+        for (int r = 0; r < 16; ++r) acc[r] = tk[b];
+#pragma unroll
+        for (int rep = 0; rep < 2; ++rep)  // acc = T + 2 x.y
+#pragma unroll
+          for (int kk = 0; kk < KSTEPS; ++kk)
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag[kk], bfrag[b][kk], acc, 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          K key;
-          if (WIDE) {
-            // ssd = |x|^2 + |y|^2 - 2 x.y; key = ssd << 32 | j
-            const long long ssd = (long long)tk[b] + (long long)(qk[r] >> 32) - 2ll * acc[r];
-            key = ((K)ssd << 32) | (qk[r] & 0xffffffffull);
-          } else {
-            key = (K)(tk[b] + qk[r] - ((uint32_t)acc[r] << (jb + 1)));
-          }
-          if (partial) {
-            const int row = t0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            key = (row < cnt) ? key : KeyT<WIDE>::kMax;
-          }
-          top2_insert(best1[b], best2[b], key);
+          top2_insert(b1[b], b2[b], ((uint32_t)acc[r] << 8) + qk[r]);
         }
       }
+    }
+    // ---- fold the chunk's top-2 (local indices) into the frame's 64-bit top-2
+#pragma unroll
+    for (int b = 0; b < kBlocksPerWave; ++b) {
+      const uint32_t ks[2] = {b1[b], b2[b]};
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        if (ks[k] < kPad)
+          top2_insert64(g1[b], g2[b], ((unsigned long long)(ks[k] >> 8) << 32) | (uint32_t)(q0 + (int)(ks[k] & 255u)));
     }
   }
 
   // ---- merge the two row halves (lanes l and l^32 own the same template column)
 #pragma unroll
   for (int b = 0; b < kBlocksPerWave; ++b) {
-    K o1, o2;
-    if (WIDE) {
-      o1 = (K)__shfl_xor((long long)best1[b], 32);
-      o2 = (K)__shfl_xor((long long)best2[b], 32);
-    } else {
-      o1 = (K)__shfl_xor((int)best1[b], 32);
-      o2 = (K)__shfl_xor((int)best2[b], 32);
-    }
-    const K m1 = best1[b] < o1 ? best1[b] : o1;
-    const K hi = best1[b] < o1 ? o1 : best1[b];
-    const K lo2 = best2[b] < o2 ? best2[b] : o2;
-    const K m2 = hi < lo2 ? hi : lo2;
+    const unsigned long long o1 = (unsigned long long)__shfl_xor((long long)g1[b], 32);
+    const unsigned long long o2 = (unsigned long long)__shfl_xor((long long)g2[b], 32);
+    unsigned long long m1 = g1[b], m2 = g2[b];
+    top2_insert64(m1, m2, o1);
+    top2_insert64(m1, m2, o2);
     const int i = tpl_row[b];
     if (h == 0 && i < n_tpl) {
       const size_t o = ((size_t)f * n_tpl + i) * 2;
-      const K ms[2] = {m1, m2};
+      const unsigned long long ms[2] = {m1, m2};
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
-        if (ms[k] == KeyT<WIDE>::kMax) {
+        if (ms[k] == kNoKey64) {
           out_idx[o + k] = -1;
           out_dist[o + k] = FLT_MAX;
         } else {
-          const unsigned long long ssd = WIDE ? ((unsigned long long)ms[k] >> 32) : (unsigned long long)(ms[k] >> jb);
-          out_idx[o + k] = (int32_t)(WIDE ? (ms[k] & 0xffffffffull) : (ms[k] & jmask));
-          out_dist[o + k] = sqrtf((float)ssd);
+          out_idx[o + k] = (int32_t)(ms[k] & 0xffffffffull);
+          out_dist[o + k] = sqrtf((float)(ms[k] >> 32));
         }
       }
     }
@@ -323,30 +325,15 @@ __global__ __launch_bounds__(kFilterThreads) void match_filter_kernel(
   }
 }
 
-int bits_for(long long v) {  // bits to represent 0..v
-  int b = 1;
-  while ((1ll << b) <= v) ++b;
-  return b;
-}
-
 int launch_knn(const uint8_t* des_tpl, int n_tpl, int D, const uint8_t* des_q, const int32_t* q_off,
                int n_frames, int max_nq, int32_t* out_idx, float* out_dist, hipStream_t s) {
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
-  const long long ssd_max = (long long)D * 255 * 255;
-  const int jb = bits_for(max_nq > 0 ? max_nq - 1 : 0);
-  const bool wide = (bits_for(ssd_max) + jb > 32) || ((((unsigned long long)ssd_max << jb) | ((1ull << jb) - 1)) >= 0xffffffffull);
+  (void)max_nq;
   dim3 grid(ceil_div(n_tpl, kTplPerWG), n_frames);
-  if (D <= 32) {
-    if (wide)
-      hipLaunchKernelGGL((knn2_l2u8_kernel<32, true>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, jb, out_idx, out_dist);
-    else
-      hipLaunchKernelGGL((knn2_l2u8_kernel<32, false>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, jb, out_idx, out_dist);
-  } else {
-    if (wide)
-      hipLaunchKernelGGL((knn2_l2u8_kernel<64, true>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, jb, out_idx, out_dist);
-    else
-      hipLaunchKernelGGL((knn2_l2u8_kernel<64, false>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, jb, out_idx, out_dist);
-  }
+  if (D <= 32)
+    hipLaunchKernelGGL((knn2_l2u8_kernel<32>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+  else
+    hipLaunchKernelGGL((knn2_l2u8_kernel<64>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
   return launch_check("knn2_l2u8_kernel");
 }
 

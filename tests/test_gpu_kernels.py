@@ -48,7 +48,8 @@ def test_knn2_matches_oracle(dev, D):
 
 
 def test_knn2_wide_keys_and_edge_counts(dev):
-    # n_q > 1024 with D = 64 does not fit 32-bit packed keys -> 64-bit key path
+    # n_q > 1024 with D = 64: ssd << 11 | j would not fit 32 bits; the kernel keys each
+    # 256-row chunk locally and folds the chunks into a 64-bit top-2
     rng = np.random.default_rng(11)
     D, n_tpl = 64, 97
     tpl = rng.integers(0, 256, (n_tpl, D), dtype=np.uint8)
@@ -59,6 +60,37 @@ def test_knn2_wide_keys_and_edge_counts(dev):
     idx, dist = idx.cpu().numpy(), dist.cpu().numpy()
     for f, q in enumerate(frames):
         ri, rd = oracle.knn2_l2u8(tpl, q)
+        assert np.array_equal(idx[f], ri), f
+        assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), f
+
+
+@pytest.mark.parametrize("D", [32, 61, 64])
+def test_knn2_chunk_boundaries_and_extreme_bytes(dev, D):
+    # exact duplicates straddling the 256-row LDS chunks (ties must go to the lower
+    # frame index across chunks), and all-0 / all-255 descriptors (SSD = D * 255^2, the
+    # largest key; the int8 offsets -128 / 127 at both ends)
+    rng = np.random.default_rng(100 + D)
+    n_tpl = 70
+    tpl = rng.integers(0, 256, (n_tpl, D), dtype=np.uint8)
+    tpl[0] = 0
+    tpl[1] = 255
+    tpl[2, ::2] = 255
+    tpl[2, 1::2] = 0
+    q = rng.integers(0, 256, (800, D), dtype=np.uint8)
+    for j in (255, 256, 511, 512, 799):
+        q[j] = tpl[5]
+    for j in (250, 300, 767, 768):
+        q[j] = tpl[6]
+    q[600] = 255
+    q[601] = 0
+    q2 = np.full((3, D), 255, np.uint8)  # every distance to tpl[0] is the maximum
+    q2[1] = 0
+    frames = [q, q2, q[:257], q[:256], q[:255]]
+    off = _csr(frames)
+    idx, dist = stages.knn2_l2u8(_t(tpl, dev), _t(np.concatenate(frames), dev), _t(off, dev), 800)
+    idx, dist = idx.cpu().numpy(), dist.cpu().numpy()
+    for f, fq in enumerate(frames):
+        ri, rd = oracle.knn2_l2u8(tpl, fq)
         assert np.array_equal(idx[f], ri), f
         assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), f
 

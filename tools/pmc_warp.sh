@@ -5,7 +5,7 @@
 set -u
 OUT=${1:-gpurun_out/pmc}
 RE=${2:-warp_affine}
-shift 2 2>/dev/null
+shift $(( $# < 2 ? $# : 2 ))
 EXTRA=("$@")
 R=$PWD
 mkdir -p "$OUT"
