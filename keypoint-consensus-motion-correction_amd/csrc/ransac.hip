@@ -69,7 +69,7 @@ __device__ __forceinline__ double resid2(const Model& m, const Pts& P, int k, do
   const double xp = fma(y, -m.s, x * m.c) + m.tx;
   const double yp = fma(y, m.c, x * m.s) + m.ty;
   const double ex = xp - P.dx[k], ey = yp - P.dy[k];
-  const double r = sqrt(ex * ex + ey * ey);
+  const double r = sqrt_resid(ex * ex + ey * ey);
   cnt += (r < thresh) ? 1 : 0;
   return r * r;
 }

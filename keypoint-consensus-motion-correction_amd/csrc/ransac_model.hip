@@ -244,7 +244,7 @@ __device__ __forceinline__ double resid2(const double (&h)[9], const Pts& P, int
     Y = Y / w;
   }
   const double ex = X - P.dx[k], ey = Y - P.dy[k];
-  const double r = sqrt(ex * ex + ey * ey);
+  const double r = sqrt_resid(ex * ex + ey * ey);
   cnt += (r < thresh) ? 1 : 0;
   return r * r;
 }

@@ -111,15 +111,23 @@ def consensus_stage(keep_bits_host: np.ndarray, n_tpl: int, n_frames: int, cfg: 
     return cons
 
 
-def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.Consensus,
-                 cfg: AlignConfig) -> stages.RansacResult:
-    """VA:137-142: RANSAC of every frame's consensus points (src = the frame's matched
-    keypoints, dst = template keypoints).  params [F, 2, 3] for the euclidean and
-    affine models (model.params[:2], like VA:319), [F, 3, 3] for the projective one."""
-    dev = kp_tpl.device
-    F, n_tpl = match.kp_ordered.shape[:2]
+def consensus_to_device(cons: stages.Consensus, dev) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The consensus point lists (pt_off, pt_idx) as device tensors."""
     pt_off = torch.from_numpy(cons.pt_off).to(dev, non_blocking=False)
     pt_idx = torch.from_numpy(cons.pt_idx if cons.pt_idx.size else np.zeros(1, np.int32)).to(dev)
+    return pt_off, pt_idx
+
+
+def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.Consensus,
+                 cfg: AlignConfig, lists_dev: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+                 ) -> stages.RansacResult:
+    """VA:137-142: RANSAC of every frame's consensus points (src = the frame's matched
+    keypoints, dst = template keypoints).  params [F, 2, 3] for the euclidean and
+    affine models (model.params[:2], like VA:319), [F, 3, 3] for the projective one.
+    ``lists_dev``: the consensus lists already on the device (consensus_to_device)."""
+    dev = kp_tpl.device
+    F, n_tpl = match.kp_ordered.shape[:2]
+    pt_off, pt_idx = lists_dev if lists_dev is not None else consensus_to_device(cons, dev)
     if cfg.ransac_model == "euclidean":
         return stages.ransac_rigid(match.kp_ordered.view(F * n_tpl, 2), kp_tpl, pt_off, cons.pt_off, pt_idx=pt_idx,
                                    src_frame_stride=n_tpl, trials=cfg.ransac_trials,
