@@ -1,6 +1,8 @@
 // Ablation lab for the warp kernel (not part of the library).  Build on this host:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude tools/warp_lab.hip -o tools/warp_lab
-// Run on the GPU box: tools/warp_lab [frames]
+// Run on the GPU box: tools/warp_lab [frames] [texture.u16]
+// (texture.u16: one raw 1080 x 1920 uint16 frame, e.g. the bench texture written by
+//  tools/write_texture.py; adds a fifth source-value set, every frame = that texture)
 #include <cmath>
 #include <cstdio>
 #include <vector>
@@ -106,10 +108,31 @@ int main(int argc, char** argv) {
   // source values: 14-bit (exact integer blend everywhere), 13-bit with 0.1% hot pixels
   // (sparse float-faithful fallback, like the bench texture), full 16-bit (fallback in
   // nearly every row)
-  for (int dist = 0; dist < 4; ++dist) {
-    static const char* dn[] = {"14-bit", "13-bit + 0.1% hot pixels", "16-bit", "13-bit + 1/8 of 32x32 blocks ~40k"};
+  std::vector<uint16_t> tex;
+  if (argc > 2) {
+    FILE* fp = fopen(argv[2], "rb");
+    if (!fp) { printf("cannot open %s\n", argv[2]); return 1; }
+    tex.resize((size_t)H * W);
+    if (fread(tex.data(), 2, tex.size(), fp) != tex.size()) { printf("short texture file\n"); return 1; }
+    fclose(fp);
+  }
+  const int only = getenv("LAB_DIST") ? atoi(getenv("LAB_DIST")) : -1;
+  for (int dist = 0; dist < (tex.empty() ? 4 : 5); ++dist) {
+    if (only >= 0 && dist != only) continue;
+    static const char* dn[] = {"14-bit", "13-bit + 0.1% hot pixels", "16-bit", "13-bit + 1/8 of 32x32 blocks ~40k",
+                               "bench texture (file)"};
     printf("-- source values: %s\n", dn[dist]);
-    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0, src, n, (uint32_t)dist);
+    if (dist < 4) {
+      hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0, src, n, (uint32_t)dist);
+    } else {
+      CK(hipMemcpy(src, tex.data(), tex.size() * 2, hipMemcpyHostToDevice));
+      for (int f = 1; f < F; ++f) CK(hipMemcpy(src + (size_t)f * H * W, src, tex.size() * 2, hipMemcpyDeviceToDevice));
+    }
+    if (getenv("LAB_ONLY56")) {  // the library's configuration only, 3 repeats
+      for (int k = 0; k < 3; ++k)
+        report("128x56 (box 20 KB)", timeit([&] { launch_warp<1, C56, 0>(src, dst, M, F, H, W, 0, ws, 0); }, reps));
+      continue;
+    }
     report("128x64 (box 24 KB)", timeit([&] { launch_warp<1, C64, 0>(src, dst, M, F, H, W, 0, ws, 0); }, reps));
     report("128x64: no-compute (zeros)", timeit([&] { launch_warp<1, C64, 1>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
     report("128x64: no staging loads", timeit([&] { launch_warp<1, C64, 2>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
