@@ -264,6 +264,33 @@ def test_knn2_f32_matches_oracle(dev, D):
         assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), f
 
 
+@pytest.mark.parametrize("scale", [1e-3, 37.0, 1e4])
+def test_knn2_f32_scaled_and_near_ties(dev, scale):
+    """The bf16x3 candidate search's error bound scales with the descriptor norms: scaled
+    descriptors, frame rows that differ from a template row by one bf16 ulp of a single
+    element (near-ties below the split's resolution) and rows of mixed magnitude."""
+    rng = np.random.default_rng(int(scale * 10))
+    n_tpl, D = 200, 128
+    tpl = (rng.normal(0, 1, (n_tpl, D)) * scale).astype(np.float32)
+    frames = []
+    for n_q in [900, 130, 33]:
+        q = (rng.normal(0, 1, (n_q, D)) * scale).astype(np.float32)
+        q[: n_q // 4] = tpl[rng.integers(0, n_tpl, n_q // 4)]
+        for k in range(n_q // 4, n_q // 4 + 12):  # copies of template row 7 nudged in one element
+            q[k] = tpl[7]
+            q[k, k % D] = np.nextafter(q[k, k % D], np.float32(np.inf), dtype=np.float32)
+        q[-3:] *= np.float32(1e-2)  # small-norm rows
+        frames.append(q)
+    off = _csr(frames)
+    idx, dist = stages.knn2_l2u8(_t(tpl, dev), _t(np.concatenate(frames).reshape(-1, D), dev), _t(off, dev),
+                                 int(np.diff(off).max()))
+    idx, dist = idx.cpu().numpy(), dist.cpu().numpy()
+    for f, q in enumerate(frames):
+        ri, rd = oracle.knn2_l2f32(tpl, q)
+        assert np.array_equal(idx[f], ri), f
+        assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), f
+
+
 def test_match_frames_f32_vs_oracle(dev):
     """SIFT-style float descriptors through knn + the reference's filters (VA:196-214)."""
     ks = synthetic.make_keypoints(12, 400, 128, (1080, 1920), seed=15, descriptor="f32")
