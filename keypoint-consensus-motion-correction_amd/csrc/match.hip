@@ -80,7 +80,45 @@ __device__ __forceinline__ int sq2(uint32_t w, int acc) {
   return __builtin_amdgcn_sdot4((int)w, 0x02020202, acc, false);
 }
 
+// Chunk staging of 16-byte pieces (D % 16 == 0): PPR pieces per padded row, KP per
+// thread.  Loads are branch-free (row clamped to the frame's last row, piece clamped to
+// the descriptor), so that all of a thread's loads are in flight together; out-of-range
+// pieces are zeroed when they land.
 template <int DP>
+struct Pieces {
+  static constexpr int kPPR = DP / 16;
+  static constexpr int kKP = kQChunk * kPPR / kThreads;
+};
+
+template <int DP>
+__device__ __forceinline__ void issue_pieces(const uint8_t* __restrict__ rows0, int D, int last, int tid,
+                                             uint4 (&pf)[Pieces<DP>::kKP]) {
+#pragma unroll
+  for (int it = 0; it < Pieces<DP>::kKP; ++it) {
+    const int e = tid + kThreads * it;
+    const int r = min(e / Pieces<DP>::kPPR, last), pc = min(e % Pieces<DP>::kPPR, D / 16 - 1);
+    pf[it] = *reinterpret_cast<const uint4*>(rows0 + (size_t)r * D + 16 * pc);
+  }
+}
+
+template <int DP, int ROWB>
+__device__ __forceinline__ void land_pieces(uint8_t* qbuf, int D, int cnt, int tid,
+                                            const uint4 (&pf)[Pieces<DP>::kKP]) {
+#pragma unroll
+  for (int it = 0; it < Pieces<DP>::kKP; ++it) {
+    const int e = tid + kThreads * it;
+    const int r = e / Pieces<DP>::kPPR, pc = e % Pieces<DP>::kPPR;
+    uint4 w = pf[it];
+    w.x ^= 0x7f7f7f7fu;  // int8 127 - b
+    w.y ^= 0x7f7f7f7fu;
+    w.z ^= 0x7f7f7f7fu;
+    w.w ^= 0x7f7f7f7fu;
+    if (r >= cnt || 16 * pc >= D) w = make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(&qbuf[r * ROWB + 16 * pc]) = w;
+  }
+}
+
+template <int DP, bool VEC16>
 __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
     const uint8_t* __restrict__ des_tpl, int n_tpl, int D, const uint8_t* __restrict__ des_q,
     const int32_t* __restrict__ q_off, int32_t* __restrict__ out_idx, float* __restrict__ out_dist) {
@@ -127,26 +165,39 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
 #pragma unroll
   for (int b = 0; b < kBlocksPerWave; ++b) g1[b] = g2[b] = kNoKey64;
 
+  // VEC16 (D % 16 == 0): the next chunk's loads are issued before the current chunk's
+  // MFMA tiles, so their latency hides behind them
+  uint4 pf[Pieces<DP>::kKP];
+  if constexpr (VEC16) {
+    if (n_q > 0) issue_pieces<DP>(des_q + (size_t)q_begin * D, D, n_q - 1, tid, pf);
+  }
   for (int q0 = 0; q0 < n_q; q0 += kQChunk) {
     const int cnt = min(kQChunk, n_q - q0);
     const int rows = (cnt + 31) & ~31;
     __syncthreads();  // previous chunk fully consumed
     // ---- stage frame descriptors [q0, q0+cnt) as int8 127 - b, zero-padded to DP columns
     const uint8_t* base = des_q + (size_t)(q_begin + q0) * D;
-    for (int e = tid; e < rows * (DP / 4); e += kThreads) {
-      const int r = e / (DP / 4);
-      const int col = (e % (DP / 4)) * 4;
-      uint32_t w = 0;
-      if (r < cnt) {
-        if ((D & 3) == 0) {
-          w = (col < D) ? (*reinterpret_cast<const uint32_t*>(base + (size_t)r * D + col) ^ 0x7f7f7f7fu) : 0u;
-        } else {
-          w = load4_xor(base + (size_t)r * D, col, D, 0x7fu);
+    if constexpr (VEC16) {
+      land_pieces<DP, ROWB>(qbuf, D, cnt, tid, pf);
+    } else {
+      for (int e = tid; e < rows * (DP / 4); e += kThreads) {
+        const int r = e / (DP / 4);
+        const int col = (e % (DP / 4)) * 4;
+        uint32_t w = 0;
+        if (r < cnt) {
+          if ((D & 3) == 0) {
+            w = (col < D) ? (*reinterpret_cast<const uint32_t*>(base + (size_t)r * D + col) ^ 0x7f7f7f7fu) : 0u;
+          } else {
+            w = load4_xor(base + (size_t)r * D, col, D, 0x7fu);
+          }
         }
+        *reinterpret_cast<uint32_t*>(&qbuf[r * ROWB + col]) = w;
       }
-      *reinterpret_cast<uint32_t*>(&qbuf[r * ROWB + col]) = w;
     }
     __syncthreads();
+    if constexpr (VEC16) {
+      if (q0 + kQChunk < n_q) issue_pieces<DP>(base + (size_t)kQChunk * D, D, n_q - 1 - q0 - kQChunk, tid, pf);
+    }
     // ---- per-row key part: Q << 8 | (j - q0)  (Q >= -D may be negative: modular)
     for (int r = tid; r < rows; r += kThreads) {
       int nb = 0;
@@ -330,10 +381,15 @@ int launch_knn(const uint8_t* des_tpl, int n_tpl, int D, const uint8_t* des_q, c
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
   (void)max_nq;
   dim3 grid(ceil_div(n_tpl, kTplPerWG), n_frames);
-  if (D <= 32)
-    hipLaunchKernelGGL((knn2_l2u8_kernel<32>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+  const bool vec16 = (D & 15) == 0;
+  if (D <= 32 && vec16)
+    hipLaunchKernelGGL((knn2_l2u8_kernel<32, true>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+  else if (D <= 32)
+    hipLaunchKernelGGL((knn2_l2u8_kernel<32, false>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+  else if (vec16)
+    hipLaunchKernelGGL((knn2_l2u8_kernel<64, true>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
   else
-    hipLaunchKernelGGL((knn2_l2u8_kernel<64>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+    hipLaunchKernelGGL((knn2_l2u8_kernel<64, false>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
   return launch_check("knn2_l2u8_kernel");
 }
 
