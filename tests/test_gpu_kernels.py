@@ -258,7 +258,7 @@ def test_warp_matches_oracle(dev, shape):
         assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], Ms[f])), f
 
 
-@pytest.mark.parametrize("values", ["14bit", "hot", "blobs", "edge16384"])
+@pytest.mark.parametrize("values", ["14bit", "hot", "blobs", "edge16384", "dense_hot", "bright_lines"])
 def test_warp_fast_path_value_ranges(dev, values):
     # the fixed-pitch staged path picks its blend per tile: exact integer for boxes below
     # 16384, packed-fp32 OpenCV evaluation otherwise; mix both within one frame
@@ -273,6 +273,13 @@ def test_warp_fast_path_value_ranges(dev, values):
         imgs = rng.integers(0, 8192, (F, H, W))
         blk = rng.random((F, H // 32 + 1, W // 32 + 1)) < 0.15
         imgs = np.where(np.repeat(np.repeat(blk, 32, 1), 32, 2)[:, :H, :W], imgs + 36000, imgs)
+    elif values == "dense_hot":  # ~3 % hot pixels: many queued fix-ups per wave (queue flushes)
+        imgs = rng.integers(0, 8192, (F, H, W))
+        imgs[rng.random((F, H, W)) < 0.03] = 60000
+    elif values == "bright_lines":  # bright horizontal lines: rows re-blended in float at once
+        imgs = rng.integers(0, 8192, (F, H, W))
+        imgs[:, 17::41, :] = 50000
+        imgs[rng.random((F, H, W)) < 1e-3] = 65535
     else:  # straddle the 2^24 boundary of the integer blend sum
         imgs = rng.integers(16370, 16400, (F, H, W))
     imgs = imgs.astype(np.uint16)
