@@ -225,21 +225,41 @@ __device__ __forceinline__ void stage_land(uint16_t* stile, const Box& box, int 
 
 // Staging of a C-channel box with 16-byte chunks of the interleaved rows (W % 8 == 0:
 // ax0 and W are multiples of 8 pixels, so a chunk is entirely inside or outside the
-// image row and zero-filling whole chunks is exactly BORDER_CONSTANT).
-template <int C>
-__device__ __forceinline__ void stage_vec_c(const uint16_t* __restrict__ S, uint16_t* stile, const Box& box, int H,
-                                            int W, int tid) {
-  const int cpr = box.pitch * C / 8;  // chunks per staged row
+// image row and zero-filling whole chunks is exactly BORDER_CONSTANT).  Chunk
+// q = tid + kThreads * k of the box; every load of a thread is issued before any lands
+// (a load-then-store loop waits for each load in turn: the 4K RGB warp took 14.6 ms per
+// 625 frames that way, 11.8 ms with the loads in flight together).
+template <class Cfg, int C>
+struct VecC {
+  static constexpr int kPasses = (Cfg::kLdsElems / 8 + kThreads - 1) / kThreads;
+};
+
+template <class Cfg, int C>
+__device__ __forceinline__ void stage_vec_c_issue(const uint16_t* __restrict__ S, const Box& box, int H, int W,
+                                                  int tid, uint4 (&chunk)[VecC<Cfg, C>::kPasses]) {
+  const int cpr = box.pitch * C / 8;
   const int total = box.rows * cpr;
   const int rowe = W * C;
-  for (int q = tid; q < total; q += kThreads) {
+#pragma unroll
+  for (int k = 0; k < VecC<Cfg, C>::kPasses; ++k) {
+    const int q = tid + kThreads * k;
     const int r = q / cpr, cc = q - r * cpr;
     const int gy = box.sy0 + r;
     const int e = box.ax0 * C + 8 * cc;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if ((unsigned)gy < (unsigned)H && e >= 0 && e < rowe)
-      v = *reinterpret_cast<const uint4*>(S + (size_t)gy * rowe + e);
-    *reinterpret_cast<uint4*>(&stile[r * box.pitch * C + 8 * cc]) = v;
+    chunk[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (q < total && (unsigned)gy < (unsigned)H && e >= 0 && e < rowe)
+      chunk[k] = *reinterpret_cast<const uint4*>(S + (size_t)gy * rowe + e);
+  }
+}
+
+template <class Cfg, int C>
+__device__ __forceinline__ void stage_vec_c_land(uint16_t* stile, const Box& box, int tid,
+                                                 const uint4 (&chunk)[VecC<Cfg, C>::kPasses]) {
+  const int total = box.rows * (box.pitch * C / 8);
+#pragma unroll
+  for (int k = 0; k < VecC<Cfg, C>::kPasses; ++k) {
+    const int q = tid + kThreads * k;
+    if (q < total) reinterpret_cast<uint4*>(stile)[q] = chunk[k];
   }
 }
 
@@ -625,7 +645,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
   if (box.mode == 3) box.mode = 0;  // lab ablations: the general staged path
   const bool vec_stage = (C == 1) && ((W & 7) == 0);
   uint4 chunk[Cfg::kRowPasses];
+  uint4 cchunk[C > 1 ? VecC<Cfg, C>::kPasses : 1];
   if (box.mode == 0 && vec_stage && VARIANT != 2) stage_issue<Cfg>(S, box, H, W, tid, chunk);  // loads first
+  if constexpr (C > 1) {
+    if (box.mode == 0 && (W & 7) == 0) stage_vec_c_issue<Cfg, C>(S, box, H, W, tid, cchunk);
+  }
   int ad[2], bd[2], X0v, Y0v;  // overlaps the loads
   lane_coords<Cfg>(minv + 6 * (size_t)f, xb, yb, W, wave, lane, box.mode == 0 ? box.ax0 : 0,
                    box.mode == 0 ? box.sy0 : 0, ad, bd, X0v, Y0v);
@@ -633,7 +657,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
     if (vec_stage) {
       if (VARIANT != 2) stage_land<Cfg>(stile, box, tid, chunk);
     } else if (C > 1 && (W & 7) == 0) {
-      stage_vec_c<C>(S, stile, box, H, W, tid);
+      if constexpr (C > 1) stage_vec_c_land<Cfg, C>(stile, box, tid, cchunk);
     } else {
       stage_scalar<C>(S, stile, box, H, W, tid);
     }
@@ -865,16 +889,20 @@ warp_perspective_u16_kernel(const uint16_t* __restrict__ src, uint16_t* __restri
   const Box box = unpack(plan[tile]);
   const bool vec_stage = (C == 1) && ((W & 7) == 0);
   uint4 chunk[Cfg::kRowPasses];
+  uint4 cchunk[C > 1 ? VecC<Cfg, C>::kPasses : 1];
   if (box.mode == 0 && vec_stage) stage_issue<Cfg>(S, box, H, W, tid, chunk);
+  if constexpr (C > 1) {
+    if (box.mode == 0 && (W & 7) == 0) stage_vec_c_issue<Cfg, C>(S, box, H, W, tid, cchunk);
+  }
   double M[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) M[k] = minv[9 * (size_t)f + k];
   if (box.mode == 0) {
-    if (vec_stage)
+    if (vec_stage) {
       stage_land<Cfg>(stile, box, tid, chunk);
-    else if (C > 1 && (W & 7) == 0)
-      stage_vec_c<C>(S, stile, box, H, W, tid);
-    else
+    } else if (C > 1 && (W & 7) == 0) {
+      if constexpr (C > 1) stage_vec_c_land<Cfg, C>(stile, box, tid, cchunk);
+    } else
       stage_scalar<C>(S, stile, box, H, W, tid);
   }
   __syncthreads();
