@@ -118,6 +118,39 @@ __device__ __forceinline__ void land_pieces(uint8_t* qbuf, int D, int cnt, int t
   }
 }
 
+// Chunk staging for any D (not a multiple of 16): the chunk's rows are one contiguous
+// byte range [start, start + cnt * D) of des_q, loaded as 16-byte pieces aligned down from
+// start (an aligned piece that begins inside the range never crosses a page the range
+// does not touch) into a raw LDS buffer, all of a thread's loads in flight together; the
+// padded int8 rows are then cut from it with two aligned LDS words + v_alignbyte per word.
+template <int DP>
+struct RawChunk {
+  static constexpr int kPieces = (kQChunk * DP + 16 + 15) / 16;          // pieces of one chunk
+  static constexpr int kKP = (kPieces + kThreads - 1) / kThreads;        // per thread
+  static constexpr int kWords = kKP * kThreads * 4 + 4;                  // raw LDS words
+};
+
+template <int DP>
+__device__ __forceinline__ void issue_raw(const uint8_t* __restrict__ start, int nbytes, int tid,
+                                          uint4 (&pf)[RawChunk<DP>::kKP]) {
+  const uint4* a = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(start) & ~(uintptr_t)15);
+  const int delta = (int)(reinterpret_cast<uintptr_t>(start) & 15);
+  const int np = (nbytes + delta + 15) >> 4;  // pieces overlapping the range
+#pragma unroll
+  for (int it = 0; it < RawChunk<DP>::kKP; ++it) {
+    const int k = tid + kThreads * it;
+    pf[it] = make_uint4(0u, 0u, 0u, 0u);
+    if (k < np) pf[it] = a[k];
+  }
+}
+
+template <int DP>
+__device__ __forceinline__ void land_raw(uint32_t* qraw, int tid, const uint4 (&pf)[RawChunk<DP>::kKP]) {
+#pragma unroll
+  for (int it = 0; it < RawChunk<DP>::kKP; ++it)
+    reinterpret_cast<uint4*>(qraw)[tid + kThreads * it] = pf[it];
+}
+
 template <int DP, bool VEC16>
 __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
     const uint8_t* __restrict__ des_tpl, int n_tpl, int D, const uint8_t* __restrict__ des_q,
@@ -126,6 +159,7 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
   constexpr int ROWB = DP + 16;  // padded LDS row stride (bytes)
   __shared__ __attribute__((aligned(16))) uint8_t qbuf[kQChunk * ROWB];
   __shared__ uint32_t qkey[kQChunk];
+  __shared__ __attribute__((aligned(16))) uint32_t qraw[VEC16 ? 4 : RawChunk<DP>::kWords];
 
   const int f = blockIdx.y;
   const int tid = threadIdx.x;
@@ -168,8 +202,11 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
   // VEC16 (D % 16 == 0): the next chunk's loads are issued before the current chunk's
   // MFMA tiles, so their latency hides behind them
   uint4 pf[Pieces<DP>::kKP];
+  uint4 rf[VEC16 ? 1 : RawChunk<DP>::kKP];
   if constexpr (VEC16) {
     if (n_q > 0) issue_pieces<DP>(des_q + (size_t)q_begin * D, D, n_q - 1, tid, pf);
+  } else {
+    if (n_q > 0) issue_raw<DP>(des_q + (size_t)q_begin * D, min(kQChunk, n_q) * D, tid, rf);
   }
   for (int q0 = 0; q0 < n_q; q0 += kQChunk) {
     const int cnt = min(kQChunk, n_q - q0);
@@ -180,16 +217,18 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
     if constexpr (VEC16) {
       land_pieces<DP, ROWB>(qbuf, D, cnt, tid, pf);
     } else {
+      land_raw<DP>(qraw, tid, rf);
+      __syncthreads();
+      const int delta = (int)(reinterpret_cast<uintptr_t>(base) & 15);
       for (int e = tid; e < rows * (DP / 4); e += kThreads) {
         const int r = e / (DP / 4);
         const int col = (e % (DP / 4)) * 4;
         uint32_t w = 0;
-        if (r < cnt) {
-          if ((D & 3) == 0) {
-            w = (col < D) ? (*reinterpret_cast<const uint32_t*>(base + (size_t)r * D + col) ^ 0x7f7f7f7fu) : 0u;
-          } else {
-            w = load4_xor(base + (size_t)r * D, col, D, 0x7fu);
-          }
+        if (r < cnt && col < D) {
+          const int o = r * D + col + delta;  // byte offset in the raw buffer
+          const uint32_t lo = qraw[o >> 2], hi = qraw[(o >> 2) + 1];
+          w = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(o & 3)) ^ 0x7f7f7f7fu;
+          if (col + 4 > D) w &= (1u << (8 * (D - col))) - 1u;  // zero past D (int8 padding)
         }
         *reinterpret_cast<uint32_t*>(&qbuf[r * ROWB + col]) = w;
       }
@@ -197,6 +236,9 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
     __syncthreads();
     if constexpr (VEC16) {
       if (q0 + kQChunk < n_q) issue_pieces<DP>(base + (size_t)kQChunk * D, D, n_q - 1 - q0 - kQChunk, tid, pf);
+    } else {
+      if (q0 + kQChunk < n_q)
+        issue_raw<DP>(base + (size_t)kQChunk * D, min(kQChunk, n_q - q0 - kQChunk) * D, tid, rf);
     }
     // ---- per-row key part: Q << 8 | (j - q0)  (Q >= -D may be negative: modular)
     for (int r = tid; r < rows; r += kThreads) {
