@@ -59,6 +59,29 @@ __device__ __forceinline__ float exact_dist(const float* __restrict__ a, const f
   return sqrtf((float)S);
 }
 
+// The same sum for 16-byte aligned rows with D % 4 == 0, read four floats per load (the
+// fallback's lanes each walk a different frame row: a quarter of the load instructions).
+__device__ __forceinline__ float exact_dist4(const float* __restrict__ a, const float* __restrict__ b, int D) {
+  double S = 0.0;
+  for (int k = 0; k < D; k += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(a + k), y = *reinterpret_cast<const float4*>(b + k);
+    double t = (double)x.x - (double)y.x;
+    S += t * t;
+    t = (double)x.y - (double)y.y;
+    S += t * t;
+    t = (double)x.z - (double)y.z;
+    S += t * t;
+    t = (double)x.w - (double)y.w;
+    S += t * t;
+  }
+  return sqrtf((float)S);
+}
+
+__device__ __forceinline__ float exact_dist_any(const float* __restrict__ a, const float* __restrict__ b, int D) {
+  const bool v4 = (D & 3) == 0 && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
+  return v4 ? exact_dist4(a, b, D) : exact_dist(a, b, D);
+}
+
 // (dist, index) lexicographic order: OpenCV's insertion gives ties to the lower index.
 __device__ __forceinline__ bool lex_less(float d, int j, float e, int k) { return d < e || (d == e && j < k); }
 
@@ -130,11 +153,15 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
   if (q >= q_off[f + 1] || q >= qrows) return;  // whole 32-lane groups exit together
   const int col = (threadIdx.x & 31) * 4;
   const float* src = des_q + (size_t)q * D;
-  float4 w;
-  w.x = col < D ? src[col] : 0.f;
-  w.y = col + 1 < D ? src[col + 1] : 0.f;
-  w.z = col + 2 < D ? src[col + 2] : 0.f;
-  w.w = col + 3 < D ? src[col + 3] : 0.f;
+  float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+  if ((D & 3) == 0 && (reinterpret_cast<uintptr_t>(des_q) & 15) == 0) {
+    if (col < D) w = *reinterpret_cast<const float4*>(src + col);
+  } else {
+    w.x = col < D ? src[col] : 0.f;
+    w.y = col + 1 < D ? src[col + 1] : 0.f;
+    w.z = col + 2 < D ? src[col + 2] : 0.f;
+    w.w = col + 3 < D ? src[col + 3] : 0.f;
+  }
   float ss = fmaf(w.w, w.w, fmaf(w.z, w.z, fmaf(w.y, w.y, w.x * w.x)));
 #pragma unroll
   for (int off = 16; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
@@ -361,7 +388,7 @@ __global__ __launch_bounds__(kThreads) void knn2_l2f32_kernel(
     for (int k = 0; k < 3; ++k) {
       if (k < ncand) {
         const int j = t.j[k];
-        top2_insert_exact(d0, j0, d1, j1, exact_dist(a, base + (size_t)j * D, D), j);
+        top2_insert_exact(d0, j0, d1, j1, exact_dist_any(a, base + (size_t)j * D, D), j);
       }
     }
     out_idx[o] = j0;
@@ -392,7 +419,7 @@ __global__ __launch_bounds__(256) void knn2_l2f32_fallback_kernel(const float* _
     float d0 = FLT_MAX, d1 = FLT_MAX;
     int j0 = -1, j1 = -1;
     for (int j = lane; j < n_q; j += 64)
-      top2_insert_exact(d0, j0, d1, j1, exact_dist(a, des_q + (size_t)(q_begin + j) * D, D), j);
+      top2_insert_exact(d0, j0, d1, j1, exact_dist_any(a, des_q + (size_t)(q_begin + j) * D, D), j);
     for (int off = 32; off > 0; off >>= 1) {
       const float e0 = __shfl_xor(d0, off), e1 = __shfl_xor(d1, off);
       const int k0 = __shfl_xor(j0, off), k1 = __shfl_xor(j1, off);
