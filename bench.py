@@ -141,14 +141,11 @@ def run_step(inp, cfg, out, timer=None, world=1, counts=None):
     else:
         keep_all = m.keep_bits.cpu().numpy()
         n_all = keep_all.shape[0]
-    cons = pipeline.consensus_stage(keep_all, n_tpl, n_all, cfg)
+    frames = None
     if world > 1:
         rank = torch.distributed.get_rank()
-        f0, nl = sum(counts[:rank]), counts[rank]
-        po = cons.pt_off
-        lo, hi = int(po[f0]), int(po[f0 + nl])
-        cons = stages.Consensus(cons.order, cons.votes, (po[f0:f0 + nl + 1] - lo).astype(np.int32),
-                                cons.pt_idx[lo:hi])
+        frames = (sum(counts[:rank]), sum(counts[:rank]) + counts[rank])
+    cons = pipeline.consensus_stage(keep_all, n_tpl, n_all, cfg, frames=frames)
     if timer:
         timer.mark("r0")
     rr = pipeline.ransac_stage(m, inp.kp_tpl, cons, cfg)

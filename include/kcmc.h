@@ -124,6 +124,15 @@ int kcmc_match_frames_f32(kcmc_ctx* ctx, const float* des_tpl_dev, const double*
 int kcmc_consensus(const uint32_t* keep_bits_host, int n_frames, int n_tpl, int n_kp_global,
                    int n_min, int32_t* out_consensus_host, int32_t* out_votes_host,
                    int* out_n_consensus, int32_t* out_pt_off_host, int32_t* out_pt_idx_host);
+/* The same consensus (from all n_frames frames' bitmasks) with the per-frame lists of
+ * frames [f_begin, f_end) only: out_pt_off_host [f_end - f_begin + 1] (starting at 0),
+ * out_pt_idx_host [(f_end - f_begin) * n_kp_global].  A rank of a frame-sharded job
+ * calls it with its own frame range after the bitmask all-gather, so that its host
+ * work per step does not grow with the number of ranks. */
+int kcmc_consensus_slice(const uint32_t* keep_bits_host, int n_frames, int n_tpl, int n_kp_global,
+                         int n_min, int f_begin, int f_end, int32_t* out_consensus_host,
+                         int32_t* out_votes_host, int* out_n_consensus, int32_t* out_pt_off_host,
+                         int32_t* out_pt_idx_host);
 
 /* --------------------------------------------------------------- K2: RANSAC
  * The seeded sample stream skimage 0.18.3 consumes: trial t of a frame with n points

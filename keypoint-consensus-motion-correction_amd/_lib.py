@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "kcmc_knn2_l2f32",
     "kcmc_match_frames_f32",
     "kcmc_consensus",
+    "kcmc_consensus_slice",
     "kcmc_hypothesis_table",
     "kcmc_ransac_prepare",
     "kcmc_ransac_rigid",
@@ -80,6 +81,7 @@ _SIGNATURES = {
     "kcmc_knn2_l2f32": ([P, P, I, I, P, P, I, I, P, P, P], I),
     "kcmc_match_frames_f32": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
     "kcmc_consensus": ([P, I, I, I, I, P, P, P, P, P], I),
+    "kcmc_consensus_slice": ([P, I, I, I, I, I, I, P, P, P, P, P], I),
     "kcmc_hypothesis_table": ([I, I, U32, I, P], I),
     "kcmc_ransac_prepare": ([P, P, I, I, U32], I),
     "kcmc_ransac_rigid": ([P, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, P], I),

@@ -212,6 +212,84 @@ class PySet {
   size_t mask_, fill_, used_;
 };
 
+// PySet's insertion/resize/probe rules on two fixed buffers (no allocation): the replay
+// of a per-frame intersection result, whose final table has at most kMax slots.
+class SmallPySet {
+ public:
+  static constexpr size_t kMax = 2048;  // holds up to 1228 keys (next resize at fill 1229)
+  SmallPySet() : t_(a_), mask_(7), fill_(0), used_(0) {
+    for (size_t i = 0; i < 8; ++i) t_[i] = kEmpty;
+  }
+  void add(int32_t key) {
+    size_t mask = mask_;
+    size_t i = (size_t)key & mask;
+    if (t_[i] == kEmpty) return store(i, key);
+    size_t perturb = (size_t)key;
+    while (true) {
+      if (t_[i] == key) return;
+      if (i + kLinearProbes <= mask) {
+        for (size_t j = 1; j <= kLinearProbes; ++j) {
+          if (t_[i + j] == kEmpty) return store(i + j, key);
+          if (t_[i + j] == key) return;
+        }
+      }
+      perturb >>= kPerturbShift;
+      i = (i * 5 + 1 + perturb) & mask;
+      if (t_[i] == kEmpty) return store(i, key);
+    }
+  }
+  template <class F>
+  void for_each(F&& f) const {
+    for (size_t i = 0; i <= mask_; ++i)
+      if (t_[i] != kEmpty) f(t_[i]);
+  }
+
+ private:
+  static constexpr int32_t kEmpty = -1;
+  static constexpr size_t kLinearProbes = 9;
+  static constexpr int kPerturbShift = 5;
+  void store(size_t slot, int32_t key) {
+    t_[slot] = key;
+    ++fill_;
+    ++used_;
+    if (fill_ * 5 < mask_ * 3) return;
+    size_t newsize = 8;
+    const size_t minused = used_ > 50000 ? used_ * 2 : used_ * 4;
+    while (newsize <= minused) newsize <<= 1;
+    int32_t* old = t_;
+    const size_t oldmask = mask_;
+    t_ = (t_ == a_) ? b_ : a_;
+    for (size_t i = 0; i < newsize; ++i) t_[i] = kEmpty;
+    mask_ = newsize - 1;
+    fill_ = used_;
+    for (size_t i = 0; i <= oldmask; ++i)
+      if (old[i] != kEmpty) insert_clean(old[i]);
+  }
+  void insert_clean(int32_t key) {
+    size_t mask = mask_;
+    size_t perturb = (size_t)key;
+    size_t i = (size_t)key & mask;
+    while (true) {
+      if (t_[i] == kEmpty) {
+        t_[i] = key;
+        return;
+      }
+      if (i + kLinearProbes <= mask) {
+        for (size_t j = 1; j <= kLinearProbes; ++j)
+          if (t_[i + j] == kEmpty) {
+            t_[i + j] = key;
+            return;
+          }
+      }
+      perturb >>= kPerturbShift;
+      i = (i * 5 + 1 + perturb) & mask;
+    }
+  }
+  int32_t* t_;
+  size_t mask_, fill_, used_;
+  int32_t a_[kMax], b_[kMax];
+};
+
 template <class F>
 void parallel_for(int n, F&& f) {
   unsigned hw = std::thread::hardware_concurrency();
@@ -221,10 +299,12 @@ void parallel_for(int n, F&& f) {
     return;
   }
   nt = std::min(nt, n / 32);
+  // contiguous blocks (no false sharing between threads' per-index outputs)
   std::vector<std::thread> th;
   for (int t = 0; t < nt; ++t)
     th.emplace_back([&, t] {
-      for (int i = t; i < n; i += nt) f(i);
+      const int b = (int)((long long)n * t / nt), e = (int)((long long)n * (t + 1) / nt);
+      for (int i = b; i < e; ++i) f(i);
     });
   for (auto& x : th) x.join();
 }
@@ -238,11 +318,12 @@ extern "C" int kcmc_hypothesis_table(int n, int trials, uint32_t seed, int min_s
   return hypothesis_table_impl(n, trials, seed, min_samples, out_host);
 }
 
-extern "C" int kcmc_consensus(const uint32_t* keep_bits, int n_frames, int n_tpl, int n_kp_global,
-                              int n_min, int32_t* out_consensus, int32_t* out_votes,
-                              int* out_n_consensus, int32_t* out_pt_off, int32_t* out_pt_idx) {
+extern "C" int kcmc_consensus_slice(const uint32_t* keep_bits, int n_frames, int n_tpl, int n_kp_global,
+                                    int n_min, int f_begin, int f_end, int32_t* out_consensus,
+                                    int32_t* out_votes, int* out_n_consensus, int32_t* out_pt_off,
+                                    int32_t* out_pt_idx) {
   if (n_frames < 0 || n_tpl < 0 || n_kp_global < 0 || (!keep_bits && n_frames > 0) ||
-      !out_n_consensus || !out_pt_off)
+      !out_n_consensus || !out_pt_off || f_begin < 0 || f_end < f_begin || f_end > n_frames)
     return fail(KCMC_EINVAL, "kcmc_consensus: bad arguments");
   const int words = (n_tpl + 31) / 32;
   auto frame_bits = [&](int f) { return keep_bits + (size_t)f * words; };
@@ -339,10 +420,15 @@ extern "C" int kcmc_consensus(const uint32_t* keep_bits, int n_frames, int n_tpl
   // insertion and resize history.  Only frames whose result keeps a key >= its final
   // table size replay the insertions.
   const std::vector<size_t> tsize = PySet::table_sizes((size_t)nc);
-  std::vector<std::vector<int32_t>> lists((size_t)n_frames);
+  const int nf = f_end - f_begin;
+  // per-frame results into a [nf, nc] scratch (no per-frame allocation), compacted below
+  std::vector<int32_t> scratch((size_t)nf * (size_t)std::max(nc, 1));
+  std::vector<int32_t> len((size_t)nf, 0);
+  // pass 1 (serial, a few dozen operations per frame): frames whose result keeps every
+  // key in its home slot list it in ascending order; the others are replayed in parallel
   std::vector<int> replay;
-  for (int f = 0; f < n_frames; ++f) {
-    const uint32_t* w = frame_bits(f);
+  for (int r = 0; r < nf; ++r) {
+    const uint32_t* w = frame_bits(f_begin + r);
     size_t m = 0;
     int top = -1;
     for (int k = 0; k < words; ++k) {
@@ -351,37 +437,55 @@ extern "C" int kcmc_consensus(const uint32_t* keep_bits, int n_frames, int n_tpl
       if (hit) top = 32 * k + 31 - __builtin_clz(hit);
     }
     if (top >= 0 && (size_t)top >= tsize[m]) {
-      replay.push_back(f);
+      replay.push_back(r);
       continue;
     }
-    auto& L = lists[(size_t)f];
-    L.reserve(m);
+    int32_t* L = scratch.data() + (size_t)r * (size_t)std::max(nc, 1);
+    int n = 0;
     for (int k = 0; k < words; ++k)
-      for (uint32_t b = w[k] & cons_bits[(size_t)k]; b; b &= b - 1) L.push_back(32 * k + __builtin_ctz(b));
+      for (uint32_t b = w[k] & cons_bits[(size_t)k]; b; b &= b - 1) L[n++] = 32 * k + __builtin_ctz(b);
+    len[(size_t)r] = n;
   }
-  parallel_for((int)replay.size(), [&](int r) {
-    const int f = replay[(size_t)r];
+  parallel_for((int)replay.size(), [&](int q) {
+    const int r = replay[(size_t)q], f = f_begin + r;
     const uint32_t* w = frame_bits(f);
-    size_t len = 0;
-    for (int k = 0; k < words; ++k) len += (size_t)__builtin_popcount(w[k]);
-    PySet result;
-    if (len > (size_t)nc) {
+    int32_t* L = scratch.data() + (size_t)r * (size_t)std::max(nc, 1);
+    size_t flen = 0;
+    for (int k = 0; k < words; ++k) flen += (size_t)__builtin_popcount(w[k]);
+    int n = 0;
+    if (flen > (size_t)nc && (size_t)nc <= 1228) {
+      // the common replay: iterate the consensus set, insert the frame's keys
+      SmallPySet result;
       for (int32_t key : cons_iter)
         if ((w[key >> 5] >> (key & 31)) & 1u) result.add(key);
+      result.for_each([&](int32_t key) { L[n++] = key; });
     } else {
-      frame_set(f).for_each([&](int64_t key) {
-        if ((cons_bits[(size_t)(key >> 5)] >> (key & 31)) & 1u) result.add(key);
-      });
+      PySet result;
+      if (flen > (size_t)nc) {
+        for (int32_t key : cons_iter)
+          if ((w[key >> 5] >> (key & 31)) & 1u) result.add(key);
+      } else {
+        frame_set(f).for_each([&](int64_t key) {
+          if ((cons_bits[(size_t)(key >> 5)] >> (key & 31)) & 1u) result.add(key);
+        });
+      }
+      result.for_each([&](int64_t key) { L[n++] = (int32_t)key; });
     }
-    auto& L = lists[(size_t)f];
-    L.reserve(result.size());
-    result.for_each([&](int64_t key) { L.push_back((int32_t)key); });
+    len[(size_t)r] = n;
   });
   out_pt_off[0] = 0;
-  for (int f = 0; f < n_frames; ++f) {
-    const auto& L = lists[(size_t)f];
-    if (out_pt_idx) std::copy(L.begin(), L.end(), out_pt_idx + out_pt_off[f]);
-    out_pt_off[f + 1] = out_pt_off[f] + (int32_t)L.size();
+  for (int r = 0; r < nf; ++r) {
+    if (out_pt_idx)
+      std::copy(scratch.begin() + (ptrdiff_t)r * std::max(nc, 1),
+                scratch.begin() + (ptrdiff_t)r * std::max(nc, 1) + len[(size_t)r], out_pt_idx + out_pt_off[r]);
+    out_pt_off[r + 1] = out_pt_off[r] + len[(size_t)r];
   }
   return KCMC_OK;
+}
+
+extern "C" int kcmc_consensus(const uint32_t* keep_bits, int n_frames, int n_tpl, int n_kp_global,
+                              int n_min, int32_t* out_consensus, int32_t* out_votes,
+                              int* out_n_consensus, int32_t* out_pt_off, int32_t* out_pt_idx) {
+  return kcmc_consensus_slice(keep_bits, n_frames, n_tpl, n_kp_global, n_min, 0, n_frames < 0 ? 0 : n_frames,
+                              out_consensus, out_votes, out_n_consensus, out_pt_off, out_pt_idx);
 }

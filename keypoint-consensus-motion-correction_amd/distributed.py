@@ -102,13 +102,10 @@ def align_sharded(inp: _pl.SlabInputs, cfg: _pl.AlignConfig, group=None, impl: S
     # K1 on the local slab, then exchange survivor bitmasks (exchange step 1)
     keep_bits, kp_ordered = impl.match(inp, cfg)
     keep_all = _all_gather_rows(keep_bits, counts, group).cpu().numpy()
-    cons = _pl.consensus_stage(keep_all, n_tpl, sum(counts), cfg, logger if rank == 0 else None)
-    # this rank's RANSAC point lists (global CSR sliced to the local frames)
-    po = cons.pt_off
-    lo, hi = int(po[f0]), int(po[f0 + n_local])
-    pt_off = (po[f0 : f0 + n_local + 1] - lo).astype(np.int32)
-    pt_idx = cons.pt_idx[lo:hi].astype(np.int32)
-    params = impl.ransac(kp_ordered, inp.kp_tpl, pt_off, pt_idx, cfg)
+    # the global consensus (every rank the same), RANSAC point lists of the local frames only
+    cons = _pl.consensus_stage(keep_all, n_tpl, sum(counts), cfg, logger if rank == 0 else None,
+                               frames=(f0, f0 + n_local))
+    params = impl.ransac(kp_ordered, inp.kp_tpl, cons.pt_off, cons.pt_idx, cfg)
     # exchange affines (exchange step 2), then the replicated host post-processing
     params_all = _all_gather_rows(params, counts, group).cpu().numpy()
     affines, skipped, interpolated, eu = _pl.postprocess_affines(params_all, cfg)

@@ -97,12 +97,23 @@ def match_stage(inp: SlabInputs, cfg: AlignConfig) -> stages.MatchResult:
 
 
 def consensus_stage(keep_bits_host: np.ndarray, n_tpl: int, n_frames: int, cfg: AlignConfig,
-                    logger: Optional[logging.Logger] = None) -> stages.Consensus:
-    cons = stages.consensus(keep_bits_host, n_tpl, cfg.n_kp_global, cfg.n_kp_global_min)
+                    logger: Optional[logging.Logger] = None,
+                    frames: Optional[Tuple[int, int]] = None) -> stages.Consensus:
+    """VA:224-286.  With ``frames`` = (f_begin, f_end) the point lists are made for those
+    frames only (a rank's share of a frame-sharded job; pt_off starts at 0), the
+    consensus and the per-frame log lines still cover every frame."""
+    cons = stages.consensus(keep_bits_host, n_tpl, cfg.n_kp_global, cfg.n_kp_global_min, frames=frames)
     if logger is not None and logger.isEnabledFor(logging.INFO):
         rates = np.array(cons.votes, dtype=np.int64) / n_frames
         logger.info(f"top n keypoints match rates: {rates}")
-        ns = np.diff(cons.pt_off)
+        if frames is None:
+            ns = np.diff(cons.pt_off)
+        else:  # every frame's point count = |consensus set & frame set|, from the bitmasks
+            kb = np.ascontiguousarray(keep_bits_host).view(np.uint32)
+            cbits = np.zeros(kb.shape[1], np.uint32)
+            for k in np.asarray(cons.order, dtype=np.int64):
+                cbits[k >> 5] |= np.uint32(1) << np.uint32(k & 31)
+            ns = np.unpackbits((kb & cbits).view(np.uint8), axis=1).sum(axis=1)
         for i in np.flatnonzero(ns < cfg.n_kp_frame_skip):
             logger.info(
                 f"transform for frame {int(i)} not estimated due to low keypoint count: "
@@ -236,14 +247,12 @@ class OverlappedSlabs:
 
                 rank = dist.get_rank(self.group)
                 keep = _all_gather_rows(match.keep_bits, self.counts, self.group).cpu().numpy()
-                cons = consensus_stage(keep, n_tpl, sum(self.counts), cfg, self.logger if rank == 0 else None)
                 f0 = sum(self.counts[:rank])
-                po = cons.pt_off
-                lo, hi = int(po[f0]), int(po[f0 + n_local])
-                local = stages.Consensus(cons.order, cons.votes, (po[f0:f0 + n_local + 1] - lo).astype(np.int32),
-                                         cons.pt_idx[lo:hi])
+                # the global consensus, point lists of this rank's frames only
+                cons = consensus_stage(keep, n_tpl, sum(self.counts), cfg, self.logger if rank == 0 else None,
+                                       frames=(f0, f0 + n_local))
                 mark("r0")
-                rr = ransac_stage(match, inp.kp_tpl, local, cfg)
+                rr = ransac_stage(match, inp.kp_tpl, cons, cfg)
                 mark("r1")
                 params = _all_gather_rows(rr.params, self.counts, self.group).cpu().numpy()
             else:

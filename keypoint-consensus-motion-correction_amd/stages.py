@@ -153,21 +153,28 @@ class Consensus:
     pt_idx: np.ndarray   # [P] i32 template indices in CPython set-iteration order (VA:274)
 
 
-def consensus(keep_bits: np.ndarray, n_tpl: int, n_kp_global: int, n_min: int) -> Consensus:
-    """VA:224-286 in native code with CPython set/Counter ordering."""
+def consensus(keep_bits: np.ndarray, n_tpl: int, n_kp_global: int, n_min: int,
+              frames: Optional[Tuple[int, int]] = None) -> Consensus:
+    """VA:224-286 in native code with CPython set/Counter ordering.  With ``frames`` =
+    (f_begin, f_end) the consensus still comes from every frame's bitmask but only the
+    point lists of frames [f_begin, f_end) are made (pt_off starts at 0): a rank's share
+    of a frame-sharded job."""
     kb = np.ascontiguousarray(keep_bits).view(np.uint32)
     F = kb.shape[0]
     if kb.shape != (F, (n_tpl + 31) // 32):
         raise ValueError("keep_bits must be [F, ceil(n_tpl/32)]")
+    f0, f1 = (0, F) if frames is None else (int(frames[0]), int(frames[1]))
+    if not 0 <= f0 <= f1 <= F:
+        raise ValueError(f"frame range {frames} outside [0, {F}]")
     n_kp_global = int(n_kp_global)
     cons = np.zeros(max(n_kp_global, 1), np.int32)
     votes = np.zeros(max(n_kp_global, 1), np.int32)
     n_c = ctypes.c_int(0)
-    pt_off = np.zeros(F + 1, np.int32)
-    pt_idx = np.zeros(max(F * max(n_kp_global, 0), 1), np.int32)
+    pt_off = np.zeros(f1 - f0 + 1, np.int32)
+    pt_idx = np.zeros(max((f1 - f0) * max(n_kp_global, 0), 1), np.int32)
     L = _lib.load()
-    _lib.check(L.kcmc_consensus(_np_ptr(kb), F, int(n_tpl), n_kp_global, int(n_min), _np_ptr(cons), _np_ptr(votes),
-                                ctypes.byref(n_c), _np_ptr(pt_off), _np_ptr(pt_idx)))
+    _lib.check(L.kcmc_consensus_slice(_np_ptr(kb), F, int(n_tpl), n_kp_global, int(n_min), f0, f1, _np_ptr(cons),
+                                      _np_ptr(votes), ctypes.byref(n_c), _np_ptr(pt_off), _np_ptr(pt_idx)))
     n = n_c.value
     return Consensus(cons[:n].copy(), votes[:n].copy(), pt_off, pt_idx[: pt_off[-1]].copy())
 

@@ -85,6 +85,24 @@ def test_native_consensus_sorted_order_shortcut_boundaries():
     _check_consensus(sets, n_tpl, 40)
 
 
+def test_native_consensus_frame_slices_match_full():
+    """kcmc_consensus_slice: the consensus of every frame, the point lists of a frame
+    range (a rank's share of a sharded job) == the full result's lists for those frames."""
+    rng = np.random.default_rng(11)
+    n_tpl, F = 500, 90
+    sets = [set(np.flatnonzero(rng.random(n_tpl) < 0.7).tolist()) for _ in range(F)]
+    kb = _bits(sets, n_tpl)
+    full = stages.consensus(kb, n_tpl, 100, 1)
+    for f0, f1 in [(0, F), (0, 1), (13, 57), (57, 90), (89, 90), (40, 40)]:
+        part = stages.consensus(kb, n_tpl, 100, 1, frames=(f0, f1))
+        assert np.array_equal(part.order, full.order) and np.array_equal(part.votes, full.votes)
+        lo, hi = full.pt_off[f0], full.pt_off[f1]
+        assert np.array_equal(part.pt_off, full.pt_off[f0:f1 + 1] - lo)
+        assert np.array_equal(part.pt_idx, full.pt_idx[lo:hi])
+    with pytest.raises(ValueError):
+        stages.consensus(kb, n_tpl, 100, 1, frames=(5, 91))
+
+
 def test_native_consensus_too_few_raises():
     with pytest.raises(VideoAligner.AlignmentError):
         stages.consensus(_bits([{1, 2}, {2, 3}], 10), 10, 10, 5)
