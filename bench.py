@@ -327,8 +327,8 @@ def load_traffic(config: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
                     help="BASELINE workload (c2 = configs[1], the headline line)")
     ap.add_argument("--frames", type=int, default=None, help="frames per GPU (default: the config's)")

@@ -74,7 +74,10 @@ struct CfgFor<4> {
 // immediate offset of the upper one, and the per-row source origins come from a per-frame
 // table through scalar loads.  Boxes wider than kFastPitch or taller than kFastRows take
 // the general staged path (mode 0).
-constexpr int kFastPitch = 144;           // pixels: 128-px tile + up to ~8 deg / 6 % zoom
+#ifndef KCMC_FAST_PITCH
+#define KCMC_FAST_PITCH 144
+#endif
+constexpr int kFastPitch = KCMC_FAST_PITCH;  // pixels: 128-px tile + up to ~8 deg / 6 % zoom
 constexpr int kFastChunks = kFastPitch / 8;  // 16-byte chunks per staged row
 template <class Cfg>
 struct Fast {

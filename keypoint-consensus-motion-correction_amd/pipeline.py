@@ -264,13 +264,21 @@ class OverlappedSlabs:
                 mark("r1")
                 params = rr.params.cpu().numpy()
         affines, skipped, interpolated, eu = postprocess_affines(params, cfg)
+        # the affines go up on the (idle) analysis stream, so the warp stream goes straight
+        # from the previous slab's warp to this one's (a copy queued behind that warp would
+        # add its own latency to every step); pinned + non_blocking, as a pageable copy
+        # waits for the device to drain
+        with torch.cuda.stream(self.analysis):
+            a = torch.from_numpy(np.ascontiguousarray(affines[f0:f0 + inp.frames.shape[0]], dtype=np.float64))
+            a = a.pin_memory().to(self.dev, non_blocking=True)
+            a_ready = torch.cuda.Event()
+            a_ready.record(self.analysis)
         with torch.cuda.stream(self.warp):
             if out is not None:
                 out.record_stream(self.warp)
             inp.frames.record_stream(self.warp)
-            # pinned + non_blocking: a pageable copy could wait for the warp stream to drain
-            a = torch.from_numpy(np.ascontiguousarray(affines[f0:f0 + inp.frames.shape[0]], dtype=np.float64))
-            a = a.pin_memory().to(self.dev, non_blocking=True)
+            a.record_stream(self.warp)
+            self.warp.wait_event(a_ready)
             mark("w0")
             aligned = warp_frames(inp.frames, a, out=out)
             mark("w1")

@@ -1,0 +1,67 @@
+"""Host timeline of the overlapped bench step (bench.py's default c2 workload): where the
+host spends a step while the warp of the previous step runs on the GPU.
+
+    python tools/host_breakdown.py [--frames 2000] [--steps 8]
+
+Prints, per step, host wall-clock milliseconds between the marks OverlappedSlabs.submit
+passes through (m0 match launched, m1, r0 after the bitmask D2H + native consensus, r1
+RANSAC launched, w0 after the affine D2H + post-processing + H2D, w1 warp launched), and
+the consensus alone on the same bitmasks.  A host chain longer than the warp means the
+warp stream idles between steps."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from kcmc_amd import pipeline  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=2000)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--priority", type=int, default=None, help="analysis stream priority (torch: -1 = high)")
+    args = ap.parse_args()
+    bc = bench.CONFIGS["c2"]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    inp, _ = bench.make_inputs(bc, args.frames, 0, dev)
+    out = torch.empty_like(inp.frames)
+    cfg = pipeline.AlignConfig(n_kp_global=bc.n_kp_global, ransac_model=bc.model)
+    ov = pipeline.OverlappedSlabs(dev, cfg)
+    if args.priority is not None:
+        ov.analysis = torch.cuda.Stream(dev, priority=args.priority)
+    rows = []
+    for s in range(args.steps + 2):
+        if s == 2:
+            ov.synchronize()
+            t_start = time.perf_counter()
+        t = {}
+        t0 = time.perf_counter()
+        ov.submit(inp, out=out, mark=lambda n: t.__setitem__(n, time.perf_counter()))
+        t["end"] = time.perf_counter()
+        if s >= 2:
+            keys = ["m0", "m1", "r0", "r1", "w0", "w1", "end"]
+            rows.append({f"{a}->{b}": round((t[b] - t[a]) * 1e3, 3) for a, b in zip(keys, keys[1:])}
+                        | {"submit_ms": round((t["end"] - t0) * 1e3, 3)})
+    ov.synchronize()
+    step_ms = (time.perf_counter() - t_start) * 1e3 / args.steps
+    keep = pipeline.match_stage(inp, cfg).keep_bits.cpu().numpy()
+    cons = []
+    for _ in range(5):
+        c0 = time.perf_counter()
+        pipeline.consensus_stage(keep, inp.des_tpl.shape[0], args.frames, cfg, None)
+        cons.append((time.perf_counter() - c0) * 1e3)
+    med = {k: round(float(np.median([r[k] for r in rows])), 3) for k in rows[0]}
+    print(json.dumps({"frames": args.frames, "priority": args.priority, "step_ms": round(step_ms, 3), "median_host_ms": med, "consensus_alone_ms": round(min(cons), 3),
+                      "cpu_count": os.cpu_count()}))
+
+
+if __name__ == "__main__":
+    main()
