@@ -123,10 +123,12 @@ def consensus_stage(keep_bits_host: np.ndarray, n_tpl: int, n_frames: int, cfg: 
 
 
 def consensus_to_device(cons: stages.Consensus, dev) -> Tuple[torch.Tensor, torch.Tensor]:
-    """The consensus point lists (pt_off, pt_idx) as device tensors."""
-    pt_off = torch.from_numpy(cons.pt_off).to(dev, non_blocking=False)
-    pt_idx = torch.from_numpy(cons.pt_idx if cons.pt_idx.size else np.zeros(1, np.int32)).to(dev)
-    return pt_off, pt_idx
+    """The consensus point lists (pt_off, pt_idx) as device tensors.  Stream-ordered
+    copies from pinned staging (the caching host allocator keeps the staging alive until
+    the copy has run): a pageable copy would block the host until the stream drains."""
+    pt_off = torch.from_numpy(cons.pt_off).pin_memory().to(dev, non_blocking=True)
+    pt_idx = torch.from_numpy(cons.pt_idx if cons.pt_idx.size else np.zeros(1, np.int32))
+    return pt_off, pt_idx.pin_memory().to(dev, non_blocking=True)
 
 
 def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.Consensus,

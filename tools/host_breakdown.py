@@ -1,7 +1,7 @@
-"""Host timeline of the overlapped bench step (bench.py's default c2 workload): where the
+"""Host timeline of the overlapped bench step (bench.py's workloads, default c2): where the
 host spends a step while the warp of the previous step runs on the GPU.
 
-    python tools/host_breakdown.py [--frames 2000] [--steps 8]
+    python tools/host_breakdown.py [--config c2] [--frames F] [--steps 8]
 
 Prints, per step, host wall-clock milliseconds between the marks OverlappedSlabs.submit
 passes through (m0 match launched, m1, r0 after the bitmask D2H + native consensus, r1
@@ -24,11 +24,13 @@ from kcmc_amd import pipeline  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=2000)
+    ap.add_argument("--config", default="c2", choices=sorted(bench.CONFIGS))
+    ap.add_argument("--frames", type=int, default=None)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--priority", type=int, default=None, help="analysis stream priority (torch: -1 = high)")
     args = ap.parse_args()
-    bc = bench.CONFIGS["c2"]
+    bc = bench.CONFIGS[args.config]
+    args.frames = args.frames or bc.frames_per_gpu
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     inp, _ = bench.make_inputs(bc, args.frames, 0, dev)
@@ -59,7 +61,7 @@ def main():
         pipeline.consensus_stage(keep, inp.des_tpl.shape[0], args.frames, cfg, None)
         cons.append((time.perf_counter() - c0) * 1e3)
     med = {k: round(float(np.median([r[k] for r in rows])), 3) for k in rows[0]}
-    print(json.dumps({"frames": args.frames, "priority": args.priority, "step_ms": round(step_ms, 3), "median_host_ms": med, "consensus_alone_ms": round(min(cons), 3),
+    print(json.dumps({"config": args.config, "frames": args.frames, "priority": args.priority, "step_ms": round(step_ms, 3), "median_host_ms": med, "consensus_alone_ms": round(min(cons), 3),
                       "cpu_count": os.cpu_count()}))
 
 
