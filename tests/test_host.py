@@ -85,6 +85,21 @@ def test_native_consensus_sorted_order_shortcut_boundaries():
     _check_consensus(sets, n_tpl, 40)
 
 
+def test_native_consensus_many_frames_threaded_vote():
+    """>= 8192 frames (the all-gathered bitmasks of a multi-GPU job): the vote counts are
+    split over threads; counts, first-occurrence order and point lists equal CPython's.
+    Key 0 only in the last frame and the top keys with counts that differ by one make
+    the per-thread partial sums and the any-mask merge observable."""
+    rng = np.random.default_rng(5)
+    n_tpl, F = 300, 9000
+    p = rng.uniform(0.05, 0.6, n_tpl)
+    p[0] = 0.0
+    sets = [set(np.flatnonzero(rng.random(n_tpl) < p).tolist()) for _ in range(F)]
+    sets[-1] = set(sorted(sets[-1] | {0}))  # built from an ascending list, like VA:214
+    _check_consensus(sets, n_tpl, 60)
+    _check_consensus(sets, n_tpl, n_tpl)
+
+
 def test_native_consensus_frame_slices_match_full():
     """kcmc_consensus_slice: the consensus of every frame, the point lists of a frame
     range (a rank's share of a sharded job) == the full result's lists for those frames."""
