@@ -7,12 +7,19 @@
 //     selection is Counter.most_common (stable by first occurrence).
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <climits>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <unistd.h>
 
 #include "kcmc_internal.h"
 
@@ -290,23 +297,106 @@ class SmallPySet {
   int32_t a_[kMax], b_[kMax];
 };
 
+// Persistent workers for the per-step host loops (the consensus replays and vote counts
+// run every step, and spawning 8-16 threads per call costs a few hundred microseconds).
+// run(tasks, fn) calls fn(0..tasks-1) on the workers and the calling thread and returns
+// when all have finished; concurrent callers are serialised.
+class WorkerPool {
+ public:
+  explicit WorkerPool(int n_workers) : pid_(getpid()) {
+    for (int i = 0; i < n_workers; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+  int size() const { return (int)workers_.size() + 1; }
+  pid_t pid() const { return pid_; }
+  void run(int tasks, const std::function<void(int)>& fn) {
+    std::lock_guard<std::mutex> caller(run_m_);
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      job_.store(&fn, std::memory_order_relaxed);
+      n_tasks_.store(tasks, std::memory_order_relaxed);
+      pending_.store(tasks, std::memory_order_relaxed);
+      next_.store(0, std::memory_order_release);
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [this] { return pending_.load(std::memory_order_acquire) == 0; });
+    next_.store(INT_MAX / 2, std::memory_order_relaxed);
+  }
+
+ private:
+  void work() {
+    while (true) {
+      const int t = next_.fetch_add(1, std::memory_order_acq_rel);
+      if (t >= n_tasks_.load(std::memory_order_relaxed)) return;
+      (*job_.load(std::memory_order_relaxed))(t);
+      if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        std::lock_guard<std::mutex> lk(m_);
+        done_cv_.notify_all();
+      }
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    while (true) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex m_, run_m_;
+  std::condition_variable cv_, done_cv_;
+  std::atomic<const std::function<void(int)>*> job_{nullptr};
+  std::atomic<int> n_tasks_{0};
+  std::atomic<int> next_{INT_MAX / 2}, pending_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  pid_t pid_;
+};
+
+WorkerPool& worker_pool() {
+  static std::mutex m;
+  static WorkerPool* pool = nullptr;
+  std::lock_guard<std::mutex> lk(m);
+  if (!pool || pool->pid() != getpid()) {  // a forked child has none of the parent's threads
+    unsigned hw = std::thread::hardware_concurrency();
+    pool = new WorkerPool((int)std::min<unsigned>(hw ? hw : 1, 16) - 1);  // never joined: lives with the process
+  }
+  return *pool;
+}
+
+// f(i) for i in [0, n) in contiguous blocks, one per pool thread (no false sharing between
+// the blocks' per-index outputs)
 template <class F>
 void parallel_for(int n, F&& f) {
-  unsigned hw = std::thread::hardware_concurrency();
-  int nt = (int)std::min<unsigned>(hw ? hw : 1, 16);
-  if (n < 64 || nt <= 1) {
+  if (n < 64) {
     for (int i = 0; i < n; ++i) f(i);
     return;
   }
-  nt = std::min(nt, n / 32);
-  // contiguous blocks (no false sharing between threads' per-index outputs)
-  std::vector<std::thread> th;
-  for (int t = 0; t < nt; ++t)
-    th.emplace_back([&, t] {
-      const int b = (int)((long long)n * t / nt), e = (int)((long long)n * (t + 1) / nt);
-      for (int i = b; i < e; ++i) f(i);
-    });
-  for (auto& x : th) x.join();
+  WorkerPool& pool = worker_pool();
+  const int nt = std::min(pool.size(), n / 32);
+  if (nt <= 1) {
+    for (int i = 0; i < n; ++i) f(i);
+    return;
+  }
+  pool.run(nt, [&](int t) {
+    const int b = (int)((long long)n * t / nt), e = (int)((long long)n * (t + 1) / nt);
+    for (int i = b; i < e; ++i) f(i);
+  });
 }
 }  // namespace
 
@@ -380,13 +470,10 @@ extern "C" int kcmc_consensus_slice(const uint32_t* keep_bits, int n_frames, int
   } else {
     std::vector<int32_t> cnt_p((size_t)vote_chunks * count.size(), 0);
     std::vector<uint32_t> any_p((size_t)vote_chunks * any.size(), 0u);
-    std::vector<std::thread> th;
-    for (int t = 0; t < vote_chunks; ++t)
-      th.emplace_back([&, t] {
-        vote((int)((long long)n_frames * t / vote_chunks), (int)((long long)n_frames * (t + 1) / vote_chunks),
-             cnt_p.data() + (size_t)t * count.size(), any_p.data() + (size_t)t * any.size());
-      });
-    for (auto& x : th) x.join();
+    worker_pool().run(vote_chunks, [&](int t) {
+      vote((int)((long long)n_frames * t / vote_chunks), (int)((long long)n_frames * (t + 1) / vote_chunks),
+           cnt_p.data() + (size_t)t * count.size(), any_p.data() + (size_t)t * any.size());
+    });
     for (int t = 0; t < vote_chunks; ++t) {
       for (size_t q = 0; q < count.size(); ++q) count[q] += cnt_p[(size_t)t * count.size() + q];
       for (size_t q = 0; q < any.size(); ++q) any[q] |= any_p[(size_t)t * any.size() + q];
