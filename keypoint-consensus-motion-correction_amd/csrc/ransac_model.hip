@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kThreads) void ransac_model_score_kernel(
     const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint64_t* __restrict__ hyp,
     const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, int n_skip,
-    double* __restrict__ out_params, double* __restrict__ best_model, uint8_t* __restrict__ out_inl,
+    double* out_params, double* best_model, uint8_t* __restrict__ out_inl,
     int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
   constexpr int K = MODEL == KCMC_MODEL_AFFINE ? 3 : 4;
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -537,8 +537,8 @@ template <int MODEL>
 __global__ __launch_bounds__(256) void ransac_model_refit_kernel(
     const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint8_t* __restrict__ inl,
-    const int32_t* __restrict__ nin, const double* __restrict__ best_model, int n_frames, double rate,
-    double* __restrict__ out_params) {
+    const int32_t* __restrict__ nin, const double* best_model, int n_frames, double rate,
+    double* out_params) {
   constexpr int n = MODEL == KCMC_MODEL_AFFINE ? 7 : 9;
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -730,9 +730,11 @@ extern "C" int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src, co
   if ((max_n > 128 ? lds_large : lds_small) > 150 * 1024)
     return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_model: max_n/trials exceed the LDS budget");
   hipStream_t s = (hipStream_t)stream;
-  void* ws = nullptr;
-  KCMC_TRY(workspace_alloc(ctx, &ws, (size_t)n_frames * 9 * sizeof(double), s));
-  double* best_model = static_cast<double*>(ws);
+  // The scoring kernel's best hypothesis model goes straight into out_params: the refit
+  // reads a frame's entries before it overwrites them (one wave per frame), and frames
+  // without a model get NaN in both roles.  No workspace: a stream-ordered pool
+  // allocation cost ~0.2 ms of host time per call.
+  double* best_model = out_params;
   const dim3 refit_grid((unsigned)ceil_div(n_frames, 4));
   if (model == KCMC_MODEL_AFFINE) {
     hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, false>), dim3(n_frames), dim3(kThreads),
@@ -756,7 +758,5 @@ extern "C" int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src, co
                        pt_idx, pt_off, src_frame_stride, out_inliers, out_n_inliers, best_model, n_frames, rate,
                        out_params);
   }
-  const int rc = launch_check("ransac_model kernels");
-  KCMC_TRY(workspace_free(ctx, ws, s));
-  return rc;
+  return launch_check("ransac_model kernels");
 }
