@@ -1,5 +1,6 @@
 // Context lifetime, error reporting and the RANSAC table upload of the kcmc C ABI.
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -69,6 +70,9 @@ extern "C" int kcmc_destroy(kcmc_ctx* ctx) {
     free_tables(ctx);
     for (auto& t : ctx->mhyp) free_model_tables(t);
     if (ctx->ws_pool) {
+      hipDeviceSynchronize();
+      for (auto& kv : ctx->stream_ws)
+        if (kv.second.ptr) hipFreeAsync(kv.second.ptr, kv.first);
       hipDeviceSynchronize();  // pending stream-ordered frees return to the pool first
       hipMemPoolDestroy(ctx->ws_pool);
     }
@@ -91,6 +95,16 @@ int workspace_alloc(kcmc_ctx* ctx, void** p, size_t bytes, hipStream_t s) {
     KCMC_TRY(hip_check(hipMemPoolSetAttribute(ctx->ws_pool, hipMemPoolAttrReleaseThreshold, &keep),
                        "hipMemPoolSetAttribute"));
   }
+  static const bool no_cache = getenv("KCMC_NO_STREAM_WS") != nullptr;  // A/B knob
+  if (!no_cache) {
+    std::lock_guard<std::mutex> lk(ctx->ws_mutex);
+    auto it = ctx->stream_ws.find(s);
+    if (it != ctx->stream_ws.end() && !it->second.busy && it->second.bytes >= bytes) {
+      it->second.busy = true;
+      *p = it->second.ptr;
+      return KCMC_OK;
+    }
+  }
   if (hipMallocFromPoolAsync(p, bytes, ctx->ws_pool, s) != hipSuccess) {
     hipGetLastError();
     return fail(KCMC_ENOMEM, "workspace: device out of memory (" + std::to_string(bytes) + " bytes)");
@@ -98,9 +112,22 @@ int workspace_alloc(kcmc_ctx* ctx, void** p, size_t bytes, hipStream_t s) {
   return KCMC_OK;
 }
 
-int workspace_free(kcmc_ctx* ctx, void* p, hipStream_t s) {
-  (void)ctx;
-  return hip_check(hipFreeAsync(p, s), "hipFreeAsync");
+int workspace_free(kcmc_ctx* ctx, void* p, hipStream_t s, size_t bytes) {
+  void* drop = p;
+  if (getenv("KCMC_NO_STREAM_WS") == nullptr) {
+    std::lock_guard<std::mutex> lk(ctx->ws_mutex);
+    kcmc_ctx::StreamScratch& c = ctx->stream_ws[s];
+    if (c.ptr == p) {  // the stream's cached block: keep it
+      c.busy = false;
+      return KCMC_OK;
+    }
+    if (!c.busy && bytes > c.bytes) {  // a larger block becomes the stream's cache
+      drop = c.ptr;
+      c.ptr = p;
+      c.bytes = bytes;
+    }
+  }
+  return drop ? hip_check(hipFreeAsync(drop, s), "hipFreeAsync") : KCMC_OK;
 }
 
 }  // namespace kcmc

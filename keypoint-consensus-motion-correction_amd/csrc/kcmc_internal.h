@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -38,6 +39,17 @@ struct kcmc_ctx {
   // Stream-ordered scratch (per-call workspaces, e.g. the warp's tile plans): a private
   // memory pool that keeps its pages between calls.
   hipMemPool_t ws_pool = nullptr;
+  // One cached workspace per stream, reused by the next call on that stream without
+  // touching the pool (stream order makes the reuse safe; a pool allocation while the
+  // previous warp still runs blocked the host for the rest of that warp).  Assumes a
+  // stream handle names one stream for the context's lifetime (torch's pooled streams).
+  struct StreamScratch {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    bool busy = false;
+  };
+  std::map<hipStream_t, StreamScratch> stream_ws;
+  std::mutex ws_mutex;
 };
 
 namespace kcmc {
@@ -53,7 +65,8 @@ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 // Stream-ordered workspace from the context's pool (valid for work enqueued on `s`
 // until workspace_free, which is itself stream-ordered).
 int workspace_alloc(kcmc_ctx* ctx, void** p, size_t bytes, hipStream_t s);
-int workspace_free(kcmc_ctx* ctx, void* p, hipStream_t s);
+// bytes > 0: the block may be kept as the stream's cached workspace (see kcmc_ctx).
+int workspace_free(kcmc_ctx* ctx, void* p, hipStream_t s, size_t bytes = 0);
 
 // VA:196-214 per frame on knn output (match.hip): reorder, ratio and displacement
 // filters, survivor bitmask, log counts.  Shared by the uint8 and float32 matchers.

@@ -972,7 +972,7 @@ extern "C" int kcmc_warp_perspective_u16(kcmc_ctx* ctx, const uint16_t* src, uin
       break;
   }
   const int rc = launch_check("warp_perspective_u16_kernel");
-  KCMC_TRY(workspace_free(ctx, ws, s));
+  KCMC_TRY(workspace_free(ctx, ws, s, wsb));
   return rc;
 }
 
@@ -1004,6 +1004,6 @@ extern "C" int kcmc_warp_affine_u16(kcmc_ctx* ctx, const uint16_t* src, uint16_t
       break;
   }
   const int rc = launch_check("warp_affine_u16_kernel");
-  KCMC_TRY(workspace_free(ctx, ws, s));
+  KCMC_TRY(workspace_free(ctx, ws, s, wsb));
   return rc;
 }

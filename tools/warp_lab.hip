@@ -14,7 +14,7 @@ int fail(int c, const std::string& m) { set_error(m); return c; }
 int hip_check(hipError_t e, const char* w) { if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", w, hipGetErrorString(e)); return KCMC_EHIP; } return 0; }
 int launch_check(const char* w) { return hip_check(hipGetLastError(), w); }
 int workspace_alloc(kcmc_ctx*, void**, size_t, hipStream_t) { return KCMC_EUNSUPPORTED; }
-int workspace_free(kcmc_ctx*, void*, hipStream_t) { return KCMC_EUNSUPPORTED; }
+int workspace_free(kcmc_ctx*, void*, hipStream_t, size_t) { return KCMC_EUNSUPPORTED; }
 }  // namespace kcmc
 // -DWARP_SRC='"path"' builds the lab against another version of warp.hip (A/B on one box)
 #ifndef WARP_SRC
