@@ -71,8 +71,10 @@ extern "C" int kcmc_destroy(kcmc_ctx* ctx) {
     for (auto& t : ctx->mhyp) free_model_tables(t);
     if (ctx->ws_pool) {
       hipDeviceSynchronize();
+      // the device is idle: free on the null stream (a cached block's own stream may
+      // already be gone when the context is destroyed at interpreter exit)
       for (auto& kv : ctx->stream_ws)
-        if (kv.second.ptr) hipFreeAsync(kv.second.ptr, kv.first);
+        if (kv.second.ptr) hipFreeAsync(kv.second.ptr, nullptr);
       hipDeviceSynchronize();  // pending stream-ordered frees return to the pool first
       hipMemPoolDestroy(ctx->ws_pool);
     }
