@@ -258,6 +258,34 @@ def test_warp_matches_oracle(dev, shape):
         assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], Ms[f])), f
 
 
+def test_warp_stream_workspace_reuse(dev):
+    """The per-stream cached workspace (kcmc_ctx::stream_ws): back-to-back warps of
+    growing and shrinking tile counts queued on two streams without host syncs (the
+    cache is reused in stream order, replaced by a larger block, never shared across
+    streams) give the same pixels as one warp at a time."""
+    rng = np.random.default_rng(21)
+    sizes = [(2, 270, 480), (6, 540, 960), (1, 135, 240), (4, 540, 960), (3, 1080, 1920)]
+    jobs = []
+    for F, H, W in sizes:
+        imgs = rng.integers(0, 65536, (F, H, W)).astype(np.uint16)
+        Ms = np.stack([synthetic.rigid(rng.normal(0, 0.01), rng.normal(0, 4), rng.normal(0, 4)) for _ in range(F)])
+        jobs.append((_t(imgs, dev), _t(Ms, dev)))
+    ref = [stages.warp_affine_u16(i, m).cpu() for i, m in jobs]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    outs = [torch.empty_like(i) for i, _ in jobs]
+    for rep in range(3):
+        for k, (i, m) in enumerate(jobs):
+            s = streams[(k + rep) % 2]
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                outs[k].zero_()
+                stages.warp_affine_u16(i, m, out=outs[k])
+            torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        for k in range(len(jobs)):
+            assert torch.equal(outs[k].cpu(), ref[k]), (rep, k)
+
+
 @pytest.mark.parametrize("values", ["14bit", "hot", "blobs", "edge16384", "dense_hot", "bright_lines"])
 def test_warp_fast_path_value_ranges(dev, values):
     # the fixed-pitch staged path picks its blend per tile: exact integer for boxes below
