@@ -23,8 +23,14 @@
  *     owned by the caller (e.g. torch ROCm tensors' data_ptr()); *_host are host
  *     pointers.  The library never frees caller memory.
  *   - Launch entry points are asynchronous on `stream` (a hipStream_t; NULL = the
- *     null stream), perform no allocation and no synchronisation, and are therefore
- *     capturable into a hipGraph.  kcmc_ransac_prepare allocates and synchronises.
+ *     null stream) and perform no synchronisation.  The warp, float-matcher and
+ *     detector entry points take a per-call workspace from the context's private
+ *     stream-ordered memory pool (hipMallocFromPoolAsync / hipFreeAsync on `stream`);
+ *     outside stream capture one block per stream is kept and reused in stream order.
+ *     Under hipGraph capture the workspace is the graph's own allocation node (never
+ *     the per-stream block), so the launches are capturable and a replay never touches
+ *     memory that later eager calls may free.  kcmc_ransac_prepare allocates and
+ *     synchronises.
  *   - Return value: KCMC_OK (0) or an error code; kcmc_last_error() returns the
  *     calling thread's last message.  Per-frame model failure is NOT an error: it is
  *     NaN in the output parameters, as in the reference (VA:321-322).

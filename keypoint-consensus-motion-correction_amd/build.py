@@ -49,8 +49,13 @@ def up_to_date() -> bool:
     return os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= _newest_input_mtime()
 
 
+# Per-source flags.  match.hip: MFMA results in VGPRs (the K1 epilogue reads every
+# accumulator once; the AGPR form added a v_accvgpr_read per distance).
+EXTRA_FLAGS = {"match.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def _compile(src: str, obj: str) -> None:
-    cmd = [hipcc(), *COMMON_FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+    cmd = [hipcc(), *COMMON_FLAGS, *EXTRA_FLAGS.get(src, []), "-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

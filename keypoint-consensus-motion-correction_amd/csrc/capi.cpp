@@ -86,27 +86,49 @@ extern "C" int kcmc_destroy(kcmc_ctx* ctx) {
 
 namespace kcmc {
 
-int workspace_alloc(kcmc_ctx* ctx, void** p, size_t bytes, hipStream_t s) {
-  if (!ctx->ws_pool) {
-    hipMemPoolProps props = {};
-    props.allocType = hipMemAllocationTypePinned;
-    props.location.type = hipMemLocationTypeDevice;
-    props.location.id = ctx->device;
-    KCMC_TRY(hip_check(hipMemPoolCreate(&ctx->ws_pool, &props), "hipMemPoolCreate"));
-    uint64_t keep = UINT64_MAX;  // never trim: the same sizes come back every call
-    KCMC_TRY(hip_check(hipMemPoolSetAttribute(ctx->ws_pool, hipMemPoolAttrReleaseThreshold, &keep),
-                       "hipMemPoolSetAttribute"));
+// KCMC_NO_STREAM_WS (A/B knob) is read once, for both workspace_alloc and workspace_free.
+static bool ws_cache_enabled() {
+  static const bool on = getenv("KCMC_NO_STREAM_WS") == nullptr;
+  return on;
+}
+
+// The per-stream cache is used only on a stream that names one ordered queue and is not
+// being captured: a block baked into a hipGraph must never be swapped or freed by later
+// eager calls, and hipStreamPerThread is one handle shared by every thread's stream.
+static bool cacheable_stream(hipStream_t s) {
+  if (!ws_cache_enabled() || s == hipStreamPerThread) return false;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+    hipGetLastError();
+    return false;
   }
-  static const bool no_cache = getenv("KCMC_NO_STREAM_WS") != nullptr;  // A/B knob
-  if (!no_cache) {
+  return st == hipStreamCaptureStatusNone;
+}
+
+int workspace_alloc(kcmc_ctx* ctx, void** p, size_t bytes, hipStream_t s) {
+  const bool cacheable = cacheable_stream(s);
+  {
     std::lock_guard<std::mutex> lk(ctx->ws_mutex);
-    auto it = ctx->stream_ws.find(s);
-    if (it != ctx->stream_ws.end() && !it->second.busy && it->second.bytes >= bytes) {
-      it->second.busy = true;
-      *p = it->second.ptr;
-      return KCMC_OK;
+    if (!ctx->ws_pool) {
+      hipMemPoolProps props = {};
+      props.allocType = hipMemAllocationTypePinned;
+      props.location.type = hipMemLocationTypeDevice;
+      props.location.id = ctx->device;
+      KCMC_TRY(hip_check(hipMemPoolCreate(&ctx->ws_pool, &props), "hipMemPoolCreate"));
+      uint64_t keep = UINT64_MAX;  // never trim: the same sizes come back every call
+      KCMC_TRY(hip_check(hipMemPoolSetAttribute(ctx->ws_pool, hipMemPoolAttrReleaseThreshold, &keep),
+                         "hipMemPoolSetAttribute"));
+    }
+    if (cacheable) {
+      auto it = ctx->stream_ws.find(s);
+      if (it != ctx->stream_ws.end() && !it->second.busy && it->second.bytes >= bytes) {
+        it->second.busy = true;
+        *p = it->second.ptr;
+        return KCMC_OK;
+      }
     }
   }
+  // a stream-ordered pool allocation (under capture: the graph's own allocation node)
   if (hipMallocFromPoolAsync(p, bytes, ctx->ws_pool, s) != hipSuccess) {
     hipGetLastError();
     return fail(KCMC_ENOMEM, "workspace: device out of memory (" + std::to_string(bytes) + " bytes)");
@@ -116,7 +138,7 @@ int workspace_alloc(kcmc_ctx* ctx, void** p, size_t bytes, hipStream_t s) {
 
 int workspace_free(kcmc_ctx* ctx, void* p, hipStream_t s, size_t bytes) {
   void* drop = p;
-  if (getenv("KCMC_NO_STREAM_WS") == nullptr) {
+  if (cacheable_stream(s)) {
     std::lock_guard<std::mutex> lk(ctx->ws_mutex);
     kcmc_ctx::StreamScratch& c = ctx->stream_ws[s];
     if (c.ptr == p) {  // the stream's cached block: keep it

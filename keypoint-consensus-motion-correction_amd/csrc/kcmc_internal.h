@@ -42,7 +42,8 @@ struct kcmc_ctx {
   // One cached workspace per stream, reused by the next call on that stream without
   // touching the pool (stream order makes the reuse safe; a pool allocation while the
   // previous warp still runs blocked the host for the rest of that warp).  Assumes a
-  // stream handle names one stream for the context's lifetime (torch's pooled streams).
+  // stream handle names one stream for the context's lifetime (torch's pooled streams);
+  // never used for hipStreamPerThread or a capturing stream (capi.cpp cacheable_stream).
   struct StreamScratch {
     void* ptr = nullptr;
     size_t bytes = 0;

@@ -7,20 +7,24 @@
 //   The distance is an exact integer contraction, so it runs on the int8 matrix
 //   cores.  With x = a - 128 (template) and y = 127 - b (frame), both int8,
 //   a - b = x + y + 1, so SSD = T + Q + 2 x.y with T = sum(x^2 + 2x) + D per template
-//   row and Q = sum(y^2 + 2y) per frame row.  v_mfma_i32_32x32x32_i8 runs the K loop
-//   twice over the same fragments with the accumulator initialised to T, so it
-//   returns T + 2 x.y directly.  A operand = 32 frame descriptors (rows j), B operand
-//   = 32 template descriptors (columns i): each lane owns one template column and 16
-//   frame rows of the 32x32 tile and keeps a running top-2 in registers.
-//   The top-2 runs on 32-bit keys (ssd << 8 | j - q0) local to a 256-row chunk of
-//   frame descriptors (ssd <= 64 * 255^2 < 2^22): for D <= 64 bytes sqrtf is strictly
-//   increasing on the integer SSD range, so integer keys order exactly
-//   like OpenCV's float distances, and the low bits make ties go to the lower frame
-//   index like OpenCV's K-insertion.  3 VALU ops per distance after the accumulator
-//   read: key = acc << 8 + qk (v_lshl_add), b2 = med3(b1, b2, key), b1 = min(b1, key).
-//   Each chunk's top-2 is merged into a 64-bit (ssd << 32 | j) top-2.  Frame
-//   descriptors are staged through LDS (converted to int8, zero-padded to DP, rows
-//   padded by 16 B so the ds_read_b128 fragment reads are bank-conflict free).
+//   row and Q = sum(y^2 + 2y) per frame row.  One v_mfma_i32_32x32x32_i8 pass per
+//   32-deep k-step gives x.y (accumulator from zero).  T is constant along a template
+//   column, so a column's frame rows are ordered by SSD - T + B = Q + 2 x.y + B, with
+//   B = 2^20 > max T making it non-negative (< 2^23).  A operand = 32 frame
+//   descriptors (rows j), B operand = 32 template descriptors (columns i): each lane
+//   owns one template column and 16 frame rows of the 32x32 tile and keeps a running
+//   top-2 in registers.
+//   The top-2 runs on 32-bit keys ((SSD - T + B) << 8 | j - q0) local to a 256-row
+//   chunk of frame descriptors: for D <= 64 bytes sqrtf is strictly increasing on the
+//   integer SSD range, so integer keys order exactly like OpenCV's float
+//   distances, and the low bits make ties go to the lower frame index like OpenCV's
+//   K-insertion.  3 VALU ops per distance: key = acc << 9 + qk (v_lshl_add, qk =
+//   (Q + B) << 8 | j - q0 from LDS), b2 = med3(b1, b2, key), b1 = min(b1, key), on two
+//   independent top-2 pairs per column (even / odd accumulator) so that consecutive
+//   distances do not wait on each other.  Each chunk's top-2 is merged into a 64-bit
+//   (ssd << 32 | j) top-2 with SSD = (key >> 8) + T - B.  Frame descriptors are staged
+//   through LDS (converted to int8, zero-padded to DP, rows padded by 16 B so the
+//   ds_read_b128 fragment reads are bank-conflict free).
 //
 // match_filter_kernel -- one workgroup per frame: VA:196-214 in float64 with the
 //   reference's exact operation order (no FMA contraction; file built with
@@ -40,8 +44,9 @@ constexpr int kThreads = 256;
 constexpr int kBlocksPerWave = 2;                         // 32-row template blocks per wave
 constexpr int kTplPerWG = (kThreads / 64) * kBlocksPerWave * 32;  // 256
 constexpr int kQChunk = 256;                              // frame descriptors per LDS chunk (8-bit local index)
-constexpr uint32_t kNoKey = 0xffffffffu;                  // chunk keys of real rows are < 2^30
-constexpr uint32_t kPad = 0xc0000000u;                    // key base of the padding rows of a tile
+constexpr uint32_t kNoKey = 0xffffffffu;                  // chunk keys of real rows are < 2^31
+constexpr uint32_t kPad = 0xc0000000u;                    // key of the padding rows of a tile (acc = 0)
+constexpr int kBias = 1 << 20;                            // B > max T = 16129 * 64
 constexpr unsigned long long kNoKey64 = ~0ull;
 
 __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
@@ -80,86 +85,106 @@ __device__ __forceinline__ int sq2(uint32_t w, int acc) {
   return __builtin_amdgcn_sdot4((int)w, 0x02020202, acc, false);
 }
 
-// Chunk staging of 16-byte pieces (D % 16 == 0): PPR pieces per padded row, KP per
-// thread.  Loads are branch-free (row clamped to the frame's last row, piece clamped to
-// the descriptor), so that all of a thread's loads are in flight together; out-of-range
-// pieces are zeroed when they land.
+// Chunk staging, one frame descriptor row per thread (row q0 + tid of a 256-row chunk).
+// The row's bytes come as 16-byte loads at offsets 0, 16, ... and the last one at D - 16,
+// so that every load lies inside the row (no read past the descriptor buffer; rows are
+// not 16-byte aligned unless D % 16 == 0); the loads of the next chunk are issued before
+// the current chunk's MFMA tiles so that their latency hides behind them.  Landing turns
+// them into the padded int8 row (127 - b, zero past D), its key part (Q + B) << 8 | row
+// and the LDS writes, all in registers.
 template <int DP>
-struct Pieces {
-  static constexpr int kPPR = DP / 16;
-  static constexpr int kKP = kQChunk * kPPR / kThreads;
+struct RowPieces {
+  static constexpr int kNP = DP / 16;
 };
 
+__device__ __forceinline__ uint4 load16(const uint8_t* p) {
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);  // global_load_dwordx4 (unaligned access is allowed for global memory)
+  return v;
+}
+
 template <int DP>
-__device__ __forceinline__ void issue_pieces(const uint8_t* __restrict__ rows0, int D, int last, int tid,
-                                             uint4 (&pf)[Pieces<DP>::kKP]) {
+__device__ __forceinline__ void issue_row(const uint8_t* __restrict__ row, int D, uint4 (&pf)[RowPieces<DP>::kNP]) {
+  if (D >= 16) {
 #pragma unroll
-  for (int it = 0; it < Pieces<DP>::kKP; ++it) {
-    const int e = tid + kThreads * it;
-    const int r = min(e / Pieces<DP>::kPPR, last), pc = min(e % Pieces<DP>::kPPR, D / 16 - 1);
-    pf[it] = *reinterpret_cast<const uint4*>(rows0 + (size_t)r * D + 16 * pc);
+    for (int k = 0; k < RowPieces<DP>::kNP; ++k) pf[k] = load16(row + min(16 * k, D - 16));
+  } else {  // short descriptors (D < 16): byte loads of piece 0
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (int c = 0; c < D; ++c) w[c >> 2] |= (uint32_t)row[c] << (8 * (c & 3));
+    pf[0] = make_uint4(w[0], w[1], w[2], w[3]);
+#pragma unroll
+    for (int k = 1; k < RowPieces<DP>::kNP; ++k) pf[k] = make_uint4(0u, 0u, 0u, 0u);
   }
+}
+
+// 16 bytes >> 8 * sh (0 <= sh < 16, uniform), zero-filled from the top.
+__device__ __forceinline__ uint4 shr_bytes(uint4 v, int sh) {
+  uint32_t w[8] = {v.x, v.y, v.z, v.w, 0u, 0u, 0u, 0u};
+  const int ws = sh >> 2;
+  const uint32_t bs = (uint32_t)(sh & 3);
+  uint32_t o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint32_t lo = w[i], hi = w[i + 1];
+    // uniform word shift by selects (no indexed registers)
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+      if (ws == k) {
+        lo = w[i + k];
+        hi = w[i + k + 1];
+      }
+    o[i] = __builtin_amdgcn_alignbyte(hi, lo, bs);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 template <int DP, int ROWB>
-__device__ __forceinline__ void land_pieces(uint8_t* qbuf, int D, int cnt, int tid,
-                                            const uint4 (&pf)[Pieces<DP>::kKP]) {
+__device__ __forceinline__ void land_row(uint8_t* qrow, uint32_t* qk, int r, bool real, int D,
+                                         const uint4 (&pf)[RowPieces<DP>::kNP]) {
+  constexpr int NP = RowPieces<DP>::kNP;
+  const int np = D >= 16 ? (D + 15) >> 4 : 1;  // pieces holding the row (uniform)
+  uint4 w[NP];
 #pragma unroll
-  for (int it = 0; it < Pieces<DP>::kKP; ++it) {
-    const int e = tid + kThreads * it;
-    const int r = e / Pieces<DP>::kPPR, pc = e % Pieces<DP>::kPPR;
-    uint4 w = pf[it];
-    w.x ^= 0x7f7f7f7fu;  // int8 127 - b
-    w.y ^= 0x7f7f7f7fu;
-    w.z ^= 0x7f7f7f7fu;
-    w.w ^= 0x7f7f7f7fu;
-    if (r >= cnt || 16 * pc >= D) w = make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint4*>(&qbuf[r * ROWB + 16 * pc]) = w;
+  for (int k = 0; k < NP; ++k) {
+    uint4 v = pf[k];
+    v.x ^= 0x7f7f7f7fu;  // int8 127 - b
+    v.y ^= 0x7f7f7f7fu;
+    v.z ^= 0x7f7f7f7fu;
+    v.w ^= 0x7f7f7f7fu;
+    if (D < 16) {  // zero past D (xor made the zero bytes 0x7f)
+      const uint32_t m[4] = {D >= 4 ? ~0u : (1u << (8 * D)) - 1u, D >= 8 ? ~0u : D <= 4 ? 0u : (1u << (8 * (D - 4))) - 1u,
+                             D >= 12 ? ~0u : D <= 8 ? 0u : (1u << (8 * (D - 8))) - 1u,
+                             D <= 12 ? 0u : (1u << (8 * (D - 12))) - 1u};
+      if (k == 0) v = make_uint4(v.x & m[0], v.y & m[1], v.z & m[2], v.w & m[3]);
+    } else if (k == np - 1) {
+      v = shr_bytes(v, 16 * np - D);  // the last piece was loaded at D - 16
+    }
+    if (k >= np || !real) v = make_uint4(0u, 0u, 0u, 0u);
+    w[k] = v;
   }
-}
-
-// Chunk staging for any D (not a multiple of 16): the chunk's rows are one contiguous
-// byte range [start, start + cnt * D) of des_q, loaded as 16-byte pieces aligned down from
-// start (an aligned piece that begins inside the range never crosses a page the range
-// does not touch) into a raw LDS buffer, all of a thread's loads in flight together; the
-// padded int8 rows are then cut from it with two aligned LDS words + v_alignbyte per word.
-template <int DP>
-struct RawChunk {
-  static constexpr int kPieces = (kQChunk * DP + 16 + 15) / 16;          // pieces of one chunk
-  static constexpr int kKP = (kPieces + kThreads - 1) / kThreads;        // per thread
-  static constexpr int kWords = kKP * kThreads * 4 + 4;                  // raw LDS words
-};
-
-template <int DP>
-__device__ __forceinline__ void issue_raw(const uint8_t* __restrict__ start, int nbytes, int tid,
-                                          uint4 (&pf)[RawChunk<DP>::kKP]) {
-  const uint4* a = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(start) & ~(uintptr_t)15);
-  const int delta = (int)(reinterpret_cast<uintptr_t>(start) & 15);
-  const int np = (nbytes + delta + 15) >> 4;  // pieces overlapping the range
+  int nb = kBias;
 #pragma unroll
-  for (int it = 0; it < RawChunk<DP>::kKP; ++it) {
-    const int k = tid + kThreads * it;
-    pf[it] = make_uint4(0u, 0u, 0u, 0u);
-    if (k < np) pf[it] = a[k];
+  for (int k = 0; k < NP; ++k) {
+    nb = sq2(w[k].x, nb);
+    nb = sq2(w[k].y, nb);
+    nb = sq2(w[k].z, nb);
+    nb = sq2(w[k].w, nb);
+    *reinterpret_cast<uint4*>(qrow + 16 * k) = w[k];
   }
+  // padding rows of the last tile (zero descriptors, so acc = 0) get the key kPad
+  *qk = real ? (((uint32_t)nb << 8) | (uint32_t)r) : kPad;
 }
 
 template <int DP>
-__device__ __forceinline__ void land_raw(uint32_t* qraw, int tid, const uint4 (&pf)[RawChunk<DP>::kKP]) {
-#pragma unroll
-  for (int it = 0; it < RawChunk<DP>::kKP; ++it)
-    reinterpret_cast<uint4*>(qraw)[tid + kThreads * it] = pf[it];
-}
-
-template <int DP, bool VEC16>
 __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
     const uint8_t* __restrict__ des_tpl, int n_tpl, int D, const uint8_t* __restrict__ des_q,
     const int32_t* __restrict__ q_off, int32_t* __restrict__ out_idx, float* __restrict__ out_dist) {
   constexpr int KSTEPS = DP / 32;
   constexpr int ROWB = DP + 16;  // padded LDS row stride (bytes)
-  __shared__ __attribute__((aligned(16))) uint8_t qbuf[kQChunk * ROWB];
-  __shared__ uint32_t qkey[kQChunk];
-  __shared__ __attribute__((aligned(16))) uint32_t qraw[VEC16 ? 4 : RawChunk<DP>::kWords];
+  // double-buffered chunks: one barrier per chunk (a wave writes chunk c + 1 only after
+  // every wave has passed the barrier of chunk c, i.e. finished chunk c - 1)
+  __shared__ __attribute__((aligned(16))) uint8_t qbuf[2][kQChunk * ROWB];
+  __shared__ __attribute__((aligned(16))) uint32_t qkey[2][kQChunk];
 
   const int f = blockIdx.y;
   const int tid = threadIdx.x;
@@ -169,6 +194,7 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
   const int h = lane >> 5;   // k-half of the fragment / row group of the output
   const int q_begin = q_off[f];
   const int n_q = q_off[f + 1] - q_begin;
+  const uint8_t* qrows = des_q + (size_t)q_begin * D;
 
   // ---- template fragments (B operand) and T = sum(x^2 + 2x) + D, kept in registers
   v4i bfrag[kBlocksPerWave][KSTEPS];
@@ -199,96 +225,53 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
 #pragma unroll
   for (int b = 0; b < kBlocksPerWave; ++b) g1[b] = g2[b] = kNoKey64;
 
-  // VEC16 (D % 16 == 0): the next chunk's loads are issued before the current chunk's
-  // MFMA tiles, so their latency hides behind them
-  uint4 pf[Pieces<DP>::kKP];
-  uint4 rf[VEC16 ? 1 : RawChunk<DP>::kKP];
-  if constexpr (VEC16) {
-    if (n_q > 0) issue_pieces<DP>(des_q + (size_t)q_begin * D, D, n_q - 1, tid, pf);
-  } else {
-    if (n_q > 0) issue_raw<DP>(des_q + (size_t)q_begin * D, min(kQChunk, n_q) * D, tid, rf);
-  }
-  for (int q0 = 0; q0 < n_q; q0 += kQChunk) {
+  uint4 pf[RowPieces<DP>::kNP];
+  if (n_q > 0) issue_row<DP>(qrows + (size_t)min(tid, n_q - 1) * D, D, pf);
+  for (int q0 = 0, buf = 0; q0 < n_q; q0 += kQChunk, buf ^= 1) {
     const int cnt = min(kQChunk, n_q - q0);
     const int rows = (cnt + 31) & ~31;
-    __syncthreads();  // previous chunk fully consumed
     // ---- stage frame descriptors [q0, q0+cnt) as int8 127 - b, zero-padded to DP columns
-    const uint8_t* base = des_q + (size_t)(q_begin + q0) * D;
-    if constexpr (VEC16) {
-      land_pieces<DP, ROWB>(qbuf, D, cnt, tid, pf);
-    } else {
-      land_raw<DP>(qraw, tid, rf);
-      __syncthreads();
-      const int delta = (int)(reinterpret_cast<uintptr_t>(base) & 15);
-      for (int e = tid; e < rows * (DP / 4); e += kThreads) {
-        const int r = e / (DP / 4);
-        const int col = (e % (DP / 4)) * 4;
-        uint32_t w = 0;
-        if (r < cnt && col < D) {
-          const int o = r * D + col + delta;  // byte offset in the raw buffer
-          const uint32_t lo = qraw[o >> 2], hi = qraw[(o >> 2) + 1];
-          w = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(o & 3)) ^ 0x7f7f7f7fu;
-          if (col + 4 > D) w &= (1u << (8 * (D - col))) - 1u;  // zero past D (int8 padding)
-        }
-        *reinterpret_cast<uint32_t*>(&qbuf[r * ROWB + col]) = w;
-      }
-    }
+    if (tid < rows) land_row<DP, ROWB>(&qbuf[buf][tid * ROWB], &qkey[buf][tid], tid, tid < cnt, D, pf);
     __syncthreads();
-    if constexpr (VEC16) {
-      if (q0 + kQChunk < n_q) issue_pieces<DP>(base + (size_t)kQChunk * D, D, n_q - 1 - q0 - kQChunk, tid, pf);
-    } else {
-      if (q0 + kQChunk < n_q)
-        issue_raw<DP>(base + (size_t)kQChunk * D, min(kQChunk, n_q - q0 - kQChunk) * D, tid, rf);
-    }
-    // ---- per-row key part: Q << 8 | (j - q0)  (Q >= -D may be negative: modular)
-    for (int r = tid; r < rows; r += kThreads) {
-      int nb = 0;
-      const uint32_t* rw = reinterpret_cast<const uint32_t*>(&qbuf[r * ROWB]);
+    if (q0 + kQChunk < n_q)
+      issue_row<DP>(qrows + (size_t)(q0 + kQChunk + min(tid, n_q - q0 - kQChunk - 1)) * D, D, pf);
+    const uint8_t* qb = qbuf[buf];
+    const uint32_t* qkb = qkey[buf];
+    uint32_t b1[kBlocksPerWave][2], b2[kBlocksPerWave][2];  // [even | odd accumulator]
 #pragma unroll
-      for (int d = 0; d < DP / 4; ++d) nb = sq2(rw[d], nb);
-      // rows past cnt (zero descriptors, so acc = T < 2^21) get keys in [kPad, kPad + 2^29)
-      qkey[r] = r < cnt ? (((uint32_t)nb << 8) | (uint32_t)r) : kPad;
-    }
-    __syncthreads();
-    uint32_t b1[kBlocksPerWave], b2[kBlocksPerWave];
-#pragma unroll
-    for (int b = 0; b < kBlocksPerWave; ++b) b1[b] = b2[b] = kNoKey;
+    for (int b = 0; b < kBlocksPerWave; ++b) b1[b][0] = b2[b][0] = b1[b][1] = b2[b][1] = kNoKey;
     // ---- MFMA tiles of 32 frame rows
     for (int t0 = 0; t0 < rows; t0 += 32) {
       v4i afrag[KSTEPS];
 #pragma unroll
       for (int kk = 0; kk < KSTEPS; ++kk)
-        afrag[kk] = *reinterpret_cast<const v4i*>(&qbuf[(t0 + c) * ROWB + 32 * kk + 16 * h]);
+        afrag[kk] = *reinterpret_cast<const v4i*>(&qb[(t0 + c) * ROWB + 32 * kk + 16 * h]);
       // rows of this lane's 16 accumulators: t0 + (r&3) + 8*(r>>2) + 4*h
       uint32_t qk[16];
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) qk[4 * g + s] = qkey[t0 + 8 * g + 4 * h + s];
+        for (int s = 0; s < 4; ++s) qk[4 * g + s] = qkb[t0 + 8 * g + 4 * h + s];
 #pragma unroll
       for (int b = 0; b < kBlocksPerWave; ++b) {
-        v16i acc;
+        v16i acc = {};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = tk[b];
+        for (int kk = 0; kk < KSTEPS; ++kk)  // acc = x.y
+          acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag[kk], bfrag[b][kk], acc, 0, 0, 0);
 #pragma unroll
-        for (int rep = 0; rep < 2; ++rep)  // acc = T + 2 x.y
-#pragma unroll
-          for (int kk = 0; kk < KSTEPS; ++kk)
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag[kk], bfrag[b][kk], acc, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          top2_insert(b1[b], b2[b], ((uint32_t)acc[r] << 8) + qk[r]);
-        }
+        for (int r = 0; r < 16; ++r) top2_insert(b1[b][r & 1], b2[b][r & 1], ((uint32_t)acc[r] << 9) + qk[r]);
       }
     }
     // ---- fold the chunk's top-2 (local indices) into the frame's 64-bit top-2
 #pragma unroll
     for (int b = 0; b < kBlocksPerWave; ++b) {
-      const uint32_t ks[2] = {b1[b], b2[b]};
+      const uint32_t ks[4] = {b1[b][0], b2[b][0], b1[b][1], b2[b][1]};
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
-        if (ks[k] < kPad)
-          top2_insert64(g1[b], g2[b], ((unsigned long long)(ks[k] >> 8) << 32) | (uint32_t)(q0 + (int)(ks[k] & 255u)));
+      for (int k = 0; k < 4; ++k)
+        if (ks[k] < kPad) {
+          const uint32_t ssd = (ks[k] >> 8) + (uint32_t)(tk[b] - kBias);
+          top2_insert64(g1[b], g2[b], ((unsigned long long)ssd << 32) | (uint32_t)(q0 + (int)(ks[k] & 255u)));
+        }
     }
   }
 
@@ -423,15 +406,10 @@ int launch_knn(const uint8_t* des_tpl, int n_tpl, int D, const uint8_t* des_q, c
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
   (void)max_nq;
   dim3 grid(ceil_div(n_tpl, kTplPerWG), n_frames);
-  const bool vec16 = (D & 15) == 0;
-  if (D <= 32 && vec16)
-    hipLaunchKernelGGL((knn2_l2u8_kernel<32, true>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
-  else if (D <= 32)
-    hipLaunchKernelGGL((knn2_l2u8_kernel<32, false>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
-  else if (vec16)
-    hipLaunchKernelGGL((knn2_l2u8_kernel<64, true>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+  if (D <= 32)
+    hipLaunchKernelGGL((knn2_l2u8_kernel<32>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
   else
-    hipLaunchKernelGGL((knn2_l2u8_kernel<64, false>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+    hipLaunchKernelGGL((knn2_l2u8_kernel<64>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
   return launch_check("knn2_l2u8_kernel");
 }
 

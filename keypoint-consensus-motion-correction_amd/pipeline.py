@@ -222,6 +222,11 @@ class OverlappedSlabs:
 
     def __init__(self, device, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
                  counts: Optional[List[int]] = None, group=None):
+        if counts is not None and len(counts) > 1 and cfg.frame_downsample_rate != 1:
+            # the rank's first frame is counted in sample frames, the affines in full-rate
+            # frames: the same restriction as distributed.align_sharded
+            raise ValueError("the sharded path requires frame_downsample_rate == 1 "
+                             "(frame_rate < 2*FRAME_SAMPLE_RATE)")
         self.dev = torch.device(device)
         self.cfg = cfg
         self.logger = logger

@@ -272,18 +272,53 @@ def test_warp_stream_workspace_reuse(dev):
         jobs.append((_t(imgs, dev), _t(Ms, dev)))
     ref = [stages.warp_affine_u16(i, m).cpu() for i, m in jobs]
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
-    outs = [torch.empty_like(i) for i, _ in jobs]
+    # every (rep, job) has its own output: the two streams run concurrently with no
+    # cross-stream waits between jobs, so a cache shared across streams would race
+    outs = [[torch.zeros_like(i) for i, _ in jobs] for _ in range(3)]
+    cur = torch.cuda.current_stream(dev)
+    for s in streams:
+        s.wait_stream(cur)
     for rep in range(3):
         for k, (i, m) in enumerate(jobs):
             s = streams[(k + rep) % 2]
-            s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(s):
-                outs[k].zero_()
-                stages.warp_affine_u16(i, m, out=outs[k])
-            torch.cuda.current_stream(dev).wait_stream(s)
-        torch.cuda.synchronize(dev)
+                stages.warp_affine_u16(i, m, out=outs[rep][k])
+    for s in streams:
+        cur.wait_stream(s)
+    torch.cuda.synchronize(dev)
+    for rep in range(3):
         for k in range(len(jobs)):
-            assert torch.equal(outs[k].cpu(), ref[k]), (rep, k)
+            assert torch.equal(outs[rep][k].cpu(), ref[k]), (rep, k)
+
+
+def test_warp_graph_capture_replay_after_larger_eager_warp(dev):
+    """A warp captured into a hipGraph owns its workspace: replaying the graph after a
+    larger eager warp on the same stream (which replaces that stream's cached block)
+    still gives the captured warp's pixels."""
+    rng = np.random.default_rng(23)
+    small = _t(rng.integers(0, 65536, (2, 270, 480)).astype(np.uint16), dev)
+    big = _t(rng.integers(0, 65536, (3, 1080, 1920)).astype(np.uint16), dev)
+    Ms = _t(np.stack([synthetic.rigid(0.01, 2.5, -1.5), synthetic.rigid(-0.02, -3.0, 4.0)]), dev)
+    Mb = _t(np.stack([synthetic.rigid(0.005 * k, 1.0 + k, -2.0) for k in range(3)]), dev)
+    ref_small = stages.warp_affine_u16(small, Ms).cpu()
+    ref_big = stages.warp_affine_u16(big, Mb).cpu()
+    out_small = torch.zeros_like(small)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        stages.warp_affine_u16(small, Ms, out=out_small)  # eager warm-up: the stream's cached block
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        stages.warp_affine_u16(small, Ms, out=out_small)
+    out_big = torch.zeros_like(big)
+    with torch.cuda.stream(s):
+        stages.warp_affine_u16(big, Mb, out=out_big)  # a larger block replaces the cache
+        out_small.zero_()
+        g.replay()
+    torch.cuda.synchronize(dev)
+    assert torch.equal(out_big.cpu(), ref_big)
+    assert torch.equal(out_small.cpu(), ref_small)
 
 
 @pytest.mark.parametrize("values", ["14bit", "hot", "blobs", "edge16384", "dense_hot", "bright_lines"])
