@@ -97,7 +97,9 @@ _SIGNATURES = {
 
 
 def lib_path() -> str:
-    return _build.LIB_PATH
+    # KCMC_LIB_PATH: an alternative build of the same library (same-box A/B runs of
+    # tools/*_rates.py); the package's own in-tree libkcmc.so otherwise
+    return os.environ.get("KCMC_LIB_PATH") or _build.LIB_PATH
 
 
 def load(auto_build: bool = True) -> ctypes.CDLL:
@@ -107,7 +109,7 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         if _lib is not None:
             return _lib
         path = lib_path()
-        if auto_build and os.environ.get("KCMC_NO_BUILD", "0") != "1":
+        if auto_build and os.environ.get("KCMC_NO_BUILD", "0") != "1" and not os.environ.get("KCMC_LIB_PATH"):
             try:
                 if not _build.up_to_date():
                     _build.build()

@@ -63,6 +63,14 @@ int launch_check(const char* what);
 
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
+// XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (speed only, never
+// relied on for correctness), so give each XCD a contiguous run of ids (bijective also
+// when n % 8 != 0): neighbouring tiles that share input then share one XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
+  const int q8 = n >> 3, r8 = n & 7, xcd = bid & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
 // Stream-ordered workspace from the context's pool (valid for work enqueued on `s`
 // until workspace_free, which is itself stream-ordered).
 int workspace_alloc(kcmc_ctx* ctx, void** p, size_t bytes, hipStream_t s);

@@ -40,9 +40,12 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr int kThreads = 256;
 constexpr int kBlocksPerWave = 2;                         // 32-row template blocks per wave
-constexpr int kTplPerWG = (kThreads / 64) * kBlocksPerWave * 32;  // 256
+template <int WAVES>
+struct KnnShape {
+  static constexpr int kThreads = 64 * WAVES;
+  static constexpr int kTplPerWG = WAVES * kBlocksPerWave * 32;  // template rows per workgroup
+};
 constexpr int kQChunk = 256;                              // frame descriptors per LDS chunk (8-bit local index)
 constexpr uint32_t kNoKey = 0xffffffffu;                  // chunk keys of real rows are < 2^31
 constexpr uint32_t kPad = 0xc0000000u;                    // key of the padding rows of a tile (acc = 0)
@@ -85,13 +88,14 @@ __device__ __forceinline__ int sq2(uint32_t w, int acc) {
   return __builtin_amdgcn_sdot4((int)w, 0x02020202, acc, false);
 }
 
-// Chunk staging, one frame descriptor row per thread (row q0 + tid of a 256-row chunk).
-// The row's bytes come as 16-byte loads at offsets 0, 16, ... and the last one at D - 16,
-// so that every load lies inside the row (no read past the descriptor buffer; rows are
-// not 16-byte aligned unless D % 16 == 0); the loads of the next chunk are issued before
-// the current chunk's MFMA tiles so that their latency hides behind them.  Landing turns
-// them into the padded int8 row (127 - b, zero past D), its key part (Q + B) << 8 | row
-// and the LDS writes, all in registers.
+// Chunk staging, one frame descriptor row per thread (row q0 + tid of a 256-row chunk):
+// 16-byte loads at offsets 0, 16, ... of the row (rows are not 16-byte aligned unless
+// D % 16 == 0; unaligned global loads are allowed), the last one running up to 15 bytes
+// into the next row (masked off when landing).  Only the very last row of des_q would run
+// past the buffer: its tail is read bytewise.  The loads of the next chunk are issued
+// before the current chunk's MFMA tiles so that their latency hides behind them.
+// Landing turns them into the padded int8 row (127 - b, zero past D), its key part
+// (Q + B) << 8 | row and the LDS writes, all in registers.
 template <int DP>
 struct RowPieces {
   static constexpr int kNP = DP / 16;
@@ -104,79 +108,56 @@ __device__ __forceinline__ uint4 load16(const uint8_t* p) {
 }
 
 template <int DP>
-__device__ __forceinline__ void issue_row(const uint8_t* __restrict__ row, int D, uint4 (&pf)[RowPieces<DP>::kNP]) {
-  if (D >= 16) {
+__device__ __forceinline__ void issue_row(const uint8_t* __restrict__ row, int D, bool last_row,
+                                          uint4 (&pf)[RowPieces<DP>::kNP]) {
+  constexpr int NP = RowPieces<DP>::kNP;
+  const int np = (D + 15) >> 4;  // pieces holding the row (uniform)
 #pragma unroll
-    for (int k = 0; k < RowPieces<DP>::kNP; ++k) pf[k] = load16(row + min(16 * k, D - 16));
-  } else {  // short descriptors (D < 16): byte loads of piece 0
+  for (int k = 0; k < NP; ++k) pf[k] = load16(row + 16 * min(k, np - 1));
+  if (last_row && (D & 15) != 0) {  // one lane in the whole grid: no read past des_q
     uint32_t w[4] = {0u, 0u, 0u, 0u};
-    for (int c = 0; c < D; ++c) w[c >> 2] |= (uint32_t)row[c] << (8 * (c & 3));
-    pf[0] = make_uint4(w[0], w[1], w[2], w[3]);
 #pragma unroll
-    for (int k = 1; k < RowPieces<DP>::kNP; ++k) pf[k] = make_uint4(0u, 0u, 0u, 0u);
+    for (int c = 0; c < 16; ++c)
+      if (16 * (np - 1) + c < D) w[c >> 2] |= (uint32_t)row[16 * (np - 1) + c] << (8 * (c & 3));
+#pragma unroll
+    for (int k = 0; k < NP; ++k)  // (a register array is never indexed at run time)
+      if (k == np - 1) pf[k] = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
-// 16 bytes >> 8 * sh (0 <= sh < 16, uniform), zero-filled from the top.
-__device__ __forceinline__ uint4 shr_bytes(uint4 v, int sh) {
-  uint32_t w[8] = {v.x, v.y, v.z, v.w, 0u, 0u, 0u, 0u};
-  const int ws = sh >> 2;
-  const uint32_t bs = (uint32_t)(sh & 3);
-  uint32_t o[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    uint32_t lo = w[i], hi = w[i + 1];
-    // uniform word shift by selects (no indexed registers)
-#pragma unroll
-    for (int k = 1; k < 4; ++k)
-      if (ws == k) {
-        lo = w[i + k];
-        hi = w[i + k + 1];
-      }
-    o[i] = __builtin_amdgcn_alignbyte(hi, lo, bs);
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
+// mask of the bytes of word `w` (0..3) of piece `k` that lie inside the descriptor
+__device__ __forceinline__ uint32_t byte_mask(int D, int k, int w) {
+  const int n = D - 16 * k - 4 * w;  // bytes of this word inside the row
+  return n >= 4 ? ~0u : (n <= 0 ? 0u : (1u << (8 * n)) - 1u);
 }
 
-template <int DP, int ROWB>
+template <int DP>
 __device__ __forceinline__ void land_row(uint8_t* qrow, uint32_t* qk, int r, bool real, int D,
                                          const uint4 (&pf)[RowPieces<DP>::kNP]) {
-  constexpr int NP = RowPieces<DP>::kNP;
-  const int np = D >= 16 ? (D + 15) >> 4 : 1;  // pieces holding the row (uniform)
-  uint4 w[NP];
-#pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    uint4 v = pf[k];
-    v.x ^= 0x7f7f7f7fu;  // int8 127 - b
-    v.y ^= 0x7f7f7f7fu;
-    v.z ^= 0x7f7f7f7fu;
-    v.w ^= 0x7f7f7f7fu;
-    if (D < 16) {  // zero past D (xor made the zero bytes 0x7f)
-      const uint32_t m[4] = {D >= 4 ? ~0u : (1u << (8 * D)) - 1u, D >= 8 ? ~0u : D <= 4 ? 0u : (1u << (8 * (D - 4))) - 1u,
-                             D >= 12 ? ~0u : D <= 8 ? 0u : (1u << (8 * (D - 8))) - 1u,
-                             D <= 12 ? 0u : (1u << (8 * (D - 12))) - 1u};
-      if (k == 0) v = make_uint4(v.x & m[0], v.y & m[1], v.z & m[2], v.w & m[3]);
-    } else if (k == np - 1) {
-      v = shr_bytes(v, 16 * np - D);  // the last piece was loaded at D - 16
-    }
-    if (k >= np || !real) v = make_uint4(0u, 0u, 0u, 0u);
-    w[k] = v;
-  }
   int nb = kBias;
 #pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    nb = sq2(w[k].x, nb);
-    nb = sq2(w[k].y, nb);
-    nb = sq2(w[k].z, nb);
-    nb = sq2(w[k].w, nb);
-    *reinterpret_cast<uint4*>(qrow + 16 * k) = w[k];
+  for (int k = 0; k < RowPieces<DP>::kNP; ++k) {
+    uint4 v = pf[k];
+    // int8 127 - b inside the row, zero past D (the masks are uniform)
+    v.x = (v.x ^ 0x7f7f7f7fu) & byte_mask(D, k, 0);
+    v.y = (v.y ^ 0x7f7f7f7fu) & byte_mask(D, k, 1);
+    v.z = (v.z ^ 0x7f7f7f7fu) & byte_mask(D, k, 2);
+    v.w = (v.w ^ 0x7f7f7f7fu) & byte_mask(D, k, 3);
+    if (!real) v = make_uint4(0u, 0u, 0u, 0u);
+    nb = sq2(v.x, nb);
+    nb = sq2(v.y, nb);
+    nb = sq2(v.z, nb);
+    nb = sq2(v.w, nb);
+    *reinterpret_cast<uint4*>(qrow + 16 * k) = v;
   }
   // padding rows of the last tile (zero descriptors, so acc = 0) get the key kPad
   *qk = real ? (((uint32_t)nb << 8) | (uint32_t)r) : kPad;
 }
 
-template <int DP>
-__global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
+// WAVES = 8: 512 template rows per workgroup share each staged chunk (half the staging
+// and barrier work per tile of the 4-wave form, which n_tpl <= 256 uses).
+template <int DP, int WAVES>
+__global__ __launch_bounds__(KnnShape<WAVES>::kThreads) void knn2_l2u8_kernel(
     const uint8_t* __restrict__ des_tpl, int n_tpl, int D, const uint8_t* __restrict__ des_q,
     const int32_t* __restrict__ q_off, int32_t* __restrict__ out_idx, float* __restrict__ out_dist) {
   constexpr int KSTEPS = DP / 32;
@@ -186,7 +167,9 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t qbuf[2][kQChunk * ROWB];
   __shared__ __attribute__((aligned(16))) uint32_t qkey[2][kQChunk];
 
-  const int f = blockIdx.y;
+  // the template blocks of one frame on one XCD (they stage the same frame rows)
+  const int tile = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  const int f = tile / gridDim.x, tblk = tile - f * gridDim.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -195,6 +178,7 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
   const int q_begin = q_off[f];
   const int n_q = q_off[f + 1] - q_begin;
   const uint8_t* qrows = des_q + (size_t)q_begin * D;
+  const int last_row = q_off[gridDim.y] - 1 - q_begin;  // des_q's last row, frame-relative
 
   // ---- template fragments (B operand) and T = sum(x^2 + 2x) + D, kept in registers
   v4i bfrag[kBlocksPerWave][KSTEPS];
@@ -202,7 +186,7 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
   int tpl_row[kBlocksPerWave];
 #pragma unroll
   for (int b = 0; b < kBlocksPerWave; ++b) {
-    const int i = blockIdx.x * kTplPerWG + (wave * kBlocksPerWave + b) * 32 + c;
+    const int i = tblk * KnnShape<WAVES>::kTplPerWG + (wave * kBlocksPerWave + b) * 32 + c;
     tpl_row[b] = i;
     int na = 0;
 #pragma unroll
@@ -225,16 +209,23 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
 #pragma unroll
   for (int b = 0; b < kBlocksPerWave; ++b) g1[b] = g2[b] = kNoKey64;
 
+  // one thread per staged row (threads 0..255; in 8-wave workgroups the other half
+  // waits at the barrier -- splitting rows over two threads measured no faster)
   uint4 pf[RowPieces<DP>::kNP];
-  if (n_q > 0) issue_row<DP>(qrows + (size_t)min(tid, n_q - 1) * D, D, pf);
+  if (n_q > 0 && tid < kQChunk) {
+    const int r = min(tid, n_q - 1);
+    issue_row<DP>(qrows + (size_t)r * D, D, r == last_row, pf);
+  }
   for (int q0 = 0, buf = 0; q0 < n_q; q0 += kQChunk, buf ^= 1) {
     const int cnt = min(kQChunk, n_q - q0);
     const int rows = (cnt + 31) & ~31;
     // ---- stage frame descriptors [q0, q0+cnt) as int8 127 - b, zero-padded to DP columns
-    if (tid < rows) land_row<DP, ROWB>(&qbuf[buf][tid * ROWB], &qkey[buf][tid], tid, tid < cnt, D, pf);
+    if (tid < rows) land_row<DP>(&qbuf[buf][tid * ROWB], &qkey[buf][tid], tid, tid < cnt, D, pf);
     __syncthreads();
-    if (q0 + kQChunk < n_q)
-      issue_row<DP>(qrows + (size_t)(q0 + kQChunk + min(tid, n_q - q0 - kQChunk - 1)) * D, D, pf);
+    if (q0 + kQChunk < n_q && tid < kQChunk) {
+      const int r = q0 + kQChunk + min(tid, n_q - q0 - kQChunk - 1);
+      issue_row<DP>(qrows + (size_t)r * D, D, r == last_row, pf);
+    }
     const uint8_t* qb = qbuf[buf];
     const uint32_t* qkb = qkey[buf];
     uint32_t b1[kBlocksPerWave][2], b2[kBlocksPerWave][2];  // [even | odd accumulator]
@@ -262,12 +253,15 @@ __global__ __launch_bounds__(kThreads) void knn2_l2u8_kernel(
         for (int r = 0; r < 16; ++r) top2_insert(b1[b][r & 1], b2[b][r & 1], ((uint32_t)acc[r] << 9) + qk[r]);
       }
     }
-    // ---- fold the chunk's top-2 (local indices) into the frame's 64-bit top-2
+    // ---- fold the chunk's top-2 (local indices) into the frame's 64-bit top-2: the
+    // even / odd pairs merge in 32 bits first (c1 <= c2 = the chunk's two smallest keys)
 #pragma unroll
     for (int b = 0; b < kBlocksPerWave; ++b) {
-      const uint32_t ks[4] = {b1[b][0], b2[b][0], b1[b][1], b2[b][1]};
+      const uint32_t c1 = min(b1[b][0], b1[b][1]);
+      const uint32_t c2 = min(max(b1[b][0], b1[b][1]), min(b2[b][0], b2[b][1]));
+      const uint32_t ks[2] = {c1, c2};
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
+      for (int k = 0; k < 2; ++k)
         if (ks[k] < kPad) {
           const uint32_t ssd = (ks[k] >> 8) + (uint32_t)(tk[b] - kBias);
           top2_insert64(g1[b], g2[b], ((unsigned long long)ssd << 32) | (uint32_t)(q0 + (int)(ks[k] & 255u)));
@@ -405,11 +399,19 @@ int launch_knn(const uint8_t* des_tpl, int n_tpl, int D, const uint8_t* des_q, c
                int n_frames, int max_nq, int32_t* out_idx, float* out_dist, hipStream_t s) {
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
   (void)max_nq;
-  dim3 grid(ceil_div(n_tpl, kTplPerWG), n_frames);
-  if (D <= 32)
-    hipLaunchKernelGGL((knn2_l2u8_kernel<32>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
-  else
-    hipLaunchKernelGGL((knn2_l2u8_kernel<64>), grid, dim3(kThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+  if (n_tpl > 256) {
+    dim3 grid(ceil_div(n_tpl, KnnShape<8>::kTplPerWG), n_frames);
+    if (D <= 32)
+      hipLaunchKernelGGL((knn2_l2u8_kernel<32, 8>), grid, dim3(512), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+    else
+      hipLaunchKernelGGL((knn2_l2u8_kernel<64, 8>), grid, dim3(512), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+  } else {
+    dim3 grid(ceil_div(n_tpl, KnnShape<4>::kTplPerWG), n_frames);
+    if (D <= 32)
+      hipLaunchKernelGGL((knn2_l2u8_kernel<32, 4>), grid, dim3(256), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+    else
+      hipLaunchKernelGGL((knn2_l2u8_kernel<64, 4>), grid, dim3(256), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+  }
   return launch_check("knn2_l2u8_kernel");
 }
 

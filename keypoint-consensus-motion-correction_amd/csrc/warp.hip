@@ -556,12 +556,7 @@ __device__ __forceinline__ void output_tile(int mode, const uint16_t* stile, con
     output_rows<Cfg, C, 2>(stile, box, S, Dst, H, W, xb, yb, wave, lane, ad, bd, X0v, Y0v);
 }
 
-// XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so give each XCD a
-// contiguous run of ids (bijective also when n % 8 != 0).
-__device__ __forceinline__ int xcd_remap(int bid, int n) {
-  const int q8 = n >> 3, r8 = n & 7, xcd = bid & 7;
-  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-}
+// (xcd_remap: kcmc_internal.h)
 
 // ------------------------------------------------------------------------- plan
 // One thread per tile (tile id = (f * nty + ty) * ntx + tx): the fp64 map inversion
