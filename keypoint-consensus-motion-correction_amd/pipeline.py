@@ -201,22 +201,54 @@ def align_slab(inp: SlabInputs, cfg: AlignConfig, logger: Optional[logging.Logge
                       rr if keep_intermediates else None, counts)
 
 
-class OverlappedSlabs:
-    """Streams slabs through the hot path with the warp of slab k overlapping the rest
-    of slab k+1.
+def _d2h_async(t: torch.Tensor) -> Tuple[torch.Tensor, torch.cuda.Event]:
+    """Stream-ordered device->host copy into pinned memory; the event marks its end."""
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    return h, ev
 
-    Match, consensus and RANSAC run on an analysis stream, the warp on a warp stream;
-    the host waits only for the analysis stream (survivor bitmasks, affines), so the
-    host steps (consensus, affine post-processing) and the small GPU stages of the next
-    slab proceed while the previous slab's frames are being warped.  Every slab still
-    runs every stage and its results equal ``align_slab``'s.
+
+@dataclass
+class _SlabInFlight:
+    """A slab whose analysis is queued: its warp waits for the next submit (or flush)."""
+
+    inp: SlabInputs
+    out: Optional[torch.Tensor]
+    f0: int
+    match: stages.MatchResult
+    cons: stages.Consensus
+    rr: stages.RansacResult
+    params_host: torch.Tensor
+    params_ready: torch.cuda.Event
+
+
+class OverlappedSlabs:
+    """Streams slabs through the hot path as a two-slab software pipeline on one stream.
+
+    submit(slab k+1) queues, in this device order,
+
+        match(k+1) -> [bitmask D2H] -> warp(k) -> RANSAC(k+1) -> [params D2H]
+
+    and the host work of the two slabs fills the GPU time between: the consensus of
+    slab k+1 (VA:224-286) runs while slab k's frames are being warped, and the affine
+    post-processing of slab k (VA:143-145) while match(k+1) runs.  The kernels never
+    share the CUs with each other (co-resident analysis kernels slowed the warp by as
+    much as they ran, and a large-LDS match workgroup starves behind the warp's tiles),
+    so a step costs the sum of its kernels plus whatever host time is not covered.
+    Every slab runs every stage and its results equal ``align_slab``'s.
+
+    submit returns the SlabResult of the slab whose warp it queued (None for the first
+    slab); flush() queues the last warp.  ``res.extras["done"]`` is an event after that
+    warp; ``aligned`` is ready once it has passed (or after synchronize()).
 
     With ``counts`` (frames per rank) the slabs are one rank's share of a frame-sharded
-    job (distributed.align_sharded's exchanges on the analysis stream).
+    job: survivor bitmasks and RANSAC parameters are all-gathered over ``group``
+    (distributed.align_sharded's two exchanges) in the same stream order.
 
         ov = OverlappedSlabs(device, cfg)
-        for inp in slabs:
-            res, done = ov.submit(inp)     # done: event on the warp stream
+        results = [ov.submit(inp) for inp in slabs][1:] + [ov.flush()]
         ov.synchronize()
     """
 
@@ -232,70 +264,79 @@ class OverlappedSlabs:
         self.logger = logger
         self.counts = counts
         self.group = group
-        self.analysis = torch.cuda.Stream(self.dev)
-        self.warp = torch.cuda.Stream(self.dev)
+        self.stream = torch.cuda.Stream(self.dev)
+        self._prev: Optional[_SlabInFlight] = None
+
+    def _sharded(self) -> bool:
+        return self.counts is not None and len(self.counts) > 1
 
     def submit(self, inp: SlabInputs, out: Optional[torch.Tensor] = None,
-               mark: Optional[Callable[[str], None]] = None):
+               mark: Optional[Callable[[str], None]] = None) -> Optional[SlabResult]:
         mark = mark or (lambda name: None)
         cfg = self.cfg
-        cur = torch.cuda.current_stream(self.dev)
-        self.analysis.wait_stream(cur)
-        self.warp.wait_stream(cur)
+        self.stream.wait_stream(torch.cuda.current_stream(self.dev))
         n_tpl = inp.des_tpl.shape[0]
         n_local = inp.q_off.numel() - 1
-        with torch.cuda.stream(self.analysis):
+        with torch.cuda.stream(self.stream):
             mark("m0")
             match = match_stage(inp, cfg)
             mark("m1")
-            if self.counts is not None and len(self.counts) > 1:
+            if self._sharded():
                 from .distributed import _all_gather_rows
                 import torch.distributed as dist
 
                 rank = dist.get_rank(self.group)
-                keep = _all_gather_rows(match.keep_bits, self.counts, self.group).cpu().numpy()
-                f0 = sum(self.counts[:rank])
-                # the global consensus, point lists of this rank's frames only
-                cons = consensus_stage(keep, n_tpl, sum(self.counts), cfg, self.logger if rank == 0 else None,
-                                       frames=(f0, f0 + n_local))
-                mark("r0")
-                rr = ransac_stage(match, inp.kp_tpl, cons, cfg)
-                mark("r1")
-                params = _all_gather_rows(rr.params, self.counts, self.group).cpu().numpy()
+                f0, n_all = sum(self.counts[:rank]), sum(self.counts)
+                keep_h, keep_ready = _d2h_async(_all_gather_rows(match.keep_bits, self.counts, self.group))
             else:
-                f0 = 0
-                keep = match.keep_bits.cpu().numpy()
-                cons = consensus_stage(keep, n_tpl, n_local, cfg, self.logger)
-                mark("r0")
-                rr = ransac_stage(match, inp.kp_tpl, cons, cfg)
-                mark("r1")
-                params = rr.params.cpu().numpy()
-        affines, skipped, interpolated, eu = postprocess_affines(params, cfg)
-        # the affines go up on the (idle) analysis stream, so the warp stream goes straight
-        # from the previous slab's warp to this one's (a copy queued behind that warp would
-        # add its own latency to every step); pinned + non_blocking, as a pageable copy
-        # waits for the device to drain
-        with torch.cuda.stream(self.analysis):
-            a = torch.from_numpy(np.ascontiguousarray(affines[f0:f0 + inp.frames.shape[0]], dtype=np.float64))
-            a = a.pin_memory().to(self.dev, non_blocking=True)
-            a_ready = torch.cuda.Event()
-            a_ready.record(self.analysis)
-        with torch.cuda.stream(self.warp):
-            if out is not None:
-                out.record_stream(self.warp)
-            inp.frames.record_stream(self.warp)
-            a.record_stream(self.warp)
-            self.warp.wait_event(a_ready)
-            mark("w0")
-            aligned = warp_frames(inp.frames, a, out=out)
-            mark("w1")
-            done = torch.cuda.Event()
-            done.record(self.warp)
-        return SlabResult(aligned, affines, eu, skipped, interpolated, consensus=cons, ransac=rr), done
+                rank, f0, n_all = 0, 0, n_local
+                keep_h, keep_ready = _d2h_async(match.keep_bits)
+            finished = self._finish_prev(mark)  # warp(k) queued behind match(k+1)
+            keep_ready.synchronize()
+            # the global consensus; with counts, point lists of this rank's frames only
+            cons = consensus_stage(keep_h.numpy(), n_tpl, n_all, cfg, self.logger if rank == 0 else None,
+                                   frames=(f0, f0 + n_local) if self._sharded() else None)
+            mark("r0")
+            rr = ransac_stage(match, inp.kp_tpl, cons, cfg)
+            mark("r1")
+            if self._sharded():
+                from .distributed import _all_gather_rows
+
+                params_h, params_ready = _d2h_async(_all_gather_rows(rr.params, self.counts, self.group))
+            else:
+                params_h, params_ready = _d2h_async(rr.params)
+            for t in (inp.frames, out):
+                if t is not None:
+                    t.record_stream(self.stream)
+            self._prev = _SlabInFlight(inp, out, f0, match, cons, rr, params_h, params_ready)
+        return finished
+
+    def _finish_prev(self, mark) -> Optional[SlabResult]:
+        p, self._prev = self._prev, None
+        if p is None:
+            return None
+        p.params_ready.synchronize()
+        affines, skipped, interpolated, eu = postprocess_affines(p.params_host.numpy(), self.cfg)
+        n = p.inp.frames.shape[0]
+        # pinned + non_blocking: a pageable copy would wait for the device to drain
+        a = torch.from_numpy(np.ascontiguousarray(affines[p.f0:p.f0 + n], dtype=np.float64))
+        a = a.pin_memory().to(self.dev, non_blocking=True)
+        mark("w0")
+        aligned = warp_frames(p.inp.frames, a, out=p.out)
+        mark("w1")
+        done = torch.cuda.Event()
+        done.record(self.stream)
+        res = SlabResult(aligned, affines, eu, skipped, interpolated, match=p.match, consensus=p.cons, ransac=p.rr)
+        res.extras["done"] = done
+        return res
+
+    def flush(self, mark: Optional[Callable[[str], None]] = None) -> Optional[SlabResult]:
+        """Queue the warp of the last submitted slab (None if there is none)."""
+        with torch.cuda.stream(self.stream):
+            return self._finish_prev(mark or (lambda name: None))
 
     def synchronize(self) -> None:
-        self.analysis.synchronize()
-        self.warp.synchronize()
+        self.stream.synchronize()
 
 
 def align_streamed(frames_host: torch.Tensor, inp: SlabInputs, cfg: AlignConfig, slab: int = 64,

@@ -129,8 +129,9 @@ def test_config2_slab_end_to_end(dev):
 
 
 def test_overlapped_slabs_equal_align_slab(dev):
-    """OverlappedSlabs (analysis stream + warp stream, slabs in flight together) gives
-    the same affines and warped frames as the sequential align_slab."""
+    """OverlappedSlabs (two slabs in flight: the warp of slab k queued between the match
+    and the RANSAC of slab k+1) gives the same affines and warped frames as the
+    sequential align_slab."""
     F, H, W = 24, 270, 480
     cfg = pipeline.AlignConfig(n_kp_global=60)
     slabs = []
@@ -144,7 +145,10 @@ def test_overlapped_slabs_equal_align_slab(dev):
                                          ks.q_off))
     ref = [pipeline.align_slab(s, cfg) for s in slabs]
     ov = pipeline.OverlappedSlabs(dev, cfg)
-    got = [ov.submit(s)[0] for s in slabs]
+    got = [ov.submit(s) for s in slabs]
+    assert got[0] is None
+    got = got[1:] + [ov.flush()]
+    assert ov.flush() is None
     ov.synchronize()
     for r, g in zip(ref, got):
         assert np.array_equal(r.affines, g.affines, equal_nan=True)

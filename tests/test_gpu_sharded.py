@@ -1,0 +1,133 @@
+"""The product's frame-sharded path on the GPU: two ranks (gloo, both on cuda:0, started
+as fresh child processes) run `distributed.align_sharded` with the HIP stages and the
+pipelined `OverlappedSlabs(counts=...)` on uneven slabs, with the template broadcast
+from rank 0 (VA:117-123 / VA:460-465 pickle it to every worker).  The concatenated
+per-rank results must be bit-identical to one single-device `align_slab` over all
+frames: the survivor-bitmask and affine all-gathers and the per-rank consensus slice
+(VA:224-286) may not change a single pixel.
+
+The ranks are separate interpreters (this file run as a script), launched before this
+process touches the GPU in the test body."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+from kcmc_amd import pipeline, synthetic  # noqa: E402
+
+WORLD = 2
+COUNTS = (9, 14)            # uneven slabs (frames per rank)
+N_TPL, D, HW = 160, 32, (120, 200)
+N_KP_GLOBAL = 40
+
+
+def _keypoints(rank: int, slab: int, model: str):
+    return synthetic.make_keypoints(COUNTS[rank], N_TPL, D, HW, seed=17, frame_seed=100 * slab + rank, model=model)
+
+
+def _frames(n: int):
+    base = synthetic.make_texture(HW, seed=4)
+    return np.broadcast_to(base, (n,) + HW).copy()
+
+
+def _inputs(ks_list, dev):
+    """SlabInputs of the concatenation of several ranks' keypoint sets."""
+    des_q = np.concatenate([k.des_q for k in ks_list])
+    kp_q = np.concatenate([k.kp_q for k in ks_list])
+    off = [0]
+    for k in ks_list:
+        off.extend((off[-1] + k.q_off[1:]).tolist())
+    q_off = np.asarray(off, np.int32)
+    n = len(q_off) - 1
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    return pipeline.SlabInputs(t(_frames(n)), t(ks_list[0].des_tpl), t(ks_list[0].kp_tpl), t(des_q), t(kp_q),
+                               t(q_off), q_off)
+
+
+def _rank_main(rank: int, port: int, out_dir: str, model: str) -> None:
+    import torch.distributed as dist
+
+    from kcmc_amd import distributed as kdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    cfg = pipeline.AlignConfig(n_kp_global=N_KP_GLOBAL, ransac_model=model)
+    slabs = [_inputs([_keypoints(rank, s, model)], dev) for s in range(2)]
+    for inp in slabs:
+        if rank != 0:  # only rank 0 holds the template; the others receive it
+            inp.des_tpl.zero_()
+            inp.kp_tpl.zero_()
+        kdist.broadcast_template(inp.des_tpl, inp.kp_tpl)
+    out = {}
+    # 1. align_sharded with the product's HIP stages
+    res = kdist.align_sharded(slabs[0], cfg, impl=kdist.HIP_STAGES)
+    torch.cuda.synchronize()
+    out["sharded_aligned"] = res.aligned.cpu().numpy()
+    out["sharded_affines"] = res.affines
+    out["sharded_skipped"] = np.asarray(res.skipped, np.int64)
+    # 2. the pipelined schedule with the two exchanges, two slabs in flight
+    ov = pipeline.OverlappedSlabs(dev, cfg, counts=list(COUNTS))
+    r0 = ov.submit(slabs[0])
+    r1 = ov.submit(slabs[1])
+    r2 = ov.flush()
+    ov.synchronize()
+    assert r0 is None and r1 is not None and r2 is not None
+    for k, r in enumerate((r1, r2)):
+        out[f"ov{k}_aligned"] = r.aligned.cpu().numpy()
+        out[f"ov{k}_affines"] = r.affines
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out)
+    dist.destroy_process_group()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("model", ["euclidean", "affine"])
+def test_sharded_hip_path_equals_single_device(tmp_path, model):
+    port = _free_port()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), str(r), str(port), str(tmp_path), model],
+                              env=env, cwd=REPO) for r in range(WORLD)]
+    try:
+        rcs = [p.wait(timeout=200) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0] * WORLD, rcs
+    got = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(WORLD)]
+
+    dev = torch.device("cuda", 0)
+    cfg = pipeline.AlignConfig(n_kp_global=N_KP_GLOBAL, ransac_model=model)
+    for s, tag in ((0, "sharded"), (0, "ov0"), (1, "ov1")):
+        ref = pipeline.align_slab(_inputs([_keypoints(r, s, model) for r in range(WORLD)], dev), cfg)
+        assert len(ref.skipped) < sum(COUNTS) // 2
+        aligned = ref.aligned.cpu().numpy()
+        for r in range(WORLD):
+            np.testing.assert_array_equal(got[r][f"{tag}_affines"], ref.affines)
+        np.testing.assert_array_equal(np.concatenate([got[r][f"{tag}_aligned"] for r in range(WORLD)]), aligned)
+        if tag == "sharded":
+            assert got[0]["sharded_skipped"].tolist() == ref.skipped
+
+
+if __name__ == "__main__":
+    _rank_main(int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4])

@@ -4,10 +4,11 @@ host spends a step while the warp of the previous step runs on the GPU.
     python tools/host_breakdown.py [--config c2] [--frames F] [--steps 8]
 
 Prints, per step, host wall-clock milliseconds between the marks OverlappedSlabs.submit
-passes through (m0 match launched, m1, r0 after the bitmask D2H + native consensus, r1
-RANSAC launched, w0 after the affine D2H + post-processing + H2D, w1 warp launched), and
-the consensus alone on the same bitmasks.  A host chain longer than the warp means the
-warp stream idles between steps."""
+passes through (m0 match launched, m1, w0 after the previous slab's params D2H wait +
+post-processing + H2D, w1 its warp launched, r0 after the bitmask D2H + native consensus,
+r1 RANSAC launched), and the consensus alone on the same bitmasks.  The GPU idles when
+the post-processing (m1->w0) outlasts the match kernels, or the consensus (w1->r0) the
+warp."""
 import argparse
 import json
 import os
@@ -27,7 +28,6 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(bench.CONFIGS))
     ap.add_argument("--frames", type=int, default=None)
     ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--priority", type=int, default=None, help="analysis stream priority (torch: -1 = high)")
     args = ap.parse_args()
     bc = bench.CONFIGS[args.config]
     args.frames = args.frames or bc.frames_per_gpu
@@ -37,8 +37,6 @@ def main():
     out = torch.empty_like(inp.frames)
     cfg = pipeline.AlignConfig(n_kp_global=bc.n_kp_global, ransac_model=bc.model)
     ov = pipeline.OverlappedSlabs(dev, cfg)
-    if args.priority is not None:
-        ov.analysis = torch.cuda.Stream(dev, priority=args.priority)
     rows = []
     for s in range(args.steps + 2):
         if s == 2:
@@ -49,9 +47,10 @@ def main():
         ov.submit(inp, out=out, mark=lambda n: t.__setitem__(n, time.perf_counter()))
         t["end"] = time.perf_counter()
         if s >= 2:
-            keys = ["m0", "m1", "r0", "r1", "w0", "w1", "end"]
+            keys = ["m0", "m1", "w0", "w1", "r0", "r1", "end"]
             rows.append({f"{a}->{b}": round((t[b] - t[a]) * 1e3, 3) for a, b in zip(keys, keys[1:])}
                         | {"submit_ms": round((t["end"] - t0) * 1e3, 3)})
+    ov.flush()
     ov.synchronize()
     step_ms = (time.perf_counter() - t_start) * 1e3 / args.steps
     keep = pipeline.match_stage(inp, cfg).keep_bits.cpu().numpy()
@@ -61,7 +60,7 @@ def main():
         pipeline.consensus_stage(keep, inp.des_tpl.shape[0], args.frames, cfg, None)
         cons.append((time.perf_counter() - c0) * 1e3)
     med = {k: round(float(np.median([r[k] for r in rows])), 3) for k in rows[0]}
-    print(json.dumps({"config": args.config, "frames": args.frames, "priority": args.priority, "step_ms": round(step_ms, 3), "median_host_ms": med, "consensus_alone_ms": round(min(cons), 3),
+    print(json.dumps({"config": args.config, "frames": args.frames, "step_ms": round(step_ms, 3), "median_host_ms": med, "consensus_alone_ms": round(min(cons), 3),
                       "cpu_count": os.cpu_count()}))
 
 
