@@ -52,6 +52,14 @@ __global__ void diff_kernel(const uint16_t* a, const uint16_t* b, size_t n, unsi
   if (c) atomicAdd(cnt, c);
 }
 
+// order-sensitive checksum of an output stack (compares the outputs of two lab builds)
+__global__ void hash_kernel(const uint16_t* a, size_t n, unsigned long long* h) {
+  unsigned long long c = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    c += (unsigned long long)a[i] * (2654435761ull * (i + 1) | 1ull);
+  atomicAdd(h, c);
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
 template <class L>
@@ -99,7 +107,7 @@ int main(int argc, char** argv) {
     return h;
   };
   void* ws;
-  CK(hipMalloc(&ws, warp_workspace_bytes<WarpCfg<32, 8192, 6>>(F, H, W)));  // the most tiles
+  CK(hipMalloc(&ws, warp_workspace_bytes<WarpCfg<24, 8192, 6>>(F, H, W)));  // the most tiles
   using C32 = WarpCfg<32, 8192, 6>;
   using C40 = WarpCfg<40, 8192, 7>;
   using C48 = WarpCfg<48, 9216, 8>;
@@ -127,6 +135,16 @@ int main(int argc, char** argv) {
     } else {
       CK(hipMemcpy(src, tex.data(), tex.size() * 2, hipMemcpyHostToDevice));
       for (int f = 1; f < F; ++f) CK(hipMemcpy(src + (size_t)f * H * W, src, tex.size() * 2, hipMemcpyDeviceToDevice));
+    }
+    if (getenv("LAB_LIB")) {  // the library's own configuration (BlockCfg), 3 repeats + output checksum
+      for (int k = 0; k < 3; ++k)
+        report("library cfg", timeit([&] { launch_warp<1>(src, dst, M, F, H, W, 0, ws, 0); }, reps));
+      (void)hipMemset(cnt, 0, 8);
+      hipLaunchKernelGGL(hash_kernel, dim3(4096), dim3(256), 0, 0, dst, n, cnt);
+      unsigned long long h = 0;
+      (void)hipMemcpy(&h, cnt, 8, hipMemcpyDeviceToHost);
+      printf("    output checksum %016llx\n", h);
+      continue;
     }
     if (getenv("LAB_ONLY56")) {  // the library's configuration only, 3 repeats
       for (int k = 0; k < 3; ++k)
