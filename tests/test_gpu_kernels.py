@@ -226,6 +226,29 @@ def test_ransac_exact_data_early_exit(dev):
     np.testing.assert_allclose(params[0], [[1, 0, 4], [0, 1, -2]], atol=1e-12)
 
 
+@pytest.mark.parametrize("thresh", [2.0, 1.7, 0.3])
+def test_ransac_inlier_threshold_boundary(dev, thresh):
+    """The count pass tests q = dx^2 + dy^2 < Tq instead of sqrt(q) < t: residuals within
+    a few ulps of the threshold (both sides, exactly on it) give the oracle's inliers."""
+    rng = np.random.default_rng(int(thresh * 10))
+    tpl = rng.uniform(-3, 3, (60, 2))
+    shift = np.array([0.75, -0.5])
+    q = tpl - shift
+    ang = rng.uniform(0, 2 * np.pi, 24)
+    for k in range(24):  # |residual| = thresh * (1 + j * 2^-50), j in -3..3, and exact multiples
+        rad = thresh * (1 + (k % 7 - 3) * 2.0 ** -50) if k < 21 else thresh
+        d = np.array([np.cos(ang[k]), np.sin(ang[k])]) * rad if k < 21 else np.array([rad, 0.0])
+        q[k] = tpl[k] - shift - d
+    off = _csr([q])
+    r = stages.ransac_rigid(_t(q, dev), _t(tpl, dev), _t(off, dev), off, residual_threshold=thresh)
+    p, i_ref, bt, ni = oracle.ransac_rigid(q, tpl, thresh=thresh)
+    assert r.best_trial.cpu().numpy()[0] == bt
+    assert r.n_inliers.cpu().numpy()[0] == ni
+    assert np.array_equal(r.inliers.cpu().numpy().astype(bool), i_ref)
+    np.testing.assert_allclose(r.params.cpu().numpy()[0], p, rtol=1e-10, atol=1e-10)
+    assert 36 <= ni < 60
+
+
 def test_ransac_gather_mode_matches_contiguous(dev):
     rng = np.random.default_rng(23)
     n_tpl, F = 60, 7
