@@ -39,6 +39,8 @@ from kcmc_amd import pipeline, stages, synthetic  # noqa: E402
 
 METRIC = "aligned frames/sec (whole node) at 1080p; RANSAC hypotheses scored/sec/GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
+I8_PEAK_TOPS = 5000.0  # dense i8 MFMA: 2x the bf16 rate per clock (MI355X_MICROARCH.md)
 TRIALS = 1000
 
 
@@ -315,13 +317,15 @@ def end_to_end(bc: BenchConfig, inp, cfg, dev, world: int, reps: int = 3):
 
 def load_traffic(config: str):
     """HBM bytes per warp launch from the committed rocprofv3 PMC pass of this config
-    (tools/pmc_warp.sh + tools/pmc_summary.py), if present."""
+    (tools/pmc_warp.sh + tools/pmc_summary.py --sha), if present, with its source: the
+    profiles/ file and the commit of the code it was measured on."""
     name = "warp_pmc_traffic.json" if config == "c2" else f"warp_pmc_traffic_{config}.json"
     p = os.path.join(REPO, "profiles", name)
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch"), d
+        return d.get("hbm_bytes_per_launch"), {"file": f"profiles/{name}", "commit": d.get("commit"),
+                                               "kernel_avg_ms_in_pmc_run": d.get("kernel_avg_ms")}
     except (OSError, ValueError):
         return None, None
 
@@ -432,7 +436,7 @@ def main():
     warp_bytes = 2 * inp.frames.numel() * inp.frames.element_size()  # read + write, algorithmic
     achieved = warp_bytes / (warp_ms * 1e-3) / 1e9
     # the committed PMC pass was taken at the config's own frame count: quote it only there
-    traffic = load_traffic(bc.name)[0] if args.frames == bc.frames_per_gpu else None
+    traffic, traffic_src = load_traffic(bc.name) if args.frames == bc.frames_per_gpu else (None, None)
     stage_ms = {"match": round(match_ms, 3), "ransac": round(ransac_ms, 3), "warp": round(warp_ms, 3)}
     if ov is None:
         stage_ms["host_and_transfers"] = round(ms_step - match_ms - ransac_ms - warp_ms, 3)
@@ -475,10 +479,31 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": warp_bytes,
             "avg_launch_ms": round(warp_ms, 4),
         },
     }
+    # the matcher against its MFMA roofline (the dominant kernel of c5): algorithmic work
+    # 2 * n_tpl * n_q * D per frame; the float matcher issues three bf16 products per
+    # fp32 product, so its issued MFMA work is 3x that and is priced against bf16 dense
+    n_q_total = float(inp.q_off_host[-1])
+    match_ops = 2.0 * bc.n_tpl * n_q_total * bc.D
+    iso_match_s = iso["match"] * 1e-3
+    if bc.descriptor == "f32":
+        issued = 3.0 * match_ops / iso_match_s / 1e12
+        result["roofline_match"] = {
+            "kernel": "split_rows_kernel + knn2_l2f32_kernel + rerank + match_filter_kernel (whole match stage)",
+            "bound": "mfma", "achieved": round(issued, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(issued / BF16_PEAK_TFLOPS, 4), "traffic": None,
+            "algorithmic_tflops_fp32_equiv": round(match_ops / iso_match_s / 1e12, 1),
+            "avg_launch_ms": iso["match"], "note": "achieved = issued bf16 MFMA work (3 x algorithmic) / isolated stage time"}
+    else:
+        tops = match_ops / iso_match_s / 1e12
+        result["roofline_match"] = {
+            "kernel": "knn2_l2u8_kernel + match_filter_kernel (whole match stage)", "bound": "mfma",
+            "achieved": round(tops, 1), "peak": I8_PEAK_TOPS, "unit": "TOP/s", "frac": round(tops / I8_PEAK_TOPS, 4),
+            "traffic": None, "avg_launch_ms": iso["match"]}
     if args.e2e:
         result["end_to_end"] = end_to_end(bc, inp, cfg, dev, world)
     if args.detect and bc.C == 1:

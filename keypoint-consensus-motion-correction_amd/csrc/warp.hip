@@ -111,6 +111,15 @@ __device__ __forceinline__ void invert_affine(const double* Min, double* M) {
   M[5] = b2;
 }
 
+// Frames whose map holds a NaN (no RANSAC model) are warped to zeros, as OpenCV's
+// BORDER_CONSTANT gives for coordinates that land outside the image; the pipeline warps
+// them again with the gap-filled maps (VA:347-407) before handing the frames out.
+__device__ __forceinline__ bool map_has_nan(const double* M, int n) {
+  bool nan = false;
+  for (int k = 0; k < n; ++k) nan = nan || M[k] != M[k];
+  return nan;
+}
+
 __device__ __forceinline__ void load_map(const double* __restrict__ Mall, int f, int inverse_map, double* M) {
   if (inverse_map) {
     for (int k = 0; k < 6; ++k) M[k] = Mall[6 * (size_t)f + k];
@@ -580,6 +589,7 @@ __global__ __launch_bounds__(256) void warp_plan_kernel(const double* __restrict
     for (int k = 0; k < 6; ++k) minv[6 * (size_t)f + k] = M[k];
   Box b = source_box<Cfg, C>(M, xb, yb, H, W);
   if (C == 1 && (W & 7) == 0 && b.mode == 0 && b.pitch <= kFastPitch && b.rows <= Fast<Cfg>::kRows) b.mode = 3;
+  if (map_has_nan(M, 6)) b.mode = 1;  // a NaN map (a frame RANSAC could not fit) warps to zeros
   plan[t] = TilePlan{b.mode, b.ax0, b.sy0, b.pitch | (b.rows << 16)};
   for (int j = tx; j < Cfg::kTileH && yb + j < H; j += ntx) {
     const int y = yb + j;
@@ -794,7 +804,8 @@ __global__ __launch_bounds__(256) void persp_plan_kernel(const double* __restric
   }
   if (t2 == 0)
     for (int k = 0; k < 9; ++k) minv[9 * (size_t)f + k] = M[k];
-  const Box b = persp_box<Cfg, C>(M, xb, yb, H, W);
+  Box b = persp_box<Cfg, C>(M, xb, yb, H, W);
+  if (map_has_nan(M, 9)) b.mode = 1;  // a NaN map (a frame RANSAC could not fit) warps to zeros
   plan[t] = TilePlan{b.mode, b.ax0, b.sy0, b.pitch | (b.rows << 16)};
 }
 

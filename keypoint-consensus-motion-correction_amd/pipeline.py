@@ -201,18 +201,40 @@ def align_slab(inp: SlabInputs, cfg: AlignConfig, logger: Optional[logging.Logge
                       rr if keep_intermediates else None, counts)
 
 
-def _d2h_async(t: torch.Tensor) -> Tuple[torch.Tensor, torch.cuda.Event]:
-    """Stream-ordered device->host copy into pinned memory; the event marks its end."""
+def _d2h_async(t: torch.Tensor, copy: torch.cuda.Stream) -> Tuple[torch.Tensor, torch.cuda.Event]:
+    """Device->host copy of ``t`` (produced on the current stream) into pinned memory on
+    the side stream ``copy``, so that the kernel stream does not stop for it; the event
+    marks its end."""
+    produced = torch.cuda.Event()
+    produced.record()
     h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-    h.copy_(t, non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
+    with torch.cuda.stream(copy):
+        copy.wait_event(produced)
+        t.record_stream(copy)
+        h.copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(copy)
     return h, ev
+
+
+def _h2d_async(arrays, dev, copy: torch.cuda.Stream):
+    """Host->device copies (pinned staging) on the side stream ``copy``; the current
+    stream waits for them.  Returns the device tensors."""
+    with torch.cuda.stream(copy):
+        outs = [torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(dev, non_blocking=True) for a in arrays]
+        ev = torch.cuda.Event()
+        ev.record(copy)
+    cur = torch.cuda.current_stream(dev)
+    cur.wait_event(ev)
+    for o in outs:
+        o.record_stream(cur)
+    return outs
 
 
 @dataclass
 class _SlabInFlight:
-    """A slab whose analysis is queued: its warp waits for the next submit (or flush)."""
+    """A slab whose match / consensus / RANSAC are queued; its warp and post-processing
+    follow in the next submit (or flush)."""
 
     inp: SlabInputs
     out: Optional[torch.Tensor]
@@ -222,6 +244,7 @@ class _SlabInFlight:
     rr: stages.RansacResult
     params_host: torch.Tensor
     params_ready: torch.cuda.Event
+    aligned: Optional[torch.Tensor] = None
 
 
 class OverlappedSlabs:
@@ -229,19 +252,24 @@ class OverlappedSlabs:
 
     submit(slab k+1) queues, in this device order,
 
-        match(k+1) -> [bitmask D2H] -> warp(k) -> RANSAC(k+1) -> [params D2H]
+        match(k+1) -> warp(k) -> RANSAC(k+1)
 
-    and the host work of the two slabs fills the GPU time between: the consensus of
-    slab k+1 (VA:224-286) runs while slab k's frames are being warped, and the affine
-    post-processing of slab k (VA:143-145) while match(k+1) runs.  The kernels never
-    share the CUs with each other (co-resident analysis kernels slowed the warp by as
-    much as they ran, and a large-LDS match workgroup starves behind the warp's tiles),
-    so a step costs the sum of its kernels plus whatever host time is not covered.
-    Every slab runs every stage and its results equal ``align_slab``'s.
+    with every transfer on a side stream.  The warp of slab k reads slab k's RANSAC
+    parameters where RANSAC left them: with frame_downsample_rate == 1 the reference's
+    post-processing (VA:143-145) hands a frame with a model its own parameters, so only
+    frames without a model need the host (NaN-gap interpolation); the warp writes zeros
+    for those and they are warped again, with the filled maps, once the host has them.
+    The consensus of slab k+1 (VA:224-286, host) runs while slab k's frames are being
+    warped.  The kernels never share the CUs with each other (co-resident analysis
+    kernels slowed the warp by as much as they ran, and a large-LDS match workgroup
+    starves behind the warp's tiles), so a step costs the sum of its kernels.  With
+    frame_downsample_rate > 1 every full-rate frame's map comes from the host
+    interpolation, and the warp of slab k waits for it.  Every slab runs every stage and
+    its results equal ``align_slab``'s.
 
     submit returns the SlabResult of the slab whose warp it queued (None for the first
-    slab); flush() queues the last warp.  ``res.extras["done"]`` is an event after that
-    warp; ``aligned`` is ready once it has passed (or after synchronize()).
+    slab); flush() queues the last warp.  ``res.extras["done"]`` is an event after the
+    slab's last warp; ``aligned`` is ready once it has passed (or after synchronize()).
 
     With ``counts`` (frames per rank) the slabs are one rank's share of a frame-sharded
     job: survivor bitmasks and RANSAC parameters are all-gathered over ``group``
@@ -265,10 +293,14 @@ class OverlappedSlabs:
         self.counts = counts
         self.group = group
         self.stream = torch.cuda.Stream(self.dev)
+        self.copy = torch.cuda.Stream(self.dev)  # bitmask / point-list / params / map transfers
         self._prev: Optional[_SlabInFlight] = None
 
     def _sharded(self) -> bool:
         return self.counts is not None and len(self.counts) > 1
+
+    def _device_maps(self) -> bool:
+        return int(self.cfg.frame_downsample_rate) == 1
 
     def submit(self, inp: SlabInputs, out: Optional[torch.Tensor] = None,
                mark: Optional[Callable[[str], None]] = None) -> Optional[SlabResult]:
@@ -287,43 +319,60 @@ class OverlappedSlabs:
 
                 rank = dist.get_rank(self.group)
                 f0, n_all = sum(self.counts[:rank]), sum(self.counts)
-                keep_h, keep_ready = _d2h_async(_all_gather_rows(match.keep_bits, self.counts, self.group))
+                keep_h, keep_ready = _d2h_async(_all_gather_rows(match.keep_bits, self.counts, self.group), self.copy)
             else:
                 rank, f0, n_all = 0, 0, n_local
-                keep_h, keep_ready = _d2h_async(match.keep_bits)
-            finished = self._finish_prev(mark)  # warp(k) queued behind match(k+1)
+                keep_h, keep_ready = _d2h_async(match.keep_bits, self.copy)
+            prev, self._prev = self._prev, None
+            if prev is not None and self._device_maps():
+                self._warp_device_maps(prev, mark)  # warp(k) queued behind match(k+1)
             keep_ready.synchronize()
             # the global consensus; with counts, point lists of this rank's frames only
             cons = consensus_stage(keep_h.numpy(), n_tpl, n_all, cfg, self.logger if rank == 0 else None,
                                    frames=(f0, f0 + n_local) if self._sharded() else None)
+            pt_idx = cons.pt_idx if cons.pt_idx.size else np.zeros(1, np.int32)
+            lists = tuple(_h2d_async((cons.pt_off, pt_idx), self.dev, self.copy))
             mark("r0")
-            rr = ransac_stage(match, inp.kp_tpl, cons, cfg)
+            rr = ransac_stage(match, inp.kp_tpl, cons, cfg, lists_dev=lists)
             mark("r1")
             if self._sharded():
                 from .distributed import _all_gather_rows
 
-                params_h, params_ready = _d2h_async(_all_gather_rows(rr.params, self.counts, self.group))
+                params_h, params_ready = _d2h_async(_all_gather_rows(rr.params, self.counts, self.group), self.copy)
             else:
-                params_h, params_ready = _d2h_async(rr.params)
+                params_h, params_ready = _d2h_async(rr.params, self.copy)
             for t in (inp.frames, out):
                 if t is not None:
                     t.record_stream(self.stream)
+            finished = self._finish(prev, mark) if prev is not None else None
             self._prev = _SlabInFlight(inp, out, f0, match, cons, rr, params_h, params_ready)
         return finished
 
-    def _finish_prev(self, mark) -> Optional[SlabResult]:
-        p, self._prev = self._prev, None
-        if p is None:
-            return None
+    def _warp_device_maps(self, p: _SlabInFlight, mark) -> None:
+        mark("w0")
+        p.aligned = warp_frames(p.inp.frames, p.rr.params, out=p.out)
+        mark("w1")
+
+    def _finish(self, p: _SlabInFlight, mark) -> SlabResult:
+        """Host post-processing of slab p (VA:143-145) and the warps that need its maps."""
         p.params_ready.synchronize()
         affines, skipped, interpolated, eu = postprocess_affines(p.params_host.numpy(), self.cfg)
         n = p.inp.frames.shape[0]
-        # pinned + non_blocking: a pageable copy would wait for the device to drain
-        a = torch.from_numpy(np.ascontiguousarray(affines[p.f0:p.f0 + n], dtype=np.float64))
-        a = a.pin_memory().to(self.dev, non_blocking=True)
-        mark("w0")
-        aligned = warp_frames(p.inp.frames, a, out=p.out)
-        mark("w1")
+        local = np.asarray(affines[p.f0:p.f0 + n], dtype=np.float64)
+        if self._device_maps():
+            # frames without a model were warped to zeros: warp them with the filled maps
+            redo = np.zeros(n, bool)
+            sk = np.asarray(skipped, dtype=np.int64) - p.f0
+            redo[sk[(sk >= 0) & (sk < n)]] = True
+            for a, b in _runs(redo):
+                (m,) = _h2d_async((local[a:b],), self.dev, self.copy)
+                warp_frames(p.inp.frames[a:b], m, out=p.aligned[a:b])
+            aligned = p.aligned
+        else:
+            (m,) = _h2d_async((local,), self.dev, self.copy)
+            mark("w0")
+            aligned = warp_frames(p.inp.frames, m, out=p.out)
+            mark("w1")
         done = torch.cuda.Event()
         done.record(self.stream)
         res = SlabResult(aligned, affines, eu, skipped, interpolated, match=p.match, consensus=p.cons, ransac=p.rr)
@@ -332,11 +381,26 @@ class OverlappedSlabs:
 
     def flush(self, mark: Optional[Callable[[str], None]] = None) -> Optional[SlabResult]:
         """Queue the warp of the last submitted slab (None if there is none)."""
+        mark = mark or (lambda name: None)
+        p, self._prev = self._prev, None
+        if p is None:
+            return None
         with torch.cuda.stream(self.stream):
-            return self._finish_prev(mark or (lambda name: None))
+            if self._device_maps():
+                self._warp_device_maps(p, mark)
+            return self._finish(p, mark)
 
     def synchronize(self) -> None:
         self.stream.synchronize()
+        self.copy.synchronize()
+
+
+def _runs(mask: np.ndarray):
+    """Maximal runs [a, b) of True in a boolean vector."""
+    if not mask.any():
+        return []
+    d = np.diff(np.concatenate(([0], mask.astype(np.int8), [0])))
+    return list(zip(np.flatnonzero(d == 1).tolist(), np.flatnonzero(d == -1).tolist()))
 
 
 def align_streamed(frames_host: torch.Tensor, inp: SlabInputs, cfg: AlignConfig, slab: int = 64,

@@ -412,6 +412,24 @@ def test_warp_all_tile_paths_at_1080p(dev):
         assert np.array_equal(out[f], oracle.warp_affine_u16(img, M)), f
 
 
+def test_warp_nan_map_gives_zeros(dev):
+    """A frame without a RANSAC model (NaN map) warps to zeros (coordinates outside the
+    image under BORDER_CONSTANT); the pipeline re-warps it with the gap-filled map."""
+    rng = np.random.default_rng(5)
+    img = rng.integers(1, 65536, (64, 136)).astype(np.uint16)
+    fr = torch.from_numpy(np.broadcast_to(img, (3, 64, 136)).copy()).to(dev)
+    M = np.stack([synthetic.rigid(0.01, 1.5, -2.0)] * 3)
+    M[1, 0, 2] = np.nan
+    for persp in (False, True):
+        if persp:
+            Mp = np.concatenate([M, np.tile([[[0.0, 0.0, 1.0]]], (3, 1, 1))], axis=1)
+            out = stages.warp_perspective_u16(fr, _t(Mp, dev)).cpu().numpy()
+        else:
+            out = stages.warp_affine_u16(fr, _t(M, dev)).cpu().numpy()
+        assert not out[1].any()
+        assert out[0].any() and np.array_equal(out[0], out[2])
+
+
 @pytest.mark.parametrize("shape", [(3, 120, 256, 3), (2, 96, 136, 4), (1, 2160, 3840, 3)])
 def test_warp_multichannel_vector_staging(dev, shape):
     """C = 3 / 4 with W % 8 == 0: 16-byte staging of interleaved rows into 128 x 24

@@ -137,6 +137,13 @@ def test_overlapped_slabs_equal_align_slab(dev):
     slabs = []
     for seed in (11, 12, 13):
         ks = synthetic.make_keypoints(F, 300, 32, (H, W), seed=seed)
+        # frames whose descriptors are all one row pass no ratio test (d1 == d2), so they
+        # get no model: leading, interior and trailing gaps (host interpolation, then a
+        # second warp of those frames)
+        rng = np.random.default_rng(seed)
+        for f in {11: (0, 1, 7), 12: (9, 10, 11, F - 1), 13: ()}[seed]:
+            a, b = ks.q_off[f], ks.q_off[f + 1]
+            ks.des_q[a:b] = rng.integers(0, 256, (1, 32), dtype=np.uint8)
         base = synthetic.make_texture((H, W), seed=seed)
         frames = torch.from_numpy(np.broadcast_to(base, (F, H, W)).copy()).to(dev)
         slabs.append(pipeline.SlabInputs(frames, torch.from_numpy(ks.des_tpl).to(dev),
@@ -150,6 +157,7 @@ def test_overlapped_slabs_equal_align_slab(dev):
     got = got[1:] + [ov.flush()]
     assert ov.flush() is None
     ov.synchronize()
+    assert [len(r.skipped) for r in ref] == [3, 4, 0]
     for r, g in zip(ref, got):
         assert np.array_equal(r.affines, g.affines, equal_nan=True)
         assert r.skipped == g.skipped and r.interpolated == g.interpolated

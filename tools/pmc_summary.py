@@ -1,6 +1,6 @@
 """Aggregate rocprofv3 --pmc CSV passes (tools/pmc_warp.sh output) per kernel dispatch.
 
-    python tools/pmc_summary.py gpurun_out/pmc [--by-kernel] [--json out.json]
+    python tools/pmc_summary.py gpurun_out/pmc [--by-kernel] [--json out.json] [--sha <commit>]
 With --by-kernel (tools/pmc_kernels.sh output) the means are per kernel name, with the
 derived utilisations (SQ_* cycle counters are quad-cycles; GRBM_GUI_ACTIVE is summed
 over the 8 XCDs, so the dispatch's cycles are GRBM_GUI_ACTIVE / 8; 256 CUs x 4 SIMDs).
@@ -20,8 +20,9 @@ def load(d):
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for p in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
         for r in csv.DictReader(open(p)):
-            per[(os.path.basename(os.path.dirname(p)), int(r["Dispatch_Id"]))][r["Counter_Name"]] += float(
-                r["Counter_Value"])
+            key = (os.path.basename(os.path.dirname(p)), int(r["Dispatch_Id"]))
+            per[key][r["Counter_Name"]] += float(r["Counter_Value"])
+            per[key]["_dispatch_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
     out = collections.defaultdict(list)
     for (pas, disp), ctrs in sorted(per.items()):
         for c, v in ctrs.items():
@@ -85,12 +86,18 @@ def main_by_kernel(d, js=None):
         json.dump(res, open(js, "w"), indent=1)
 
 
-def main(d, js=None):
+def main(d, js=None, sha=None):
     agg = load(d)
     mean = {c: sum(v) / len(v) for c, v in agg.items()}
+    disp_ns = mean.pop("_dispatch_ns", None)
     for c in sorted(mean):
         print(f"{c:28s} {mean[c]:.6g}")
-    res = {"counters_mean_per_dispatch": mean}
+    res = {"commit": sha, "counters_mean_per_dispatch": mean,
+           "kernel_avg_ms": round(disp_ns / 1e6, 4) if disp_ns else None}
+    if disp_ns:
+        print(f"kernel avg duration in the PMC passes: {disp_ns / 1e6:.4f} ms (profiled runs clock lower)")
+    if sha:
+        print(f"commit: {sha}")
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         rd = 2 * mean["FETCH_SIZE"] * 1024
         wr = mean["WRITE_SIZE"] * 1024
@@ -103,4 +110,8 @@ def main(d, js=None):
 if __name__ == "__main__":
     a = sys.argv[1:]
     js = a[a.index("--json") + 1] if "--json" in a else None
-    (main_by_kernel if "--by-kernel" in a else main)(a[0], js)
+    sha = a[a.index("--sha") + 1] if "--sha" in a else None
+    if "--by-kernel" in a:
+        main_by_kernel(a[0], js)
+    else:
+        main(a[0], js, sha)
