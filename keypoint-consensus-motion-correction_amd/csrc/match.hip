@@ -3,7 +3,8 @@
 // Reference: VA:194-214 (cv2.BFMatcher(crossCheck=False).knnMatch(des_template,
 // des_query, k=2), best-match reorder, ratio filter, median displacement filter).
 //
-// knn2_l2u8_kernel -- one workgroup = 256 template rows x one frame.
+// knn2_l2u8_kernel -- persistent: a workgroup keeps 256 / 512 template rows in registers
+//   and matches them against a strided set of frames.
 //   The distance is an exact integer contraction, so it runs on the int8 matrix
 //   cores.  With x = a - 128 (template) and y = 127 - b (frame), both int8,
 //   a - b = x + y + 1, so SSD = T + Q + 2 x.y with T = sum(x^2 + 2x) + D per template
@@ -154,12 +155,17 @@ __device__ __forceinline__ void land_row(uint8_t* qrow, uint32_t* qk, int r, boo
   *qk = real ? (((uint32_t)nb << 8) | (uint32_t)r) : kPad;
 }
 
-// WAVES = 8: 512 template rows per workgroup share each staged chunk (half the staging
-// and barrier work per tile of the 4-wave form, which n_tpl <= 256 uses).
+// Persistent, template-stationary: workgroup (tg, g) keeps template rows
+// [tg * kTplPerWG, +kTplPerWG) in registers for the whole launch and walks frames g,
+// g + G, g + 2G, ... (G workgroups per template group), so the template is loaded once per
+// workgroup instead of once per frame, and the loads of the next 256-row chunk -- which
+// may be the next frame's first -- are in flight while the current chunk is matched.
+// WAVES = 8: 512 template rows share each staged chunk (n_tpl > 256); WAVES = 4 otherwise.
 template <int DP, int WAVES>
 __global__ __launch_bounds__(KnnShape<WAVES>::kThreads) void knn2_l2u8_kernel(
     const uint8_t* __restrict__ des_tpl, int n_tpl, int D, const uint8_t* __restrict__ des_q,
-    const int32_t* __restrict__ q_off, int32_t* __restrict__ out_idx, float* __restrict__ out_dist) {
+    const int32_t* __restrict__ q_off, int n_frames, int n_tg, int32_t* __restrict__ out_idx,
+    float* __restrict__ out_dist) {
   constexpr int KSTEPS = DP / 32;
   constexpr int ROWB = DP + 16;  // padded LDS row stride (bytes)
   // double-buffered chunks: one barrier per chunk (a wave writes chunk c + 1 only after
@@ -167,18 +173,16 @@ __global__ __launch_bounds__(KnnShape<WAVES>::kThreads) void knn2_l2u8_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t qbuf[2][kQChunk * ROWB];
   __shared__ __attribute__((aligned(16))) uint32_t qkey[2][kQChunk];
 
-  // the template blocks of one frame on one XCD (they stage the same frame rows)
-  const int tile = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
-  const int f = tile / gridDim.x, tblk = tile - f * gridDim.x;
+  // the template groups of a frame get consecutive ids of one XCD's run: they stage the
+  // same frame rows, which then stay in that XCD's L2
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int tg = id % n_tg, g = id / n_tg, G = gridDim.x / n_tg;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int c = lane & 31;   // MFMA column (template row within a block)
   const int h = lane >> 5;   // k-half of the fragment / row group of the output
-  const int q_begin = q_off[f];
-  const int n_q = q_off[f + 1] - q_begin;
-  const uint8_t* qrows = des_q + (size_t)q_begin * D;
-  const int last_row = q_off[gridDim.y] - 1 - q_begin;  // des_q's last row, frame-relative
+  const int last_global = q_off[n_frames] - 1;  // des_q's last row
 
   // ---- template fragments (B operand) and T = sum(x^2 + 2x) + D, kept in registers
   v4i bfrag[kBlocksPerWave][KSTEPS];
@@ -186,7 +190,7 @@ __global__ __launch_bounds__(KnnShape<WAVES>::kThreads) void knn2_l2u8_kernel(
   int tpl_row[kBlocksPerWave];
 #pragma unroll
   for (int b = 0; b < kBlocksPerWave; ++b) {
-    const int i = tblk * KnnShape<WAVES>::kTplPerWG + (wave * kBlocksPerWave + b) * 32 + c;
+    const int i = tg * KnnShape<WAVES>::kTplPerWG + (wave * kBlocksPerWave + b) * 32 + c;
     tpl_row[b] = i;
     int na = 0;
 #pragma unroll
@@ -205,90 +209,108 @@ __global__ __launch_bounds__(KnnShape<WAVES>::kThreads) void knn2_l2u8_kernel(
     tk[b] = na + D;
   }
 
-  unsigned long long g1[kBlocksPerWave], g2[kBlocksPerWave];
-#pragma unroll
-  for (int b = 0; b < kBlocksPerWave; ++b) g1[b] = g2[b] = kNoKey64;
-
-  // one thread per staged row (threads 0..255; in 8-wave workgroups the other half
-  // waits at the barrier -- splitting rows over two threads measured no faster)
-  uint4 pf[RowPieces<DP>::kNP];
-  if (n_q > 0 && tid < kQChunk) {
-    const int r = min(tid, n_q - 1);
-    issue_row<DP>(qrows + (size_t)r * D, D, r == last_row, pf);
-  }
-  for (int q0 = 0, buf = 0; q0 < n_q; q0 += kQChunk, buf ^= 1) {
-    const int cnt = min(kQChunk, n_q - q0);
-    const int rows = (cnt + 31) & ~31;
-    // ---- stage frame descriptors [q0, q0+cnt) as int8 127 - b, zero-padded to DP columns
-    if (tid < rows) land_row<DP>(&qbuf[buf][tid * ROWB], &qkey[buf][tid], tid, tid < cnt, D, pf);
-    __syncthreads();
-    if (q0 + kQChunk < n_q && tid < kQChunk) {
-      const int r = q0 + kQChunk + min(tid, n_q - q0 - kQChunk - 1);
-      issue_row<DP>(qrows + (size_t)r * D, D, r == last_row, pf);
+  // ---- the item sequence: the 256-row chunks of frames g, g + G, ... that have rows
+  // (a frame without rows still gets its epilogue).  nxt = the item whose loads are in
+  // flight: frame nf, first row nq0 (nf >= n_frames: none).
+  auto advance = [&](int f, int q0) -> int2 {  // the item after (f, q0)
+    if (q0 + kQChunk < q_off[f + 1] - q_off[f]) return make_int2(f, q0 + kQChunk);
+    for (f += G; f < n_frames && q_off[f + 1] == q_off[f]; f += G) {
     }
-    const uint8_t* qb = qbuf[buf];
-    const uint32_t* qkb = qkey[buf];
-    uint32_t b1[kBlocksPerWave][2], b2[kBlocksPerWave][2];  // [even | odd accumulator]
+    return make_int2(f, 0);
+  };
+  auto issue = [&](int2 it, uint4 (&pf)[RowPieces<DP>::kNP]) {
+    if (it.x < n_frames && tid < kQChunk) {
+      const int qb = q_off[it.x], nq = q_off[it.x + 1] - qb;
+      const int r = qb + it.y + min(tid, nq - it.y - 1);
+      issue_row<DP>(des_q + (size_t)r * D, D, r == last_global, pf);
+    }
+  };
+  uint4 pf[RowPieces<DP>::kNP];
+  int2 nxt = make_int2(g, 0);  // the first item: frame g's first chunk, or the next frame with rows
+  if (g < n_frames && q_off[g + 1] == q_off[g]) nxt = advance(g, 0);
+  issue(nxt, pf);
+  int buf = 0;
+  for (int f = g; f < n_frames; f += G) {
+    const int n_q = q_off[f + 1] - q_off[f];
+    unsigned long long g1[kBlocksPerWave], g2[kBlocksPerWave];
 #pragma unroll
-    for (int b = 0; b < kBlocksPerWave; ++b) b1[b][0] = b2[b][0] = b1[b][1] = b2[b][1] = kNoKey;
-    // ---- MFMA tiles of 32 frame rows
-    for (int t0 = 0; t0 < rows; t0 += 32) {
-      v4i afrag[KSTEPS];
+    for (int b = 0; b < kBlocksPerWave; ++b) g1[b] = g2[b] = kNoKey64;
+    for (int q0 = 0; q0 < n_q; q0 += kQChunk, buf ^= 1) {
+      const int cnt = min(kQChunk, n_q - q0);
+      const int rows = (cnt + 31) & ~31;
+      // ---- stage frame descriptors [q0, q0+cnt) as int8 127 - b, zero-padded to DP columns
+      if (tid < rows) land_row<DP>(&qbuf[buf][tid * ROWB], &qkey[buf][tid], tid, tid < cnt, D, pf);
+      __syncthreads();
+      nxt = advance(f, q0);
+      issue(nxt, pf);
+      const uint8_t* qb = qbuf[buf];
+      const uint32_t* qkb = qkey[buf];
+      uint32_t b1[kBlocksPerWave][2], b2[kBlocksPerWave][2];  // [even | odd accumulator]
 #pragma unroll
-      for (int kk = 0; kk < KSTEPS; ++kk)
-        afrag[kk] = *reinterpret_cast<const v4i*>(&qb[(t0 + c) * ROWB + 32 * kk + 16 * h]);
-      // rows of this lane's 16 accumulators: t0 + (r&3) + 8*(r>>2) + 4*h
-      uint32_t qk[16];
+      for (int b = 0; b < kBlocksPerWave; ++b) b1[b][0] = b2[b][0] = b1[b][1] = b2[b][1] = kNoKey;
+      // ---- MFMA tiles of 32 frame rows
+      for (int t0 = 0; t0 < rows; t0 += 32) {
+        v4i afrag[KSTEPS];
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
+        for (int kk = 0; kk < KSTEPS; ++kk)
+          afrag[kk] = *reinterpret_cast<const v4i*>(&qb[(t0 + c) * ROWB + 32 * kk + 16 * h]);
+        // rows of this lane's 16 accumulators: t0 + (r&3) + 8*(r>>2) + 4*h
+        uint32_t qk[16];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) qk[4 * g + s] = qkb[t0 + 8 * g + 4 * h + s];
+        for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) qk[4 * gg + s2] = qkb[t0 + 8 * gg + 4 * h + s2];
+        // every block's MFMAs first, so that block b + 1's matrix work overlaps block b's
+        // top-2 epilogue instead of the epilogue waiting out each chain's latency
+        v16i acc[kBlocksPerWave];
+#pragma unroll
+        for (int b = 0; b < kBlocksPerWave; ++b) {
+          acc[b] = v16i{};
+#pragma unroll
+          for (int kk = 0; kk < KSTEPS; ++kk)  // acc = x.y
+            acc[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag[kk], bfrag[b][kk], acc[b], 0, 0, 0);
+        }
+#pragma unroll
+        for (int b = 0; b < kBlocksPerWave; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) top2_insert(b1[b][r & 1], b2[b][r & 1], ((uint32_t)acc[b][r] << 9) + qk[r]);
+      }
+      // ---- fold the chunk's top-2 (local indices) into the frame's 64-bit top-2: the
+      // even / odd pairs merge in 32 bits first (c1 <= c2 = the chunk's two smallest keys)
 #pragma unroll
       for (int b = 0; b < kBlocksPerWave; ++b) {
-        v16i acc = {};
+        const uint32_t c1 = min(b1[b][0], b1[b][1]);
+        const uint32_t c2 = min(max(b1[b][0], b1[b][1]), min(b2[b][0], b2[b][1]));
+        const uint32_t ks[2] = {c1, c2};
 #pragma unroll
-        for (int kk = 0; kk < KSTEPS; ++kk)  // acc = x.y
-          acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag[kk], bfrag[b][kk], acc, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) top2_insert(b1[b][r & 1], b2[b][r & 1], ((uint32_t)acc[r] << 9) + qk[r]);
+        for (int k = 0; k < 2; ++k)
+          if (ks[k] < kPad) {
+            const uint32_t ssd = (ks[k] >> 8) + (uint32_t)(tk[b] - kBias);
+            top2_insert64(g1[b], g2[b], ((unsigned long long)ssd << 32) | (uint32_t)(q0 + (int)(ks[k] & 255u)));
+          }
       }
     }
-    // ---- fold the chunk's top-2 (local indices) into the frame's 64-bit top-2: the
-    // even / odd pairs merge in 32 bits first (c1 <= c2 = the chunk's two smallest keys)
+    // ---- merge the two row halves (lanes l and l^32 own the same template column)
 #pragma unroll
     for (int b = 0; b < kBlocksPerWave; ++b) {
-      const uint32_t c1 = min(b1[b][0], b1[b][1]);
-      const uint32_t c2 = min(max(b1[b][0], b1[b][1]), min(b2[b][0], b2[b][1]));
-      const uint32_t ks[2] = {c1, c2};
+      const unsigned long long o1 = (unsigned long long)__shfl_xor((long long)g1[b], 32);
+      const unsigned long long o2 = (unsigned long long)__shfl_xor((long long)g2[b], 32);
+      unsigned long long m1 = g1[b], m2 = g2[b];
+      top2_insert64(m1, m2, o1);
+      top2_insert64(m1, m2, o2);
+      const int i = tpl_row[b];
+      if (h == 0 && i < n_tpl) {
+        const size_t o = ((size_t)f * n_tpl + i) * 2;
+        const unsigned long long ms[2] = {m1, m2};
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
-        if (ks[k] < kPad) {
-          const uint32_t ssd = (ks[k] >> 8) + (uint32_t)(tk[b] - kBias);
-          top2_insert64(g1[b], g2[b], ((unsigned long long)ssd << 32) | (uint32_t)(q0 + (int)(ks[k] & 255u)));
-        }
-    }
-  }
-
-  // ---- merge the two row halves (lanes l and l^32 own the same template column)
-#pragma unroll
-  for (int b = 0; b < kBlocksPerWave; ++b) {
-    const unsigned long long o1 = (unsigned long long)__shfl_xor((long long)g1[b], 32);
-    const unsigned long long o2 = (unsigned long long)__shfl_xor((long long)g2[b], 32);
-    unsigned long long m1 = g1[b], m2 = g2[b];
-    top2_insert64(m1, m2, o1);
-    top2_insert64(m1, m2, o2);
-    const int i = tpl_row[b];
-    if (h == 0 && i < n_tpl) {
-      const size_t o = ((size_t)f * n_tpl + i) * 2;
-      const unsigned long long ms[2] = {m1, m2};
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        if (ms[k] == kNoKey64) {
-          out_idx[o + k] = -1;
-          out_dist[o + k] = FLT_MAX;
-        } else {
-          out_idx[o + k] = (int32_t)(ms[k] & 0xffffffffull);
-          out_dist[o + k] = sqrtf((float)(ms[k] >> 32));
+        for (int k = 0; k < 2; ++k) {
+          if (ms[k] == kNoKey64) {
+            out_idx[o + k] = -1;
+            out_dist[o + k] = FLT_MAX;
+          } else {
+            out_idx[o + k] = (int32_t)(ms[k] & 0xffffffffull);
+            out_dist[o + k] = sqrtf((float)(ms[k] >> 32));
+          }
         }
       }
     }
@@ -395,22 +417,37 @@ __global__ __launch_bounds__(kFilterThreads) void match_filter_kernel(
   }
 }
 
+// Workgroups that fill the device once (2 per CU at 8 waves, 4 at 4 waves: the kernels'
+// ~100 VGPRs allow 4 waves per SIMD), split evenly over the template groups.
+int knn_grid(int n_tg, int n_frames, int wgs_per_cu) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  const int G = std::max(1, std::min(n_frames, cus * wgs_per_cu / n_tg));
+  return n_tg * G;
+}
+
 int launch_knn(const uint8_t* des_tpl, int n_tpl, int D, const uint8_t* des_q, const int32_t* q_off,
                int n_frames, int max_nq, int32_t* out_idx, float* out_dist, hipStream_t s) {
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
   (void)max_nq;
   if (n_tpl > 256) {
-    dim3 grid(ceil_div(n_tpl, KnnShape<8>::kTplPerWG), n_frames);
+    const int n_tg = ceil_div(n_tpl, KnnShape<8>::kTplPerWG);
+    const dim3 grid(knn_grid(n_tg, n_frames, 2));
     if (D <= 32)
-      hipLaunchKernelGGL((knn2_l2u8_kernel<32, 8>), grid, dim3(512), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+      hipLaunchKernelGGL((knn2_l2u8_kernel<32, 8>), grid, dim3(512), 0, s, des_tpl, n_tpl, D, des_q, q_off, n_frames, n_tg, out_idx, out_dist);
     else
-      hipLaunchKernelGGL((knn2_l2u8_kernel<64, 8>), grid, dim3(512), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+      hipLaunchKernelGGL((knn2_l2u8_kernel<64, 8>), grid, dim3(512), 0, s, des_tpl, n_tpl, D, des_q, q_off, n_frames, n_tg, out_idx, out_dist);
   } else {
-    dim3 grid(ceil_div(n_tpl, KnnShape<4>::kTplPerWG), n_frames);
+    const int n_tg = ceil_div(n_tpl, KnnShape<4>::kTplPerWG);
+    const dim3 grid(knn_grid(n_tg, n_frames, 4));
     if (D <= 32)
-      hipLaunchKernelGGL((knn2_l2u8_kernel<32, 4>), grid, dim3(256), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+      hipLaunchKernelGGL((knn2_l2u8_kernel<32, 4>), grid, dim3(256), 0, s, des_tpl, n_tpl, D, des_q, q_off, n_frames, n_tg, out_idx, out_dist);
     else
-      hipLaunchKernelGGL((knn2_l2u8_kernel<64, 4>), grid, dim3(256), 0, s, des_tpl, n_tpl, D, des_q, q_off, out_idx, out_dist);
+      hipLaunchKernelGGL((knn2_l2u8_kernel<64, 4>), grid, dim3(256), 0, s, des_tpl, n_tpl, D, des_q, q_off, n_frames, n_tg, out_idx, out_dist);
   }
   return launch_check("knn2_l2u8_kernel");
 }
