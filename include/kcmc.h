@@ -101,6 +101,21 @@ int kcmc_match_frames(kcmc_ctx* ctx, const uint8_t* des_tpl_dev, const double* k
                       double* out_kp_ordered_dev, uint32_t* out_keep_bits_dev,
                       int32_t* out_counts_dev, kcmc_stream_t stream);
 
+/* -------------------------------------------------- K1 opt-in: binary descriptors, NORM_HAMMING
+ * BFMatcher(NORM_HAMMING).knnMatch(k=2): distance = number of differing bits (as a float),
+ * ties to the lower frame index.  NOT the reference's matcher (VA:194 uses the default
+ * NORM_L2, kcmc_knn2_l2u8); for binary ORB/BRIEF/AKAZE descriptors where Hamming is
+ * wanted.  1 <= D <= 64 bytes, fewer than 2^21 rows per frame.  Arguments as
+ * kcmc_knn2_l2u8 / kcmc_match_frames (the filters VA:196-214 are the same). */
+int kcmc_knn2_hamming(kcmc_ctx* ctx, const uint8_t* des_tpl_dev, int n_tpl, int D, const uint8_t* des_q_dev,
+                      const int32_t* q_off_dev, int n_frames, int max_nq, int32_t* out_idx_dev,
+                      float* out_dist_dev, kcmc_stream_t stream);
+int kcmc_match_frames_hamming(kcmc_ctx* ctx, const uint8_t* des_tpl_dev, const double* kp_tpl_dev, int n_tpl,
+                              int D, const uint8_t* des_q_dev, const double* kp_q_dev, const int32_t* q_off_dev,
+                              int n_frames, int max_nq, double ratio, double d_lo, double d_hi,
+                              int32_t* out_idx_dev, float* out_dist_dev, double* out_kp_ordered_dev,
+                              uint32_t* out_keep_bits_dev, int32_t* out_counts_dev, kcmc_stream_t stream);
+
 /* -------------------------------------------------- K1 extension: float descriptors
  * BFMatcher(NORM_L2).knnMatch(k=2) on float32 descriptors (BASELINE config 5,
  * SIFT-style; the reference's AKAZE/BRISK descriptors are uint8, VA:22-25).  Distance:

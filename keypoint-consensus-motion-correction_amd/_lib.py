@@ -30,6 +30,8 @@ EXPORTED_SYMBOLS = (
     "kcmc_match_frames",
     "kcmc_knn2_l2f32",
     "kcmc_match_frames_f32",
+    "kcmc_knn2_hamming",
+    "kcmc_match_frames_hamming",
     "kcmc_consensus",
     "kcmc_consensus_slice",
     "kcmc_hypothesis_table",
@@ -80,6 +82,8 @@ _SIGNATURES = {
     "kcmc_match_frames": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
     "kcmc_knn2_l2f32": ([P, P, I, I, P, P, I, I, P, P, P], I),
     "kcmc_match_frames_f32": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
+    "kcmc_knn2_hamming": ([P, P, I, I, P, P, I, I, P, P, P], I),
+    "kcmc_match_frames_hamming": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
     "kcmc_consensus": ([P, I, I, I, I, P, P, P, P, P], I),
     "kcmc_consensus_slice": ([P, I, I, I, I, I, I, P, P, P, P, P], I),
     "kcmc_hypothesis_table": ([I, I, U32, I, P], I),
@@ -126,7 +130,11 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         except OSError as e:
             raise KcmcLibraryError(f"failed to load {path}: {e}") from e
         for name, (args, res) in _SIGNATURES.items():
-            fn = getattr(L, name)
+            fn = getattr(L, name, None)
+            if fn is None:
+                if os.environ.get("KCMC_LIB_PATH"):  # an older A/B build: its missing entries stay unbound
+                    continue
+                raise KcmcLibraryError(f"{path}: missing symbol {name} (stale build?)")
             fn.argtypes = args
             fn.restype = res
         if L.kcmc_abi_version() != ABI_VERSION:

@@ -39,6 +39,9 @@ class AlignConfig:
     # Extension (BASELINE configs 3-5): the skimage model class RANSAC fits.  The
     # reference always uses "euclidean" (EuclideanTransform, VA:311).
     ransac_model: str = "euclidean"     # "euclidean" | "affine" | "projective"
+    # Opt-in (not the reference's matcher): BFMatcher norm, "l2" (the reference's
+    # cv2.BFMatcher() default, VA:194) or "hamming" (NORM_HAMMING for binary descriptors).
+    match_norm: str = "l2"
 
     @property
     def effective_frame_skip(self) -> int:
@@ -93,7 +96,7 @@ def log_frame_counts(logger: logging.Logger, counts: np.ndarray, first_index: in
 
 def match_stage(inp: SlabInputs, cfg: AlignConfig) -> stages.MatchResult:
     return stages.match_frames(inp.des_tpl, inp.kp_tpl, inp.des_q, inp.kp_q, inp.q_off, inp.q_off_host,
-                               ratio=cfg.ratio, d_lo=cfg.d_lo, d_hi=cfg.d_hi)
+                               ratio=cfg.ratio, d_lo=cfg.d_lo, d_hi=cfg.d_hi, norm=cfg.match_norm)
 
 
 def consensus_stage(keep_bits_host: np.ndarray, n_tpl: int, n_frames: int, cfg: AlignConfig,

@@ -97,6 +97,22 @@ def knn2_l2u8(des_tpl: torch.Tensor, des_q: torch.Tensor, q_off: torch.Tensor, m
     return idx, dist
 
 
+def knn2_hamming(des_tpl: torch.Tensor, des_q: torch.Tensor, q_off: torch.Tensor, max_nq: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """cv2.BFMatcher(cv2.NORM_HAMMING).knnMatch(des_tpl, des_q[frame], k=2) for every frame
+    (binary uint8 descriptors; opt-in, the reference's matcher is NORM_L2, VA:194)."""
+    dev = _device_of(des_tpl)
+    _require(des_tpl, "des_tpl", torch.uint8, dev, 2)
+    _require(des_q, "des_q", torch.uint8, dev, 2)
+    _require(q_off, "q_off", torch.int32, dev, 1)
+    n_tpl, D = des_tpl.shape
+    F = q_off.numel() - 1
+    idx = torch.empty((F, n_tpl, 2), dtype=torch.int32, device=dev)
+    dist = torch.empty((F, n_tpl, 2), dtype=torch.float32, device=dev)
+    _lib.check(_lib.load().kcmc_knn2_hamming(_ctx(dev).handle, _ptr(des_tpl), n_tpl, D, _ptr(des_q), _ptr(q_off), F,
+                                             int(max_nq), _ptr(idx), _ptr(dist), _stream(dev)))
+    return idx, dist
+
+
 def match_frames(
     des_tpl: torch.Tensor,
     kp_tpl: torch.Tensor,
@@ -107,11 +123,17 @@ def match_frames(
     ratio: float = 0.75,
     d_lo: float = 0.5,
     d_hi: float = 2.0,
+    norm: str = "l2",
 ) -> MatchResult:
     """VA:194-214 for every frame: knn k=2 + reorder + ratio + median filters.
-    uint8 descriptors (the reference's) or float32 (SIFT-style extension)."""
+    uint8 descriptors (the reference's) or float32 (SIFT-style extension); ``norm``
+    "hamming" (uint8 only) is the opt-in NORM_HAMMING matcher for binary descriptors."""
+    if norm not in ("l2", "hamming"):
+        raise ValueError(f"norm must be 'l2' or 'hamming' (got {norm!r})")
     dev = _device_of(des_tpl)
     f32 = des_tpl.dtype == torch.float32
+    if norm == "hamming" and f32:
+        raise TypeError("NORM_HAMMING needs binary (uint8) descriptors")
     _require(des_tpl, "des_tpl", torch.float32 if f32 else torch.uint8, dev, 2)
     _require(kp_tpl, "kp_tpl", torch.float64, dev, 2)
     _require(des_q, "des_q", torch.float32 if f32 else torch.uint8, dev, 2)
@@ -136,7 +158,7 @@ def match_frames(
         counts=torch.empty((F, 4), dtype=torch.int32, device=dev),
     )
     L = _lib.load()
-    fn = L.kcmc_match_frames_f32 if f32 else L.kcmc_match_frames
+    fn = L.kcmc_match_frames_f32 if f32 else (L.kcmc_match_frames_hamming if norm == "hamming" else L.kcmc_match_frames)
     _lib.check(fn(
         _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F,
         int(nq.max()) if F else 0, float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist),

@@ -114,6 +114,10 @@ class VideoAligner:
     # (AffineTransform, min_samples 3) or "projective" (ProjectiveTransform, min_samples 4,
     # frames warped with warpPerspective).
     RANSAC_MODEL = "euclidean"
+    # New (opt-in, not the reference's matcher): the BFMatcher norm -- "l2" (the
+    # reference's cv2.BFMatcher() default, VA:194) or "hamming" (NORM_HAMMING, for binary
+    # ORB/BRIEF/AKAZE descriptors; csrc/match_hamming.hip).
+    MATCH_NORM = "l2"
 
     def __init__(self, logger: LoggerAdapter = None):
         self.logger = logger
@@ -143,7 +147,8 @@ class VideoAligner:
             ratio=cls.DESCRIPTOR_DISTANCE_RATIO_THRESH, d_lo=d_lo, d_hi=d_hi, ransac_trials=cls.RANSAC_MAX_TRIALS,
             ransac_threshold=float(cls.RANSAC_RESIDUAL_THRESH), ransac_min_samples=cls.RANSAC_MIN_SAMPLES,
             seed=cls.RANDOM_SEED, spatial_rate=cls.SPATIAL_DOWNSAMPLE_RATE,
-            frame_downsample_rate=int(frame_downsample_rate), ransac_model=cls.RANSAC_MODEL)
+            frame_downsample_rate=int(frame_downsample_rate), ransac_model=cls.RANSAC_MODEL,
+            match_norm=cls.MATCH_NORM)
 
     # ------------------------------------------------------------- public API
     def align_images(

@@ -24,6 +24,7 @@
  * fma() is written explicitly, mirroring the reference platform.
  */
 #include <float.h>
+#include <limits.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -74,6 +75,45 @@ int kcmc_oracle_knn2_l2u8(const uint8_t* query, int n_query, const uint8_t* trai
     out_idx[2 * i + 1] = bi[1];
     out_dist[2 * i] = bd[0];
     out_dist[2 * i + 1] = bd[1];
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* K1 opt-in extension oracle: BFMatcher(NORM_HAMMING).knnMatch(k=2) on binary  */
+/* descriptors (ORB / BRIEF / AKAZE-MLDB bytes).  NOT the reference's matcher:  */
+/* VA:194 constructs cv2.BFMatcher with its default NORM_L2.  OpenCV's          */
+/* normHamming counts the differing bits (an integer), batchDistance keeps the  */
+/* K best by the same insertion as NORM_L2 (strict >, so the lower train index  */
+/* wins ties), and DMatch.distance holds the count as a float.                   */
+/* ------------------------------------------------------------------------- */
+int kcmc_oracle_knn2_hamming(const uint8_t* query, int n_query, const uint8_t* train, int n_train, int D,
+                             int32_t* out_idx, float* out_dist) {
+  if (n_query < 0 || n_train < 0 || D <= 0) return -1;
+  for (int i = 0; i < n_query; ++i) {
+    const uint8_t* a = query + (size_t)i * D;
+    int bd[2] = {INT_MAX, INT_MAX};
+    int32_t bi[2] = {-1, -1};
+    for (int j = 0; j < n_train; ++j) {
+      const uint8_t* b = train + (size_t)j * D;
+      int d = 0;
+      for (int k = 0; k < D; ++k) d += __builtin_popcount((unsigned)(a[k] ^ b[k]));
+      if (d < bd[1]) {
+        if (d < bd[0]) {
+          bd[1] = bd[0];
+          bi[1] = bi[0];
+          bd[0] = d;
+          bi[0] = j;
+        } else {
+          bd[1] = d;
+          bi[1] = j;
+        }
+      }
+    }
+    for (int k = 0; k < 2; ++k) {
+      out_idx[2 * i + k] = bi[k];
+      out_dist[2 * i + k] = bi[k] < 0 ? FLT_MAX : (float)bd[k];
+    }
   }
   return 0;
 }

@@ -54,6 +54,7 @@ def lib() -> ctypes.CDLL:
         P = ctypes.c_void_p
         i = ctypes.c_int
         L.kcmc_oracle_knn2_l2u8.argtypes = [P, i, P, i, i, P, P]
+        L.kcmc_oracle_knn2_hamming.argtypes = [P, i, P, i, i, P, P]
         L.kcmc_oracle_warp_affine_u16.argtypes = [P, i, i, i, P, i, P, i, i]
         L.kcmc_oracle_invert_affine.argtypes = [P, P]
         L.kcmc_oracle_pairwise_sum.argtypes = [P, i]
@@ -79,6 +80,20 @@ def _p(a: np.ndarray):
 
 
 # --------------------------------------------------------------------------- K1
+def knn2_hamming(query: np.ndarray, train: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """OpenCV ``BFMatcher(cv2.NORM_HAMMING).knnMatch(query, train, k=2)`` on binary (uint8)
+    descriptors: the opt-in extension matcher (the reference itself uses NORM_L2, VA:194).
+    Same outputs as ``knn2_l2u8`` with integer bit-count distances."""
+    q = np.ascontiguousarray(query, dtype=np.uint8)
+    t = np.ascontiguousarray(train, dtype=np.uint8)
+    assert q.ndim == 2 and t.ndim == 2 and q.shape[1] == t.shape[1]
+    idx = np.empty((q.shape[0], 2), np.int32)
+    dist = np.empty((q.shape[0], 2), np.float32)
+    rc = lib().kcmc_oracle_knn2_hamming(_p(q), q.shape[0], _p(t), t.shape[0], q.shape[1], _p(idx), _p(dist))
+    assert rc == 0
+    return idx, dist
+
+
 def knn2_l2u8(query: np.ndarray, train: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
     """OpenCV ``BFMatcher().knnMatch(query, train, k=2)`` for uint8 descriptors.
 
