@@ -32,6 +32,9 @@ SHAPES = {
     "c3": (2500, 500, 61, "u8", 512, 512),
     "c4": (625, 4096, 61, "u8", 2160, 3840),
     "c5": (500, 4096, 128, "f32", 1080, 1920),
+    # the opt-in NORM_HAMMING matcher on c2's shape (VALU popcount, priced against the
+    # VALU issue rate: 2 * D/4 + 3 instructions per distance)
+    "c2h": (2000, 500, 32, "hamming", 1080, 1920),
 }
 
 
@@ -56,17 +59,22 @@ def main():
     out = {"device": torch.cuda.get_device_name(0)}
     for name in args.configs.split(","):
         F, n_tpl, D, desc, H, W = SHAPES[name]
-        ks = synthetic.make_keypoints(F, n_tpl, D, (H, W), seed=3, frame_seed=0, descriptor=desc)
+        ks = synthetic.make_keypoints(F, n_tpl, D, (H, W), seed=3, frame_seed=0,
+                                      descriptor="u8" if desc == "hamming" else desc)
         tpl = torch.from_numpy(ks.des_tpl).to(dev)
         q = torch.from_numpy(ks.des_q).to(dev)
         off = torch.from_numpy(ks.q_off).to(dev)
         max_nq = int(np.diff(ks.q_off).max())
-        ms = timed(lambda: stages.knn2_l2u8(tpl, q, off, max_nq), args.reps)  # dispatches on dtype
+        knn = stages.knn2_hamming if desc == "hamming" else stages.knn2_l2u8  # l2u8 dispatches on dtype
+        ms = timed(lambda: knn(tpl, q, off, max_nq), args.reps)
         ops = 2.0 * n_tpl * float(ks.q_off[-1]) * D
         rate = ops / (ms * 1e-3) / 1e12
         r = {"frames": F, "n_tpl": n_tpl, "D": D, "descriptor": desc, "mean_n_q": round(ks.q_off[-1] / F, 1),
              "ms": round(ms, 4), "algorithmic_ops": ops}
-        if desc == "f32":
+        if desc == "hamming":
+            d = n_tpl * float(ks.q_off[-1])
+            r.update({"G_distances_per_s": round(d / (ms * 1e-3) / 1e9, 1)})
+        elif desc == "f32":
             r.update({"TFLOPs_fp32_equiv": round(rate, 1), "bf16_mfma_TFLOPs_issued": round(3 * rate, 1),
                       "peak": BF16_PEAK_TFLOPS, "frac_bf16_issued": round(3 * rate / BF16_PEAK_TFLOPS, 4)})
         else:
