@@ -361,12 +361,14 @@ constexpr int kBrightShare = 3;  // bright chunks * kBrightShare > box chunks ->
 // Output rows of a mode-3 tile, with the per-row overheads of output_rows removed: row
 // origins are scalar, the lower tap row is an immediate LDS offset, the store is a buffer
 // store with the row offset in soffset.
-template <class Cfg, int BLEND>
+// INTERIOR: the tile lies inside the frame (every row exists, every lane's pixel pair is
+// stored), so the rows carry no bounds test and no store mask.
+template <class Cfg, int BLEND, bool INTERIOR>
 __device__ __forceinline__ void fast_rows(const uint16_t* stile, const int2* __restrict__ rt, int ox, int oy,
                                           uint16_t* __restrict__ Dst, int H, int W, int xb, int yb, int wave, int lane,
                                           const int (&ad)[2], const int (&bd)[2]) {
   const uint32_t xoff = 2u * (uint32_t)(xb + 2 * lane);  // byte offset of the lane's pixel pair
-  const bool store_ok = xb + 2 * lane + 2 <= W;          // W is even here
+  const bool store_ok = INTERIOR || xb + 2 * lane + 2 <= W;  // W is even here
   const __amdgpu_buffer_rsrc_t dst_rsrc = __builtin_amdgcn_make_buffer_rsrc(Dst, 0, 2 * H * W, 0x00020000);
   int2 org[Cfg::kTileH / 4];  // all row origins up front (scalar loads; the table is padded)
 #pragma unroll
@@ -374,7 +376,7 @@ __device__ __forceinline__ void fast_rows(const uint16_t* stile, const int2* __r
 #pragma unroll
   for (int i = 0; i < Cfg::kTileH / 4; ++i) {
     const int y = yb + wave + 4 * i;  // wave-uniform
-    if (y >= H) break;
+    if (!INTERIOR && y >= H) break;
     const int X0 = org[i].x - ox, Y0 = org[i].y - oy;
     uint32_t v[2][4], fx[2], fy[2];
 #pragma unroll
@@ -641,12 +643,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
       const uint32_t bright = fl.x + fl.y + fl.z + fl.w;
       const int2* rt = rowtab + ((size_t)f * 4 + wave) * hq + (yb >> 2);
       const int ox = box.ax0 * 1024, oy = box.sy0 * 1024;
-      if (bright == 0)
-        fast_rows<Cfg, kDark>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
-      else if ((int)bright * kBrightShare <= box.rows * (box.pitch >> 3))
-        fast_rows<Cfg, kMixed>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
-      else
-        fast_rows<Cfg, kBright>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+      const bool interior = yb + Cfg::kTileH <= H && xb + kTileW <= W;
+      if (bright == 0) {
+        if (interior)
+          fast_rows<Cfg, kDark, true>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+        else
+          fast_rows<Cfg, kDark, false>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+      } else if ((int)bright * kBrightShare <= box.rows * (box.pitch >> 3)) {
+        if (interior)
+          fast_rows<Cfg, kMixed, true>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+        else
+          fast_rows<Cfg, kMixed, false>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+      } else {
+        fast_rows<Cfg, kBright, false>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+      }
       return;
     }
   }
