@@ -8,10 +8,11 @@ K1 match (GPU) -> survivor bitmasks to host -> consensus (host, native) -> K2 RA
 Detection is not part of the path (no detector exists in this image; keypoints are
 synthetic, see kcmc_amd/synthetic.py).
 
-Steps are issued through pipeline.OverlappedSlabs, a two-slab software pipeline on one
-stream (device order match(k+1) -> warp(k) -> RANSAC(k+1)): the host consensus of step
-k+1 runs while step k's frames are warped; every step still runs every stage, and the
-pipeline is drained inside the timed region.  --serial runs the steps strictly one
+Steps are issued through pipeline.OverlappedSlabs, a software pipeline on one stream
+(device order match(k) -> warp(k-1) -> RANSAC(k); --pipeline-depth 3 for match(k) ->
+warp(k-2) -> RANSAC(k-1)): the host consensus of step k runs while step k-1's frames
+are warped; every step still runs every stage, and the pipeline is drained inside the
+timed region.  --serial runs the steps strictly one
 after another.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -347,6 +348,8 @@ def main():
     ap.add_argument("--detect", action="store_true",
                     help="also time align from raw uint16 frames on the device: normalisation + ORB-style "
                          "detection + the hot path (pipeline.align_frames); reported as `with_detection`")
+    ap.add_argument("--pipeline-depth", type=int, default=2, choices=(2, 3),
+                    help="slabs in flight in the pipelined schedule (pipeline.OverlappedSlabs depth)")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
@@ -380,7 +383,8 @@ def main():
     counts = [args.frames] * world
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s; {args.frames} frames {bc.H}x{bc.W}x{bc.C} on {dev}")
 
-    ov = None if args.serial else pipeline.OverlappedSlabs(dev, cfg, counts=counts if world > 1 else None)
+    ov = None if args.serial else pipeline.OverlappedSlabs(dev, cfg, counts=counts if world > 1 else None,
+                                                            depth=args.pipeline_depth)
 
     def step(timer):
         if ov is None:
@@ -388,11 +392,11 @@ def main():
         res = ov.submit(inp, out=out, mark=timer.mark if timer else None)
         return (res.consensus, res.ransac) if res is not None else None
 
-    def drain(timer):  # the pipelined schedule: queue the last slab's warp
+    def drain(timer):  # the pipelined schedule: finish the slabs still in flight
         if ov is None:
             return None
         res = ov.flush(mark=timer.mark if timer else None)
-        return (res.consensus, res.ransac) if res is not None else None
+        return (res[-1].consensus, res[-1].ransac) if res else None
 
     for _ in range(args.warmup):
         step(None)
@@ -441,7 +445,8 @@ def main():
     if ov is None:
         stage_ms["host_and_transfers"] = round(ms_step - match_ms - ransac_ms - warp_ms, 3)
     else:  # step k+1's match/consensus/RANSAC/post-processing overlap step k's warp
-        stage_ms["schedule"] = "pipelined: match(k+1) -> warp(k) -> RANSAC(k+1) on one stream, host consensus under the warp"
+        stage_ms["schedule"] = ("pipelined: match(k) -> warp(k-1) -> RANSAC(k)" if args.pipeline_depth == 2 else
+                                "pipelined: match(k) -> warp(k-2) -> RANSAC(k-1)") + " on one stream, host consensus under the warp"
         stage_ms["step_minus_warp"] = round(ms_step - warp_ms, 3)
     result = {
         "metric": METRIC,

@@ -236,55 +236,66 @@ def _h2d_async(arrays, dev, copy: torch.cuda.Stream):
 
 @dataclass
 class _SlabInFlight:
-    """A slab whose match / consensus / RANSAC are queued; its warp and post-processing
-    follow in the next submit (or flush)."""
+    """A slab on its way through the pipeline: matched (survivor bitmasks on their way to
+    the host), then fitted (RANSAC queued, parameters on their way to the host)."""
 
     inp: SlabInputs
     out: Optional[torch.Tensor]
     f0: int
     match: stages.MatchResult
-    cons: stages.Consensus
-    rr: stages.RansacResult
-    params_host: torch.Tensor
-    params_ready: torch.cuda.Event
+    keep_host: torch.Tensor
+    keep_ready: torch.cuda.Event
+    cons: Optional[stages.Consensus] = None
+    rr: Optional[stages.RansacResult] = None
+    params_host: Optional[torch.Tensor] = None
+    params_ready: Optional[torch.cuda.Event] = None
     aligned: Optional[torch.Tensor] = None
 
 
 class OverlappedSlabs:
-    """Streams slabs through the hot path as a two-slab software pipeline on one stream.
+    """Streams slabs through the hot path as a software pipeline on one stream.
 
-    submit(slab k+1) queues, in this device order,
+    submit(slab k) queues, in this device order (``depth=2``, the default),
 
-        match(k+1) -> warp(k) -> RANSAC(k+1)
+        match(k) -> warp(k-1) -> RANSAC(k)
 
-    with every transfer on a side stream.  The warp of slab k reads slab k's RANSAC
-    parameters where RANSAC left them: with frame_downsample_rate == 1 the reference's
-    post-processing (VA:143-145) hands a frame with a model its own parameters, so only
-    frames without a model need the host (NaN-gap interpolation); the warp writes zeros
-    for those and they are warped again, with the filled maps, once the host has them.
-    The consensus of slab k+1 (VA:224-286, host) runs while slab k's frames are being
-    warped.  The kernels never share the CUs with each other (co-resident analysis
+    with every transfer on a side stream: the host enqueues match(k) and the warp of the
+    slab fitted last time, then waits for slab k's survivor bitmasks (VA:224-286
+    consensus) while warp(k-1) keeps the device busy, and queues RANSAC(k) behind it.
+    ``depth=3`` queues match(k) -> warp(k-2) -> RANSAC(k-1) instead, so the consensus uses
+    bitmasks that were ready a whole step earlier; same-box A/B
+    found it no faster at c2 and slower at c3, so it is opt-in.  The warp of a slab reads
+    its RANSAC parameters where RANSAC left them: with frame_downsample_rate == 1 the
+    reference's post-processing (VA:143-145) hands a frame with a model its own
+    parameters, so only frames without a model need the host (NaN-gap interpolation); the
+    warp writes zeros for those and they are warped again, with the filled maps, once the
+    host has them.  The kernels never share the CUs with each other (co-resident analysis
     kernels slowed the warp by as much as they ran, and a large-LDS match workgroup
-    starves behind the warp's tiles), so a step costs the sum of its kernels.  With
-    frame_downsample_rate > 1 every full-rate frame's map comes from the host
-    interpolation, and the warp of slab k waits for it.  Every slab runs every stage and
-    its results equal ``align_slab``'s.
+    starves behind the warp's tiles), so a step costs the sum of its kernels unless the
+    host is slower.  With frame_downsample_rate > 1 every full-rate frame's map comes from
+    the host interpolation, and the warp of slab k waits for it.  Every slab runs every
+    stage and its results equal ``align_slab``'s.
 
-    submit returns the SlabResult of the slab whose warp it queued (None for the first
-    slab); flush() queues the last warp.  ``res.extras["done"]`` is an event after the
-    slab's last warp; ``aligned`` is ready once it has passed (or after synchronize()).
+    submit returns the SlabResult of the slab ``depth - 1`` submissions back (None
+    before that); flush() finishes the slabs still in flight and returns their results
+    in order.
+    ``res.extras["done"]`` is an event after the slab's last warp; ``aligned`` is ready
+    once it has passed (or after synchronize()).
 
     With ``counts`` (frames per rank) the slabs are one rank's share of a frame-sharded
     job: survivor bitmasks and RANSAC parameters are all-gathered over ``group``
-    (distributed.align_sharded's two exchanges) in the same stream order.
+    (distributed.align_sharded's two exchanges) in the same stream order on every rank.
 
         ov = OverlappedSlabs(device, cfg)
-        results = [ov.submit(inp) for inp in slabs][1:] + [ov.flush()]
+        results = [r for r in (ov.submit(inp) for inp in slabs) if r is not None] + ov.flush()
         ov.synchronize()
     """
 
     def __init__(self, device, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
-                 counts: Optional[List[int]] = None, group=None):
+                 counts: Optional[List[int]] = None, group=None, depth: int = 2):
+        if depth not in (2, 3):
+            raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
+        self.depth = depth
         if counts is not None and len(counts) > 1 and cfg.frame_downsample_rate != 1:
             # the rank's first frame is counted in sample frames, the affines in full-rate
             # frames: the same restriction as distributed.align_sharded
@@ -297,7 +308,8 @@ class OverlappedSlabs:
         self.group = group
         self.stream = torch.cuda.Stream(self.dev)
         self.copy = torch.cuda.Stream(self.dev)  # bitmask / point-list / params / map transfers
-        self._prev: Optional[_SlabInFlight] = None
+        self._matched: Optional[_SlabInFlight] = None  # match queued, consensus pending
+        self._fitted: Optional[_SlabInFlight] = None   # RANSAC queued, warp pending
 
     def _sharded(self) -> bool:
         return self.counts is not None and len(self.counts) > 1
@@ -305,51 +317,71 @@ class OverlappedSlabs:
     def _device_maps(self) -> bool:
         return int(self.cfg.frame_downsample_rate) == 1
 
+    def _rank(self) -> int:
+        if not self._sharded():
+            return 0
+        import torch.distributed as dist
+
+        return dist.get_rank(self.group)
+
     def submit(self, inp: SlabInputs, out: Optional[torch.Tensor] = None,
                mark: Optional[Callable[[str], None]] = None) -> Optional[SlabResult]:
         mark = mark or (lambda name: None)
-        cfg = self.cfg
         self.stream.wait_stream(torch.cuda.current_stream(self.dev))
-        n_tpl = inp.des_tpl.shape[0]
-        n_local = inp.q_off.numel() - 1
         with torch.cuda.stream(self.stream):
-            mark("m0")
-            match = match_stage(inp, cfg)
-            mark("m1")
-            if self._sharded():
-                from .distributed import _all_gather_rows
-                import torch.distributed as dist
-
-                rank = dist.get_rank(self.group)
-                f0, n_all = sum(self.counts[:rank]), sum(self.counts)
-                keep_h, keep_ready = _d2h_async(_all_gather_rows(match.keep_bits, self.counts, self.group), self.copy)
-            else:
-                rank, f0, n_all = 0, 0, n_local
-                keep_h, keep_ready = _d2h_async(match.keep_bits, self.copy)
-            prev, self._prev = self._prev, None
-            if prev is not None and self._device_maps():
-                self._warp_device_maps(prev, mark)  # warp(k) queued behind match(k+1)
-            keep_ready.synchronize()
-            # the global consensus; with counts, point lists of this rank's frames only
-            cons = consensus_stage(keep_h.numpy(), n_tpl, n_all, cfg, self.logger if rank == 0 else None,
-                                   frames=(f0, f0 + n_local) if self._sharded() else None)
-            pt_idx = cons.pt_idx if cons.pt_idx.size else np.zeros(1, np.int32)
-            lists = tuple(_h2d_async((cons.pt_off, pt_idx), self.dev, self.copy))
-            mark("r0")
-            rr = ransac_stage(match, inp.kp_tpl, cons, cfg, lists_dev=lists)
-            mark("r1")
-            if self._sharded():
-                from .distributed import _all_gather_rows
-
-                params_h, params_ready = _d2h_async(_all_gather_rows(rr.params, self.counts, self.group), self.copy)
-            else:
-                params_h, params_ready = _d2h_async(rr.params, self.copy)
             for t in (inp.frames, out):
                 if t is not None:
                     t.record_stream(self.stream)
-            finished = self._finish(prev, mark) if prev is not None else None
-            self._prev = _SlabInFlight(inp, out, f0, match, cons, rr, params_h, params_ready)
-        return finished
+            new = self._match(inp, out, mark)
+            fitted, self._fitted = self._fitted, None
+            if fitted is not None and self._device_maps():
+                self._warp_device_maps(fitted, mark)  # warp(k-depth+1) queued behind match(k)
+            if self.depth == 2:
+                self._fitted = self._fit(new, mark)  # RANSAC(k) after warp(k-1)
+            else:
+                if self._matched is not None:
+                    self._fitted = self._fit(self._matched, mark)  # RANSAC(k-1) after warp(k-2)
+                self._matched = new
+            return self._finish(fitted, mark) if fitted is not None else None
+
+    def _match(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
+        mark("m0")
+        match = match_stage(inp, self.cfg)
+        mark("m1")
+        if self._sharded():
+            from .distributed import _all_gather_rows
+
+            rank = self._rank()
+            f0 = sum(self.counts[:rank])
+            keep_h, keep_ready = _d2h_async(_all_gather_rows(match.keep_bits, self.counts, self.group), self.copy)
+        else:
+            f0 = 0
+            keep_h, keep_ready = _d2h_async(match.keep_bits, self.copy)
+        return _SlabInFlight(inp, out, f0, match, keep_h, keep_ready)
+
+    def _fit(self, p: _SlabInFlight, mark) -> _SlabInFlight:
+        """The consensus (host) and RANSAC (device) of a matched slab."""
+        cfg = self.cfg
+        n_tpl = p.inp.des_tpl.shape[0]
+        n_local = p.inp.q_off.numel() - 1
+        n_all = sum(self.counts) if self._sharded() else n_local
+        p.keep_ready.synchronize()
+        # the global consensus; with counts, point lists of this rank's frames only
+        p.cons = consensus_stage(p.keep_host.numpy(), n_tpl, n_all, cfg, self.logger if self._rank() == 0 else None,
+                                 frames=(p.f0, p.f0 + n_local) if self._sharded() else None)
+        pt_idx = p.cons.pt_idx if p.cons.pt_idx.size else np.zeros(1, np.int32)
+        lists = tuple(_h2d_async((p.cons.pt_off, pt_idx), self.dev, self.copy))
+        mark("r0")
+        p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, cfg, lists_dev=lists)
+        mark("r1")
+        if self._sharded():
+            from .distributed import _all_gather_rows
+
+            p.params_host, p.params_ready = _d2h_async(_all_gather_rows(p.rr.params, self.counts, self.group),
+                                                       self.copy)
+        else:
+            p.params_host, p.params_ready = _d2h_async(p.rr.params, self.copy)
+        return p
 
     def _warp_device_maps(self, p: _SlabInFlight, mark) -> None:
         mark("w0")
@@ -382,16 +414,21 @@ class OverlappedSlabs:
         res.extras["done"] = done
         return res
 
-    def flush(self, mark: Optional[Callable[[str], None]] = None) -> Optional[SlabResult]:
-        """Queue the warp of the last submitted slab (None if there is none)."""
+    def flush(self, mark: Optional[Callable[[str], None]] = None) -> List[SlabResult]:
+        """Finish every slab still in flight; their results, oldest first."""
         mark = mark or (lambda name: None)
-        p, self._prev = self._prev, None
-        if p is None:
-            return None
+        out: List[SlabResult] = []
         with torch.cuda.stream(self.stream):
-            if self._device_maps():
-                self._warp_device_maps(p, mark)
-            return self._finish(p, mark)
+            while self._fitted is not None or self._matched is not None:
+                fitted, self._fitted = self._fitted, None
+                if fitted is not None and self._device_maps():
+                    self._warp_device_maps(fitted, mark)
+                if self._matched is not None:
+                    self._fitted = self._fit(self._matched, mark)
+                    self._matched = None
+                if fitted is not None:
+                    out.append(self._finish(fitted, mark))
+        return out
 
     def synchronize(self) -> None:
         self.stream.synchronize()

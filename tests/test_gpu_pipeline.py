@@ -128,9 +128,10 @@ def test_config2_slab_end_to_end(dev):
         assert np.array_equal(out[f], oracle.warp_affine_u16(base, res.affines[f]))
 
 
-def test_overlapped_slabs_equal_align_slab(dev):
-    """OverlappedSlabs (two slabs in flight: the warp of slab k queued between the match
-    and the RANSAC of slab k+1) gives the same affines and warped frames as the
+@pytest.mark.parametrize("depth", [2, 3])
+def test_overlapped_slabs_equal_align_slab(dev, depth):
+    """OverlappedSlabs (depth 2: device order match(k) -> warp(k-1) -> RANSAC(k); depth 3:
+    match(k) -> warp(k-2) -> RANSAC(k-1)) gives the same affines and warped frames as the
     sequential align_slab."""
     F, H, W = 24, 270, 480
     cfg = pipeline.AlignConfig(n_kp_global=60)
@@ -151,11 +152,11 @@ def test_overlapped_slabs_equal_align_slab(dev):
                                          torch.from_numpy(ks.kp_q).to(dev), torch.from_numpy(ks.q_off).to(dev),
                                          ks.q_off))
     ref = [pipeline.align_slab(s, cfg) for s in slabs]
-    ov = pipeline.OverlappedSlabs(dev, cfg)
+    ov = pipeline.OverlappedSlabs(dev, cfg, depth=depth)
     got = [ov.submit(s) for s in slabs]
-    assert got[0] is None
-    got = got[1:] + [ov.flush()]
-    assert ov.flush() is None
+    assert all(g is None for g in got[:depth - 1])
+    got = got[depth - 1:] + ov.flush()
+    assert ov.flush() == []
     ov.synchronize()
     assert [len(r.skipped) for r in ref] == [3, 4, 0]
     for r, g in zip(ref, got):

@@ -52,7 +52,7 @@ def _inputs(ks_list, dev):
                                t(q_off), q_off)
 
 
-def _rank_main(rank: int, port: int, out_dir: str, model: str) -> None:
+def _rank_main(rank: int, port: int, out_dir: str, model: str, depth: int) -> None:
     import torch.distributed as dist
 
     from kcmc_amd import distributed as kdist
@@ -62,7 +62,7 @@ def _rank_main(rank: int, port: int, out_dir: str, model: str) -> None:
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     cfg = pipeline.AlignConfig(n_kp_global=N_KP_GLOBAL, ransac_model=model)
-    slabs = [_inputs([_keypoints(rank, s, model)], dev) for s in range(2)]
+    slabs = [_inputs([_keypoints(rank, s, model)], dev) for s in range(3)]
     for inp in slabs:
         if rank != 0:  # only rank 0 holds the template; the others receive it
             inp.des_tpl.zero_()
@@ -75,14 +75,13 @@ def _rank_main(rank: int, port: int, out_dir: str, model: str) -> None:
     out["sharded_aligned"] = res.aligned.cpu().numpy()
     out["sharded_affines"] = res.affines
     out["sharded_skipped"] = np.asarray(res.skipped, np.int64)
-    # 2. the pipelined schedule with the two exchanges, two slabs in flight
-    ov = pipeline.OverlappedSlabs(dev, cfg, counts=list(COUNTS))
-    r0 = ov.submit(slabs[0])
-    r1 = ov.submit(slabs[1])
-    r2 = ov.flush()
+    # 2. the pipelined schedule with the two exchanges, `depth` slabs in flight
+    ov = pipeline.OverlappedSlabs(dev, cfg, counts=list(COUNTS), depth=depth)
+    r = [ov.submit(s) for s in slabs]
+    rest = ov.flush()
     ov.synchronize()
-    assert r0 is None and r1 is not None and r2 is not None
-    for k, r in enumerate((r1, r2)):
+    assert all(x is None for x in r[:depth - 1]) and len(rest) == depth - 1
+    for k, r in enumerate(r[depth - 1:] + rest):
         out[f"ov{k}_aligned"] = r.aligned.cpu().numpy()
         out[f"ov{k}_affines"] = r.affines
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out)
@@ -101,11 +100,11 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("model", ["euclidean", "affine"])
-def test_sharded_hip_path_equals_single_device(tmp_path, model):
+@pytest.mark.parametrize("model,depth", [("euclidean", 2), ("affine", 3)])
+def test_sharded_hip_path_equals_single_device(tmp_path, model, depth):
     port = _free_port()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), str(r), str(port), str(tmp_path), model],
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), str(r), str(port), str(tmp_path), model, str(depth)],
                               env=env, cwd=REPO) for r in range(WORLD)]
     try:
         rcs = [p.wait(timeout=200) for p in procs]
@@ -118,7 +117,7 @@ def test_sharded_hip_path_equals_single_device(tmp_path, model):
 
     dev = torch.device("cuda", 0)
     cfg = pipeline.AlignConfig(n_kp_global=N_KP_GLOBAL, ransac_model=model)
-    for s, tag in ((0, "sharded"), (0, "ov0"), (1, "ov1")):
+    for s, tag in ((0, "sharded"), (0, "ov0"), (1, "ov1"), (2, "ov2")):
         ref = pipeline.align_slab(_inputs([_keypoints(r, s, model) for r in range(WORLD)], dev), cfg)
         assert len(ref.skipped) < sum(COUNTS) // 2
         aligned = ref.aligned.cpu().numpy()
@@ -130,4 +129,4 @@ def test_sharded_hip_path_equals_single_device(tmp_path, model):
 
 
 if __name__ == "__main__":
-    _rank_main(int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4])
+    _rank_main(int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5]))

@@ -4,11 +4,10 @@ host spends a step while the warp of the previous step runs on the GPU.
     python tools/host_breakdown.py [--config c2] [--frames F] [--steps 8]
 
 Prints, per step, host wall-clock milliseconds between the marks OverlappedSlabs.submit
-passes through (m0 match launched, m1, w0 after the previous slab's params D2H wait +
-post-processing + H2D, w1 its warp launched, r0 after the bitmask D2H + native consensus,
-r1 RANSAC launched), and the consensus alone on the same bitmasks.  The GPU idles when
-the post-processing (m1->w0) outlasts the match kernels, or the consensus (w1->r0) the
-warp."""
+passes through (m0 match(k) launched, m1, w0/w1 around the warp(k-2) launch, r0 after
+the bitmask wait + native consensus of slab k-1, r1 its RANSAC launched, end after the
+post-processing of slab k-2), and the consensus alone on the same bitmasks.  The device
+idles when the host's chain outlasts the step's kernels."""
 import argparse
 import json
 import os
@@ -60,7 +59,11 @@ def main():
         pipeline.consensus_stage(keep, inp.des_tpl.shape[0], args.frames, cfg, None)
         cons.append((time.perf_counter() - c0) * 1e3)
     med = {k: round(float(np.median([r[k] for r in rows])), 3) for k in rows[0]}
-    print(json.dumps({"config": args.config, "frames": args.frames, "step_ms": round(step_ms, 3), "median_host_ms": med, "consensus_alone_ms": round(min(cons), 3),
+    sub = np.array([r["submit_ms"] for r in rows])
+    pct = {p: round(float(np.percentile(sub, p)), 3) for p in (10, 50, 90, 99)}
+    slow = [(i, {k: v for k, v in r.items() if v > 2 * med[k] + 0.05}) for i, r in enumerate(rows)
+            if r["submit_ms"] > 1.5 * med["submit_ms"]]
+    print(json.dumps({"config": args.config, "frames": args.frames, "step_ms": round(step_ms, 3), "median_host_ms": med, "submit_ms_percentiles": pct, "slow_submits": slow[:12], "consensus_alone_ms": round(min(cons), 3),
                       "cpu_count": os.cpu_count()}))
 
 
