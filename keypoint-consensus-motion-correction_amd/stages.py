@@ -80,7 +80,12 @@ def _check_offsets(q_off_host: np.ndarray, n_frames: int) -> None:
 
 def knn2_l2u8(des_tpl: torch.Tensor, des_q: torch.Tensor, q_off: torch.Tensor, max_nq: int) -> Tuple[torch.Tensor, torch.Tensor]:
     """cv2.BFMatcher().knnMatch(des_tpl, des_q[frame], k=2) for every frame at once.
-    uint8 descriptors (the reference's AKAZE/BRISK) or float32 (SIFT-style extension)."""
+    uint8 descriptors (the reference's AKAZE/BRISK): exact integer distances, bit-exact
+    with OpenCV's.  float32 (SIFT-style extension): the distance is DEFINED by this build
+    as sqrtf of the sequentially fp64-accumulated sum of squares (oracle
+    kcmc_oracle_knn2_l2f32); OpenCV's batchDistL2_32f accumulates in float in a
+    build-dependent SIMD order, so near-ties (distances equal to ~1 ulp) can rank
+    differently than with cv2 -- parity with OpenCV is unpinned for float descriptors."""
     dev = _device_of(des_tpl)
     f32 = des_tpl.dtype == torch.float32
     _require(des_tpl, "des_tpl", torch.float32 if f32 else torch.uint8, dev, 2)
@@ -126,8 +131,10 @@ def match_frames(
     norm: str = "l2",
 ) -> MatchResult:
     """VA:194-214 for every frame: knn k=2 + reorder + ratio + median filters.
-    uint8 descriptors (the reference's) or float32 (SIFT-style extension); ``norm``
-    "hamming" (uint8 only) is the opt-in NORM_HAMMING matcher for binary descriptors."""
+    uint8 descriptors (the reference's) or float32 (SIFT-style extension; its distance is
+    this build's fp64-accumulated L2, not OpenCV's float accumulation, so near-tie order
+    against cv2 is unpinned -- see knn2_l2u8); ``norm`` "hamming" (uint8 only) is the
+    opt-in NORM_HAMMING matcher for binary descriptors."""
     if norm not in ("l2", "hamming"):
         raise ValueError(f"norm must be 'l2' or 'hamming' (got {norm!r})")
     dev = _device_of(des_tpl)
