@@ -19,10 +19,11 @@
 //   chunk of frame descriptors: for D <= 64 bytes sqrtf is strictly increasing on the
 //   integer SSD range, so integer keys order exactly like OpenCV's float
 //   distances, and the low bits make ties go to the lower frame index like OpenCV's
-//   K-insertion.  3 VALU ops per distance: key = acc << 9 + qk (v_lshl_add, qk =
-//   (Q + B) << 8 | j - q0 from LDS), b2 = med3(b1, b2, key), b1 = min(b1, key), on two
-//   independent top-2 pairs per column (even / odd accumulator) so that consecutive
-//   distances do not wait on each other.  Each chunk's top-2 is merged into a 64-bit
+//   K-insertion.  2.5 VALU ops per distance (the kernel is bound by integer VALU issue,
+//   4 cycles per wave64 op): key = acc << 9 + qk (v_lshl_add, qk = (Q + B) << 8 | j - q0
+//   from LDS) for two rows of a column, then b2 = min(b2, med3(b1, ka, kb)),
+//   b1 = min3(b1, ka, kb), on two independent top-2 pairs per column so that consecutive
+//   pairs do not wait on each other.  Each chunk's top-2 is merged into a 64-bit
 //   (ssd << 32 | j) top-2 with SSD = (key >> 8) + T - B.  Frame descriptors are staged
 //   through LDS (converted to int8, zero-padded to DP, rows padded by 16 B so the
 //   ds_read_b128 fragment reads are bank-conflict free).
@@ -59,10 +60,25 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
   return r;
 }
 
+__device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // b1 <= b2 always; new b2 = median(b1, b2, key), new b1 = min(b1, key).
 __device__ __forceinline__ void top2_insert(uint32_t& b1, uint32_t& b2, uint32_t key) {
   b2 = med3_u32(b1, b2, key);
   b1 = b1 < key ? b1 : key;
+}
+
+// two keys at once (3 ops): the second smallest of {b1, b2, ka, kb} is
+// min(b2, median(b1, ka, kb)) because b2 >= b1.  Exact when the keys are distinct or
+// equal keys are interchangeable (the per-chunk keys carry their row).
+__device__ __forceinline__ void top2_insert2(uint32_t& b1, uint32_t& b2, uint32_t ka, uint32_t kb) {
+  const uint32_t m = med3_u32(b1, ka, kb);
+  b1 = min3_u32(b1, ka, kb);
+  b2 = b2 < m ? b2 : m;
 }
 
 __device__ __forceinline__ void top2_insert64(unsigned long long& b1, unsigned long long& b2, unsigned long long key) {
@@ -273,7 +289,9 @@ __global__ __launch_bounds__(KnnShape<WAVES>::kThreads) void knn2_l2u8_kernel(
 #pragma unroll
         for (int b = 0; b < kBlocksPerWave; ++b)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) top2_insert(b1[b][r & 1], b2[b][r & 1], ((uint32_t)acc[b][r] << 9) + qk[r]);
+          for (int p = 0; p < 8; ++p)
+            top2_insert2(b1[b][p & 1], b2[b][p & 1], ((uint32_t)acc[b][2 * p] << 9) + qk[2 * p],
+                         ((uint32_t)acc[b][2 * p + 1] << 9) + qk[2 * p + 1]);
       }
       // ---- fold the chunk's top-2 (local indices) into the frame's 64-bit top-2: the
       // even / odd pairs merge in 32 bits first (c1 <= c2 = the chunk's two smallest keys)
@@ -419,37 +437,52 @@ __global__ __launch_bounds__(kFilterThreads) void match_filter_kernel(
 
 // Workgroups that fill the device once (2 per CU at 8 waves, 4 at 4 waves: the kernels'
 // ~100 VGPRs allow 4 waves per SIMD), split evenly over the template groups.
-int knn_grid(int n_tg, int n_frames, int wgs_per_cu) {
+int device_cus() {
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   }
-  const int G = std::max(1, std::min(n_frames, cus * wgs_per_cu / n_tg));
+  return cus;
+}
+
+// persistent grid: n_tg template groups x G frame strides, G = the resident workgroups
+// per template group (workgroups never wait on each other, so a wrong residency count
+// costs balance, not progress)
+int knn_grid(int n_tg, int n_frames, int wgs_per_cu) {
+  const int G = std::max(1, std::min(n_frames, device_cus() * std::max(1, wgs_per_cu) / n_tg));
   return n_tg * G;
+}
+
+template <typename K>
+int resident_wgs(K kernel, int threads) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, threads, 0) != hipSuccess || n <= 0) n = 1;
+  return n;
+}
+
+template <int DP, int WAVES>
+int launch_knn_row(const uint8_t* des_tpl, int n_tpl, int D, const uint8_t* des_q, const int32_t* q_off,
+                   int n_frames, int32_t* out_idx, float* out_dist, hipStream_t s) {
+  auto* k = knn2_l2u8_kernel<DP, WAVES>;
+  static const int per_cu = resident_wgs(k, KnnShape<WAVES>::kThreads);
+  const int n_tg = ceil_div(n_tpl, KnnShape<WAVES>::kTplPerWG);
+  hipLaunchKernelGGL(k, dim3(knn_grid(n_tg, n_frames, per_cu)), dim3(KnnShape<WAVES>::kThreads), 0, s, des_tpl,
+                     n_tpl, D, des_q, q_off, n_frames, n_tg, out_idx, out_dist);
+  return launch_check("knn2_l2u8_kernel");
 }
 
 int launch_knn(const uint8_t* des_tpl, int n_tpl, int D, const uint8_t* des_q, const int32_t* q_off,
                int n_frames, int max_nq, int32_t* out_idx, float* out_dist, hipStream_t s) {
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
   (void)max_nq;
-  if (n_tpl > 256) {
-    const int n_tg = ceil_div(n_tpl, KnnShape<8>::kTplPerWG);
-    const dim3 grid(knn_grid(n_tg, n_frames, 2));
-    if (D <= 32)
-      hipLaunchKernelGGL((knn2_l2u8_kernel<32, 8>), grid, dim3(512), 0, s, des_tpl, n_tpl, D, des_q, q_off, n_frames, n_tg, out_idx, out_dist);
-    else
-      hipLaunchKernelGGL((knn2_l2u8_kernel<64, 8>), grid, dim3(512), 0, s, des_tpl, n_tpl, D, des_q, q_off, n_frames, n_tg, out_idx, out_dist);
-  } else {
-    const int n_tg = ceil_div(n_tpl, KnnShape<4>::kTplPerWG);
-    const dim3 grid(knn_grid(n_tg, n_frames, 4));
-    if (D <= 32)
-      hipLaunchKernelGGL((knn2_l2u8_kernel<32, 4>), grid, dim3(256), 0, s, des_tpl, n_tpl, D, des_q, q_off, n_frames, n_tg, out_idx, out_dist);
-    else
-      hipLaunchKernelGGL((knn2_l2u8_kernel<64, 4>), grid, dim3(256), 0, s, des_tpl, n_tpl, D, des_q, q_off, n_frames, n_tg, out_idx, out_dist);
-  }
-  return launch_check("knn2_l2u8_kernel");
+  const bool wide = n_tpl > 256;  // 512 template rows share each staged chunk
+  if (D <= 32)
+    return wide ? launch_knn_row<32, 8>(des_tpl, n_tpl, D, des_q, q_off, n_frames, out_idx, out_dist, s)
+                : launch_knn_row<32, 4>(des_tpl, n_tpl, D, des_q, q_off, n_frames, out_idx, out_dist, s);
+  return wide ? launch_knn_row<64, 8>(des_tpl, n_tpl, D, des_q, q_off, n_frames, out_idx, out_dist, s)
+              : launch_knn_row<64, 4>(des_tpl, n_tpl, D, des_q, q_off, n_frames, out_idx, out_dist, s);
 }
 
 int check_match_args(const void* des_tpl, int n_tpl, int D, const void* des_q, const void* q_off,
