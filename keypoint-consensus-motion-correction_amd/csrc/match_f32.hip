@@ -7,29 +7,37 @@
 //   S = sum_k ((double)a_k - (double)b_k)^2 (sequential, fp64), dist = sqrtf((float)S),
 // top-2 by (dist, frame index) like OpenCV's K-insertion.
 //
-// split_rows_kernel -- once per call: every frame row as bf16 hi | lo (v = hi + lo + e,
-//   |e| <= 2^-18 |v|; hi = RNE(v), v - hi exact, lo = RNE(v - hi)) and its fp32 squared
-//   norm, so that the template blocks of a frame share one conversion.
+// tpl_norm_max_kernel -- once per call: K = max over template rows of |a|^2 (fp32).
 //
-// knn2_l2f32_kernel -- one workgroup = 128 template rows x one frame (4 waves x one block
-//   of 32 rows; 3 waves per SIMD, several workgroups per CU so that one workgroup's
-//   barriers overlap another's matrix work).  Phase 1 on the bf16 matrix cores:
-//   d~ = |a|^2 + |b|^2 - 2 a.b with a.b ~ hi.hi + hi.lo + lo.hi by
-//   v_mfma_f32_32x32x16_bf16 (3 MFMAs per k-step of 16: 5.3x fewer cycles than
-//   v_mfma_f32_32x32x2_f32 for the same contraction).  B = the 32 template rows, split in
-//   registers; A = 32 frame rows per chunk, copied from the split rows into LDS (the next
-//   chunk's loads in flight during the current chunk's MFMAs).  Each lane keeps its
-//   template row's chunk top-4 on 32-bit keys (d~'s float bits with the low 6 mantissa
-//   bits replaced by the chunk-local row, 4 VALU per distance) and folds it into a running
-//   approximate top-4.  The error of a listed value is bounded by
-//     eps = (6 (D + 4) 2^-24 + 2^-15) (|a| + max|b|)^2
+// split_tiles_kernel -- once per call: every frame's rows, 32 at a time, written as the
+//   exact LDS image the matcher copies (18 KiB per tile: bf16 hi rows | bf16 lo rows, each
+//   row padded to 272 B, then C = (|b|^2 + K) / 2 per row; v = hi + lo + e with
+//   |e| <= 2^-18 |v|; hi = RNE(v), v - hi exact, lo = RNE(v - hi)), and each tile's
+//   max |b|^2.  Rows past the frame's last get C = +inf.
+//
+// knn2_l2f32_kernel -- one workgroup = 256 template rows x one frame (8 waves x one block
+//   of 32 rows).  Tiles reach LDS by LDS-DMA (global_load_lds_dwordx4, three buffers:
+//   two tiles in flight ahead of the one in use, one barrier per tile; no staging
+//   registers).  On the bf16 matrix cores, with the template
+//   operand negated and the accumulator started at the row's C,
+//     v = (|b|^2 + K) / 2 - a.b,  a.b ~ hi.hi + hi.lo + lo.hi
+//   (v_mfma_f32_32x32x16_bf16, 3 MFMAs per k-step of 16: 5.3x fewer cycles than
+//   v_mfma_f32_32x32x2_f32 for the same contraction).  v orders a lane's frame rows
+//   exactly like |a - b|^2 = 2 v + |a|^2 - K (K >= |a|^2 keeps it non-negative), so a
+//   distance costs 7 VALU: clamp, key (v's float bits with the low mantissa bits
+//   replaced by the row within a group of kFoldTiles tiles), and the sorted top-4
+//   insertion; each group's top-4 is folded into a running approximate top-4.  The
+//   error of a listed value is bounded by
+//     eps = (5 (D + 2) 2^-24 + 0.6 (3 2^-18 + t)) (sqrt(K) + max|b|)^2 * 1.02
+//   with t = the keys' relative truncation (derivation at its use below).
 //   (derivation at its use below).
-//   A frame row can be among the exact top-2 only if d~ <= d~(2) + 2 eps, so when the
+//   A frame row can be among the exact top-2 only if v <= v(2) + 2 eps, so when the
 //   approximate 4th value exceeds that bound the exact top-2 lies within the top-3
 //   candidates: phase 2 re-evaluates them with the exact fp64 definition and orders
 //   them by (dist, index).  Rows that cannot be certified (near-ties of 4+ frame
-//   descriptors) are appended to a list that knn2_l2f32_fallback_kernel finishes by
-//   exact brute force, one wave per row.
+//   descriptors) are appended to their frame's list, which knn2_l2f32_fallback_kernel
+//   finishes by exact brute force, reading each frame row once per batch of up to 4
+//   listed rows.
 #include <cfloat>
 
 #include "kcmc_internal.h"
@@ -40,13 +48,24 @@ namespace {
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 512;
+constexpr int kWaves = kThreads / 64;
+constexpr int kNBuf = 3;                           // tile buffers: two tiles in flight ahead of the one in use
 constexpr int kBlocks = 1;                         // 32-row template blocks per wave (2: 1 wave per SIMD)
-constexpr int kTplPerWG = (kThreads / 64) * kBlocks * 32;  // 128
+constexpr int kTplPerWG = kWaves * kBlocks * 32;  // 256
 constexpr int kDP = 128;                           // padded descriptor length
 constexpr int kKSteps = kDP / 16;                  // k-steps of v_mfma_f32_32x32x16_bf16
-constexpr int kQChunk = 32;                        // frame rows per LDS chunk (one MFMA tile; local index < 64)
+constexpr int kTile = 32;                          // frame rows per tile image (one MFMA tile)
+constexpr int kFoldTiles = 2;                      // tiles per top-4 fold (the row within them is in the key)
+constexpr uint32_t kRowMask = kFoldTiles * kTile - 1;
+// relative truncation of a key (its low log2(kFoldTiles * kTile) mantissa bits)
+constexpr float kKeyTrunc = (float)(kFoldTiles * kTile) * 1.1920929e-7f;
 constexpr int kRowB = kDP + 8;                     // padded LDS row (bf16 elements, 272 B)
+constexpr int kImgLo = kTile * kRowB * 2;          // byte offset of the lo rows in a tile image
+constexpr int kImgC = 2 * kImgLo;                  // byte offset of the per-row C values
+constexpr int kImgBytes = 18 * 1024;               // tile image, whole 1 KiB LDS-DMA pieces
+constexpr int kPieces = kImgBytes / 1024;
+static_assert(kImgC + kTile * 4 <= kImgBytes, "tile image layout");
 constexpr uint32_t kNoKey = 0xffffffffu;
 
 // The build's exact distance (identical operation order in the oracle).
@@ -142,77 +161,118 @@ __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
   lo = (__bf16)(v - (float)hi);
 }
 
-// Frame rows split once for every template block: row q -> bf16 hi[128] | lo[128] (zero
-// past D) and its fp32 squared norm.  32 lanes per row, 4 floats each.
-__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ des_q, int D,
-                                                         const int32_t* __restrict__ q_off, int n_frames,
-                                                         uint2* __restrict__ qsplit, float* __restrict__ qnorm,
-                                                         long long qrows) {
-  const int f = blockIdx.y;
-  const int q = q_off[f] + blockIdx.x * 8 + (threadIdx.x >> 5);
-  if (q >= q_off[f + 1] || q >= qrows) return;  // whole 32-lane groups exit together
+// K = max_i |a_i|^2 over the template rows (positive float bits order as integers; *Kbits
+// zeroed before the launch).  32 lanes per row, 4 floats each.
+__global__ __launch_bounds__(256) void tpl_norm_max_kernel(const float* __restrict__ des_tpl, int n_tpl, int D,
+                                                           unsigned* __restrict__ Kbits) {
+  const int i = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (i >= n_tpl) return;  // whole 32-lane groups exit together
   const int col = (threadIdx.x & 31) * 4;
-  const float* src = des_q + (size_t)q * D;
-  float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
-  if ((D & 3) == 0 && (reinterpret_cast<uintptr_t>(des_q) & 15) == 0) {
-    if (col < D) w = *reinterpret_cast<const float4*>(src + col);
-  } else {
-    w.x = col < D ? src[col] : 0.f;
-    w.y = col + 1 < D ? src[col + 1] : 0.f;
-    w.z = col + 2 < D ? src[col + 2] : 0.f;
-    w.w = col + 3 < D ? src[col + 3] : 0.f;
-  }
-  float ss = fmaf(w.w, w.w, fmaf(w.z, w.z, fmaf(w.y, w.y, w.x * w.x)));
+  const float* src = des_tpl + (size_t)i * D;
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (col + k < D) ss = fmaf(src[col + k], src[col + k], ss);
 #pragma unroll
   for (int off = 16; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
-  if ((threadIdx.x & 31) == 0) qnorm[q] = ss;
-  __bf16 hv[4], lv[4];
-  split_bf16(w.x, hv[0], lv[0]);
-  split_bf16(w.y, hv[1], lv[1]);
-  split_bf16(w.z, hv[2], lv[2]);
-  split_bf16(w.w, hv[3], lv[3]);
-  qsplit[(size_t)q * 64 + (threadIdx.x & 31)] = *reinterpret_cast<const uint2*>(hv);
-  qsplit[(size_t)q * 64 + 32 + (threadIdx.x & 31)] = *reinterpret_cast<const uint2*>(lv);
+  if ((threadIdx.x & 31) == 0) atomicMax(Kbits, __float_as_uint(ss));
 }
 
-// Loads of one chunk of split frame rows (32 x 16 B per row; 4 pieces per thread at 512
-// threads, in named registers: an indexed array here was placed in scratch memory),
-// addresses clamped to the frame's last row (and to the split buffer, should max_nq
-// undercount).
-static_assert(kQChunk * 32 / kThreads == 4, "issue_chunk loads four 16-byte pieces per thread");
-__device__ __forceinline__ uint4 chunk_piece(const uint4* __restrict__ qs, int q0n, int e, int last, int first) {
-  return qs[(size_t)(q0n + max(min(e >> 5, last), first)) * 32 + (e & 31)];
-}
-__device__ __forceinline__ void issue_chunk(const uint4* __restrict__ qs, const float* __restrict__ qnorm,
-                                            long long qrows, int q_begin, int n_q, int q0n, int tid, uint4& p0,
-                                            uint4& p1, uint4& p2, uint4& p3, float& pn) {
-  const int last = (int)min((long long)(n_q - 1 - q0n), qrows - 1 - q_begin - q0n);
-  const int first = -q_begin - q0n;
-  p0 = chunk_piece(qs, q0n, tid, last, first);
-  p1 = chunk_piece(qs, q0n, tid + kThreads, last, first);
-  p2 = chunk_piece(qs, q0n, tid + 2 * kThreads, last, first);
-  p3 = chunk_piece(qs, q0n, tid + 3 * kThreads, last, first);
-  if (tid < kQChunk) pn = qnorm[q_begin + q0n + max(min(tid, last), first)];
+// Frame f's tile t (rows 32 t .. 32 t + 31) -> img[(f * tpf + t) * kImgBytes]: the LDS
+// image the matcher copies (hi rows, lo rows, C = (|b|^2 + K) / 2 per row; rows past the
+// frame's last: zero descriptors, C = +inf), and the tile's max |b|^2 -> tile_max[f * tpf
+// + t].  One workgroup per tile, 8 rows per pass (32 lanes per row, 4 floats each).
+__global__ __launch_bounds__(256) void split_tiles_kernel(const float* __restrict__ des_q, int D,
+                                                          const int32_t* __restrict__ q_off, int tpf,
+                                                          const unsigned* __restrict__ Kbits,
+                                                          uint8_t* __restrict__ img,
+                                                          float* __restrict__ tile_max) {
+  __shared__ float s_max[4];
+  const int f = blockIdx.y, t = blockIdx.x;
+  const int n_q = q_off[f + 1] - q_off[f];
+  const int n_rows = min(n_q, tpf * kTile);
+  if (t * kTile >= n_rows) return;  // the whole workgroup
+  const int col = (threadIdx.x & 31) * 4;
+  const bool v4 = (D & 3) == 0 && (reinterpret_cast<uintptr_t>(des_q) & 15) == 0;
+  const float K = __uint_as_float(*Kbits);
+  uint8_t* tile = img + ((size_t)f * tpf + t) * kImgBytes;
+  float tmax = 0.f;
+#pragma unroll
+  for (int pass = 0; pass < kTile / 8; ++pass) {
+    const int rr = pass * 8 + (threadIdx.x >> 5);
+    const int r = t * kTile + rr;
+    const bool real = r < n_rows;
+    const float* src = des_q + (size_t)(q_off[f] + r) * D;
+    float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (real) {
+      if (v4) {
+        if (col < D) w = *reinterpret_cast<const float4*>(src + col);
+      } else {
+        w.x = col < D ? src[col] : 0.f;
+        w.y = col + 1 < D ? src[col + 1] : 0.f;
+        w.z = col + 2 < D ? src[col + 2] : 0.f;
+        w.w = col + 3 < D ? src[col + 3] : 0.f;
+      }
+    }
+    float ss = fmaf(w.w, w.w, fmaf(w.z, w.z, fmaf(w.y, w.y, w.x * w.x)));
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+    tmax = fmaxf(tmax, ss);
+    if ((threadIdx.x & 31) == 0) *reinterpret_cast<float*>(tile + kImgC + 4 * rr) = real ? 0.5f * (ss + K) : INFINITY;
+    __bf16 hv[4], lv[4];
+    split_bf16(w.x, hv[0], lv[0]);
+    split_bf16(w.y, hv[1], lv[1]);
+    split_bf16(w.z, hv[2], lv[2]);
+    split_bf16(w.w, hv[3], lv[3]);
+    *reinterpret_cast<uint2*>(tile + (rr * kRowB + col) * 2) = *reinterpret_cast<const uint2*>(hv);
+    *reinterpret_cast<uint2*>(tile + kImgLo + (rr * kRowB + col) * 2) = *reinterpret_cast<const uint2*>(lv);
+  }
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+  if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = tmax;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    tile_max[(size_t)f * tpf + t] = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
 }
 
-__device__ __forceinline__ void land_piece(__bf16* qhi, __bf16* qlo, int e, const uint4& v) {
-  const int r = e >> 5, part = e & 31;
-  __bf16* dstp = (part < 16 ? qhi : qlo) + r * kRowB + 8 * (part & 15);
-  *reinterpret_cast<uint4*>(dstp) = v;
+// One tile image (18 x 1 KiB) global -> LDS: wave w copies pieces w, w + kWaves, ...
+// (each lane 16 B; the LDS destination of a piece is M0 + lane * 16).  Issued by inline
+// asm: with __builtin_amdgcn_global_load_lds the compiler treats every later ds_read of
+// the staging array as dependent on every copy in flight and waits vmcnt(0) before it,
+// which drains the prefetch; here the counted vmcnt waits and the barrier in the tile
+// loop order the copies against the reads (M0 is saved and restored around each issue).
+__device__ __forceinline__ void dma_piece(const uint8_t* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+__device__ __forceinline__ void dma_tile(const uint8_t* __restrict__ src, uint8_t* dst, int wave, int lane) {
+  const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(dst);  // the LDS offset
+#pragma unroll
+  for (int p0 = 0; p0 < kPieces; p0 += kWaves) {
+    const int p = p0 + wave;  // wave-uniform
+    if (p < kPieces)
+      dma_piece(src + p * 1024 + lane * 16, (uint32_t)__builtin_amdgcn_readfirstlane((int)(base + (uint32_t)(p * 1024))));
+  }
 }
 
-__global__ __launch_bounds__(kThreads) void knn2_l2f32_kernel(
+// 4 waves per SIMD (<= 128 VGPRs): without the cap the compiler hoists every fragment
+// read of a tile (239 VGPRs, 2 waves per SIMD)
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void knn2_l2f32_kernel(
     const float* __restrict__ des_tpl, int n_tpl, int D, const float* __restrict__ des_q,
-    const int32_t* __restrict__ q_off, const uint2* __restrict__ qsplit, const float* __restrict__ qnorm,
-    long long qrows, int32_t* __restrict__ out_idx, float* __restrict__ out_dist, int32_t* __restrict__ fallback,
-    int32_t* __restrict__ n_fallback) {
-  __shared__ __attribute__((aligned(16))) __bf16 qhi[kQChunk * kRowB];
-  __shared__ __attribute__((aligned(16))) __bf16 qlo[kQChunk * kRowB];
-  __shared__ float qn[kQChunk];
-  __shared__ unsigned s_maxqn;  // max |b|^2 over the frame (float bits; positive floats order as ints)
+    const int32_t* __restrict__ q_off, const uint8_t* __restrict__ img, int tpf,
+    const unsigned* __restrict__ Kbits, const float* __restrict__ tile_max, int32_t* __restrict__ out_idx,
+    float* __restrict__ out_dist, int32_t* __restrict__ fallback, int32_t* __restrict__ fb_cnt) {
+  __shared__ __attribute__((aligned(16))) uint8_t tbuf[kNBuf][kImgBytes];
 
   // XCD-aware order: the workgroups of one frame get consecutive ids of one XCD's run
-  // (dispatch is round-robin over the 8 XCDs), so the frame's descriptors stay in that
+  // (dispatch is round-robin over the 8 XCDs), so the frame's tile images stay in that
   // XCD's L2 for all of its template blocks
   const int ntb = gridDim.x;
   const int wg = xcd_remap(blockIdx.x + ntb * blockIdx.y, ntb * gridDim.y);
@@ -223,18 +283,23 @@ __global__ __launch_bounds__(kThreads) void knn2_l2f32_kernel(
   const int h = lane >> 5;  // k-half of the fragments / row group of the output
   const int q_begin = q_off[f];
   const int n_q = q_off[f + 1] - q_begin;
-  if (tid == 0) s_maxqn = 0u;
+  const int n_tiles = min((n_q + kTile - 1) / kTile, tpf);
+  const uint8_t* fimg = img + (size_t)f * tpf * kImgBytes;
+  if (n_tiles > 0) dma_tile(fimg, tbuf[0], wave, lane);
+  if (n_tiles > 1) dma_tile(fimg + kImgBytes, tbuf[1], wave, lane);
+  // LDS-DMA pieces this wave issues per tile (wave-uniform): the count left in flight
+  // while tile t + 1 is still landing
+  const bool many = wave < kPieces % kWaves;
+  static_assert(kPieces / kWaves == 2 && kPieces % kWaves != 0, "vmcnt counts below assume 2 or 3 pieces per wave");
 
-  // ---- template fragments (B operand, bf16 hi/lo split) kept in registers: lane (c, h)
-  // holds row i's elements k = 16 s + 8 h + j of k-step s; and the row's squared norm
+  // ---- template fragments (B operand, bf16 hi/lo split of -a) kept in registers: lane
+  // (c, h) holds row i's elements k = 16 s + 8 h + j of k-step s
   bf16x8 bhi[kBlocks][kKSteps], blo[kBlocks][kKSteps];
-  float tn[kBlocks];
   int tpl_row[kBlocks];
 #pragma unroll
   for (int b = 0; b < kBlocks; ++b) {
     const int i = tb * kTplPerWG + (wave * kBlocks + b) * 32 + c;
     tpl_row[b] = i;
-    float na = 0.f;
 #pragma unroll
     for (int st = 0; st < kKSteps; ++st)
 #pragma unroll
@@ -242,12 +307,10 @@ __global__ __launch_bounds__(kThreads) void knn2_l2f32_kernel(
         const int k = 16 * st + 8 * h + j;
         const float v = (i < n_tpl && k < D) ? des_tpl[(size_t)i * D + k] : 0.f;
         __bf16 hv, lv;
-        split_bf16(v, hv, lv);
+        split_bf16(-v, hv, lv);
         bhi[b][st][j] = hv;
         blo[b][st][j] = lv;
-        na = fmaf(v, v, na);
       }
-    tn[b] = na + __shfl_xor(na, 32);
   }
 
   Top4 best[kBlocks];
@@ -258,80 +321,89 @@ __global__ __launch_bounds__(kThreads) void knn2_l2f32_kernel(
 #pragma unroll
     for (int k = 0; k < 3; ++k) best[b].j[k] = -1;
   }
-
-  const float* base = des_q + (size_t)q_begin * D;
-  // staging: the frame's rows were split once by split_rows_kernel (bf16 hi | lo, 512 B
-  // per row, and the fp32 squared norm), so a chunk is a plain copy of 64 x 512 B; the
-  // next chunk's loads are issued before the current chunk's MFMA tiles so that their
-  // latency is hidden behind them.  Addresses are clamped to the frame's last row (the
-  // tile outputs of rows >= cnt are never listed).
-  const uint4* qs = reinterpret_cast<const uint4*>(qsplit) + (size_t)q_begin * 32;
-  uint4 p0, p1, p2, p3;
-  float pn = 0.f;
-  if (n_q > 0) issue_chunk(qs, qnorm, qrows, q_begin, n_q, 0, tid, p0, p1, p2, p3, pn);
-  for (int q0 = 0; q0 < n_q; q0 += kQChunk) {
-    const int cnt = min(kQChunk, n_q - q0);
-    __syncthreads();  // previous chunk consumed
-    land_piece(qhi, qlo, tid, p0);
-    land_piece(qhi, qlo, tid + kThreads, p1);
-    land_piece(qhi, qlo, tid + 2 * kThreads, p2);
-    land_piece(qhi, qlo, tid + 3 * kThreads, p3);
-    if (tid < kQChunk) {
-      qn[tid] = pn;
-      if (tid < cnt) atomicMax(&s_maxqn, __float_as_uint(pn));
+  uint32_t ck[kBlocks][4];
+  int cur = 0;  // t % kNBuf
+  for (int t = 0; t < n_tiles; ++t) {
+    // tile t has landed (this wave's pieces: vmcnt, leaving tile t + 1's in flight; the
+    // others': the barrier) and every wave is done with tile t - 1, whose buffer the copy
+    // of tile t + 2 overwrites.  A raw s_barrier: __syncthreads() would wait vmcnt(0).
+    if (t + 1 == n_tiles)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (many)
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < n_tiles) {
+      const int nb = cur >= 1 ? cur - 1 : kNBuf - 1;  // (t + 2) % kNBuf
+      dma_tile(fimg + (size_t)(t + 2) * kImgBytes, tbuf[nb], wave, lane);
     }
-    __syncthreads();
-    if (q0 + kQChunk < n_q) issue_chunk(qs, qnorm, qrows, q_begin, n_q, q0 + kQChunk, tid, p0, p1, p2, p3, pn);
-    // ---- 32-row tiles: a.b ~ hi.hi + hi.lo + lo.hi on the bf16 matrix cores (fp32
-    // accumulation); the chunk's top-4 per lane on 32-bit keys (d~ with the low 6
-    // mantissa bits replaced by the chunk-local row)
-    uint32_t ck[kBlocks][4];
+    const uint8_t* tbp = tbuf[cur];
+    cur = cur + 1 == kNBuf ? 0 : cur + 1;
+    if ((t & (kFoldTiles - 1)) == 0) {
 #pragma unroll
-    for (int b = 0; b < kBlocks; ++b)
+      for (int b = 0; b < kBlocks; ++b)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) ck[b][k] = kNoKey;
-    for (int t0 = 0; t0 < cnt; t0 += 32) {
-      v16f acc[kBlocks];
+        for (int k = 0; k < 4; ++k) ck[b][k] = kNoKey;
+    }
+    // accumulators start at the rows' C: lane's 16 rows (r & 3) + 8 (r >> 2) + 4h
+    const float* cq = reinterpret_cast<const float*>(tbp + kImgC);
+    v16f acc0;
 #pragma unroll
-      for (int b = 0; b < kBlocks; ++b) acc[b] = v16f{0.f};
-      const __bf16* ah = &qhi[(t0 + c) * kRowB + 8 * h];
-      const __bf16* al = &qlo[(t0 + c) * kRowB + 8 * h];
+    for (int g = 0; g < 4; ++g) {
+      const float4 q4 = *reinterpret_cast<const float4*>(cq + 8 * g + 4 * h);
+      acc0[4 * g] = q4.x;
+      acc0[4 * g + 1] = q4.y;
+      acc0[4 * g + 2] = q4.z;
+      acc0[4 * g + 3] = q4.w;
+    }
+    v16f acc[kBlocks];
 #pragma unroll
-      for (int st = 0; st < kKSteps; ++st) {
-        const bf16x8 a_h = *reinterpret_cast<const bf16x8*>(ah + 16 * st);
-        const bf16x8 a_l = *reinterpret_cast<const bf16x8*>(al + 16 * st);
+    for (int b = 0; b < kBlocks; ++b) acc[b] = acc0;
+    const __bf16* ah = reinterpret_cast<const __bf16*>(tbp) + c * kRowB + 8 * h;
+    const __bf16* al = reinterpret_cast<const __bf16*>(tbp + kImgLo) + c * kRowB + 8 * h;
 #pragma unroll
-        for (int b = 0; b < kBlocks; ++b) {
-          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_h, bhi[b][st], acc[b], 0, 0, 0);
-          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_h, blo[b][st], acc[b], 0, 0, 0);
-          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_l, bhi[b][st], acc[b], 0, 0, 0);
-        }
-      }
-      // lane's 16 accumulators: chunk rows t0 + (r & 3) + 8 (r >> 2) + 4h of column c
+    for (int st = 0; st < kKSteps; ++st) {
+      const bf16x8 a_h = *reinterpret_cast<const bf16x8*>(ah + 16 * st);
+      const bf16x8 a_l = *reinterpret_cast<const bf16x8*>(al + 16 * st);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = t0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const bool ok = row < cnt;
-        const float qv = qn[row];
-#pragma unroll
-        for (int b = 0; b < kBlocks; ++b) {
-          const float x = fmaf(-2.f, acc[b][r], tn[b] + qv);
-          // negative d~ -> +0 (signed max on the bits); NaN sorts after every finite key
-          const uint32_t xb = (uint32_t)max(__float_as_int(x), 0);
-          top4_key(ck[b], ok ? ((xb & ~63u) | (uint32_t)row) : kNoKey);
-        }
+      for (int b = 0; b < kBlocks; ++b) {
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_h, bhi[b][st], acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_h, blo[b][st], acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_l, bhi[b][st], acc[b], 0, 0, 0);
       }
     }
-    // ---- fold the chunk's top-4 into the running top-4 (the chunk's 4th key bounds
-    // every row of the chunk it did not report, and so does the running 4th value)
+    // keys: v's bits (negative v -> +0 by a signed max; +inf / NaN sort after every
+    // finite key) with the row within the group of kFoldTiles tiles in the low bits
+    const uint32_t pair_row = (uint32_t)(t & (kFoldTiles - 1)) * kTile + 4 * h;
 #pragma unroll
-    for (int b = 0; b < kBlocks; ++b)
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t row = pair_row + (uint32_t)((r & 3) + 8 * (r >> 2));
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (ck[b][k] != kNoKey) top4_insert(best[b], __uint_as_float(ck[b][k] & ~63u), q0 + (int)(ck[b][k] & 63u));
+      for (int b = 0; b < kBlocks; ++b)
+        top4_key(ck[b], ((uint32_t)max(__float_as_int(acc[b][r]), 0) & ~kRowMask) | row);
+    }
+    // ---- fold the group's top-4 into the running top-4 (the group's 4th key bounds
+    // every row of the group it did not report, and so does the running 4th value)
+    if ((t & (kFoldTiles - 1)) == kFoldTiles - 1 || t + 1 == n_tiles) {
+      const int base = (t & ~(kFoldTiles - 1)) * kTile;
+#pragma unroll
+      for (int b = 0; b < kBlocks; ++b)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (ck[b][k] != kNoKey)
+            top4_insert(best[b], __uint_as_float(ck[b][k] & ~kRowMask), base + (int)(ck[b][k] & kRowMask));
+    }
   }
-  __syncthreads();
-  const float maxb = sqrtf(__uint_as_float(s_maxqn));
+  // the frame's max |b|^2, from its tiles'
+  float maxqn = 0.f;
+  for (int t = lane; t < n_tiles; t += 64) maxqn = fmaxf(maxqn, tile_max[(size_t)f * tpf + t]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) maxqn = fmaxf(maxqn, __shfl_xor(maxqn, off));
+  const float maxb = sqrtf(maxqn);
+  const float sK = sqrtf(__uint_as_float(*Kbits));
 
   // ---- merge the two row halves (lanes c and c + 32 own the same template row)
 #pragma unroll
@@ -352,18 +424,21 @@ __global__ __launch_bounds__(kThreads) void knn2_l2f32_kernel(
   if (h != 0) return;
 
   // ---- certify and re-rank with the exact distance
+  const float* base = des_q + (size_t)q_begin * D;
 #pragma unroll
   for (int b = 0; b < kBlocks; ++b) {
     const int i = tpl_row[b];
     if (i >= n_tpl) continue;
     const Top4& t = best[b];
-    const float ra = sqrtf(fmaxf(tn[b], 0.f));
-    // |d~ - d| <= eps for every listed value (units U = (|a| + max|b|)^2): norms 2 D u,
-    // 2 a.b through bf16x3 <= (3D 2u + 3 2^-18) U / 2 (split residual + fp32 accumulation
-    // of 3D exact bf16 products, rounding or truncating), two final roundings, and the
-    // key truncation 2^-17; bounded with margin by (6 (D + 4) u + 2^-15) U, u = 2^-24.
-    const float U = (ra + maxb) * (ra + maxb);
-    const float eps = (6.f * (float)(D + 4) * 5.9604645e-8f + 3.0517578e-5f) * U * 1.01f + 1e-30f;
+    // |v~ - v| for every listed value, with v = (|b|^2 + K)/2 - a.b exact and
+    // S = (|b|^2 + K)/2 + |a||b| <= U/2, U = (sqrt(K) + max|b|)^2, u = 2^-24: the norm and
+    // C roundings (D + 1) u S; the bf16x3 residual 3 2^-18 S; the fp32 accumulation of
+    // C and 3D exact bf16 products (rounding or truncating) (3D + 1) 2u 1.01 S; the key
+    // truncation kKeyTrunc S.  Sum <= (4 (D + 1) u + (3 2^-18 + kKeyTrunc) / 2) U, taken
+    // with margin as (5 (D + 2) u + 0.6 (3 2^-18 + kKeyTrunc)) U 1.02.
+    const float U = (sK + maxb) * (sK + maxb);
+    const float eps =
+        (5.f * (float)(D + 2) * 5.9604645e-8f + 0.6f * (1.1444092e-5f + kKeyTrunc)) * U * 1.02f + 1e-30f;
     const float thr = t.v[1] + 2.f * eps;
     int ncand;
     if (!(t.v[1] < INFINITY)) {
@@ -376,9 +451,9 @@ __global__ __launch_bounds__(kThreads) void knn2_l2f32_kernel(
       ncand = -1;
     }
     const size_t o = ((size_t)f * n_tpl + i) * 2;
-    if (ncand < 0) {
-      const int slot = atomicAdd(n_fallback, 1);
-      fallback[slot] = (int32_t)((size_t)f * n_tpl + i);
+    if (ncand < 0) {  // frame f's list (room for every template row)
+      const int slot = atomicAdd(&fb_cnt[f], 1);
+      fallback[(size_t)f * n_tpl + slot] = i;
       continue;
     }
     float d0 = FLT_MAX, d1 = FLT_MAX;
@@ -398,40 +473,121 @@ __global__ __launch_bounds__(kThreads) void knn2_l2f32_kernel(
   }
 }
 
-// Exact brute force for the rows phase 1 could not certify: one wave per row, lanes
-// stride over the frame's rows, then a wave-wide lexicographic top-2 merge.  Every wave
-// exits once the list is exhausted.
-__global__ __launch_bounds__(256) void knn2_l2f32_fallback_kernel(const float* __restrict__ des_tpl, int n_tpl, int D,
-                                                                  const float* __restrict__ des_q,
-                                                                  const int32_t* __restrict__ q_off,
-                                                                  const int32_t* __restrict__ fallback,
-                                                                  const int32_t* __restrict__ n_fallback,
-                                                                  int32_t* __restrict__ out_idx,
-                                                                  float* __restrict__ out_dist) {
-  const int lane = threadIdx.x & 63;
-  const int nw = gridDim.x * (blockDim.x >> 6);
-  const int n = *n_fallback;
-  for (int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w < n; w += nw) {
-    const int fi = fallback[w];
-    const int f = fi / n_tpl, i = fi - f * n_tpl;
-    const int q_begin = q_off[f], n_q = q_off[f + 1] - q_begin;
-    const float* a = des_tpl + (size_t)i * D;
-    float d0 = FLT_MAX, d1 = FLT_MAX;
-    int j0 = -1, j1 = -1;
-    for (int j = lane; j < n_q; j += 64)
-      top2_insert_exact(d0, j0, d1, j1, exact_dist_any(a, des_q + (size_t)(q_begin + j) * D, D), j);
-    for (int off = 32; off > 0; off >>= 1) {
-      const float e0 = __shfl_xor(d0, off), e1 = __shfl_xor(d1, off);
-      const int k0 = __shfl_xor(j0, off), k1 = __shfl_xor(j1, off);
-      if (k0 >= 0) top2_insert_exact(d0, j0, d1, j1, e0, k0);
-      if (k1 >= 0) top2_insert_exact(d0, j0, d1, j1, e1, k1);
+// Exact brute force for the rows phase 1 could not certify: frame f's listed template
+// rows (fb[f * n_tpl + k], k < fb_cnt[f]) in batches of up to kFbBatch, batch y of a
+// frame on workgroup (f, y mod kFbSplit).  Every frame row is read once per batch and
+// scored against the batch's rows (in LDS) -- each distance one lane's sequential fp64
+// sum, the build's definition -- then a wave-wide and a workgroup-wide lexicographic
+// top-2 merge per listed row.
+constexpr int kFbThreads = 256;
+constexpr int kFbBatch = 4;
+constexpr int kFbSplit = 8;
+
+template <int NB>
+__device__ __forceinline__ void fb_scan(const float (*sa)[kDP], const float* __restrict__ frame, int n_q, int D,
+                                        bool v4, int tid, float (&d0)[kFbBatch], int (&j0)[kFbBatch],
+                                        float (&d1)[kFbBatch], int (&j1)[kFbBatch]) {
+  for (int j = tid; j < n_q; j += kFbThreads) {
+    const float* row = frame + (size_t)j * D;
+    double S[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) S[b] = 0.0;
+    if (v4) {
+      for (int k = 0; k < D; k += 4) {
+        const float4 y = *reinterpret_cast<const float4*>(row + k);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const float4 x = *reinterpret_cast<const float4*>(&sa[b][k]);
+          double t = (double)x.x - (double)y.x;
+          S[b] += t * t;
+          t = (double)x.y - (double)y.y;
+          S[b] += t * t;
+          t = (double)x.z - (double)y.z;
+          S[b] += t * t;
+          t = (double)x.w - (double)y.w;
+          S[b] += t * t;
+        }
+      }
+    } else {
+      for (int k = 0; k < D; ++k) {
+        const double y = (double)row[k];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const double t = (double)sa[b][k] - y;
+          S[b] += t * t;
+        }
+      }
     }
-    if (lane == 0) {
-      const size_t o = (size_t)fi * 2;
-      out_idx[o] = j0;
-      out_idx[o + 1] = j1;
-      out_dist[o] = d0;
-      out_dist[o + 1] = d1;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) top2_insert_exact(d0[b], j0[b], d1[b], j1[b], sqrtf((float)S[b]), j);
+  }
+}
+
+__global__ __launch_bounds__(kFbThreads) void knn2_l2f32_fallback_kernel(const float* __restrict__ des_tpl, int n_tpl,
+                                                                         int D, const float* __restrict__ des_q,
+                                                                         const int32_t* __restrict__ q_off,
+                                                                         const int32_t* __restrict__ fb,
+                                                                         const int32_t* __restrict__ fb_cnt,
+                                                                         int32_t* __restrict__ out_idx,
+                                                                         float* __restrict__ out_dist) {
+  __shared__ __attribute__((aligned(16))) float sa[kFbBatch][kDP];
+  __shared__ float sd[kFbThreads / 64][kFbBatch][2];
+  __shared__ int sj[kFbThreads / 64][kFbBatch][2];
+  const int f = blockIdx.x;
+  const int cnt = fb_cnt[f];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q_begin = q_off[f], n_q = q_off[f + 1] - q_begin;
+  const bool v4 = (D & 3) == 0 && (reinterpret_cast<uintptr_t>(des_q) & 15) == 0;
+  for (int k0 = blockIdx.y * kFbBatch; k0 < cnt; k0 += kFbSplit * kFbBatch) {
+    const int nb = min(kFbBatch, cnt - k0);
+    __syncthreads();  // the previous batch's merge is done with sa / sd / sj
+    for (int e = tid; e < kFbBatch * kDP; e += kFbThreads) {
+      const int b = e / kDP, k = e - b * kDP;
+      sa[b][k] = (b < nb && k < D) ? des_tpl[(size_t)fb[(size_t)f * n_tpl + k0 + b] * D + k] : 0.f;
+    }
+    __syncthreads();
+    float d0[kFbBatch], d1[kFbBatch];
+    int j0[kFbBatch], j1[kFbBatch];
+#pragma unroll
+    for (int b = 0; b < kFbBatch; ++b) {
+      d0[b] = d1[b] = FLT_MAX;
+      j0[b] = j1[b] = -1;
+    }
+    const float* frame = des_q + (size_t)q_begin * D;
+    switch (nb) {  // workgroup-uniform
+      case 1: fb_scan<1>(sa, frame, n_q, D, v4, tid, d0, j0, d1, j1); break;
+      case 2: fb_scan<2>(sa, frame, n_q, D, v4, tid, d0, j0, d1, j1); break;
+      case 3: fb_scan<3>(sa, frame, n_q, D, v4, tid, d0, j0, d1, j1); break;
+      default: fb_scan<4>(sa, frame, n_q, D, v4, tid, d0, j0, d1, j1); break;
+    }
+#pragma unroll
+    for (int b = 0; b < kFbBatch; ++b) {
+      for (int off = 32; off > 0; off >>= 1) {
+        const float e0 = __shfl_xor(d0[b], off), e1 = __shfl_xor(d1[b], off);
+        const int m0 = __shfl_xor(j0[b], off), m1 = __shfl_xor(j1[b], off);
+        if (m0 >= 0) top2_insert_exact(d0[b], j0[b], d1[b], j1[b], e0, m0);
+        if (m1 >= 0) top2_insert_exact(d0[b], j0[b], d1[b], j1[b], e1, m1);
+      }
+      if (lane == 0) {
+        sd[wave][b][0] = d0[b];
+        sd[wave][b][1] = d1[b];
+        sj[wave][b][0] = j0[b];
+        sj[wave][b][1] = j1[b];
+      }
+    }
+    __syncthreads();
+    if (tid < nb) {
+      const int b = tid;
+      float e0 = sd[0][b][0], e1 = sd[0][b][1];
+      int m0 = sj[0][b][0], m1 = sj[0][b][1];
+      for (int v = 1; v < kFbThreads / 64; ++v)
+        for (int k = 0; k < 2; ++k)
+          if (sj[v][b][k] >= 0) top2_insert_exact(e0, m0, e1, m1, sd[v][b][k], sj[v][b][k]);
+      const size_t o = ((size_t)f * n_tpl + fb[(size_t)f * n_tpl + k0 + b]) * 2;
+      out_idx[o] = m0;
+      out_idx[o + 1] = m1;
+      out_dist[o] = e0;
+      out_dist[o + 1] = e1;
     }
   }
 }
@@ -451,28 +607,37 @@ int check_f32_args(const void* des_tpl, int n_tpl, int D, const void* des_q, con
 int launch_knn_f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const float* des_q, const int32_t* q_off,
                    int n_frames, int max_nq, int32_t* out_idx, float* out_dist, hipStream_t s) {
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
-  // workspace: fallback counter + list, then the split frame rows (512 B each) and their
-  // norms, sized for n_frames * max_nq rows (the CSR total is a device value)
+  // workspace: per-frame fallback counters and lists (room for every template row), K,
+  // the tiles' max |b|^2, then the tile images (tpf = ceil(max_nq / 32) per frame; the
+  // CSR total is a device value)
   const size_t rows = (size_t)n_frames * n_tpl;
-  const size_t qrows = (size_t)n_frames * (size_t)max(max_nq, 0);
-  const size_t fb_bytes = ((rows + 1) * sizeof(int32_t) + 255) & ~(size_t)255;
+  const int tpf = ceil_div(max(max_nq, 0), kTile);
+  const size_t cnt_bytes = ((size_t)n_frames * sizeof(int32_t) + 255) & ~(size_t)255;
+  const size_t fb_bytes = (rows * sizeof(int32_t) + 255) & ~(size_t)255;
+  const size_t norm_bytes = (256 + (size_t)n_frames * tpf * sizeof(float) + 255) & ~(size_t)255;
+  const size_t img_bytes = (size_t)n_frames * tpf * kImgBytes;
   void* ws = nullptr;
-  KCMC_TRY(workspace_alloc(ctx, &ws, fb_bytes + qrows * 512 + qrows * sizeof(float), s));
-  int32_t* n_fb = static_cast<int32_t*>(ws);
-  int32_t* fb = n_fb + 1;
-  uint2* qsplit = reinterpret_cast<uint2*>(static_cast<char*>(ws) + fb_bytes);
-  float* qnorm = reinterpret_cast<float*>(static_cast<char*>(ws) + fb_bytes + qrows * 512);
-  KCMC_TRY(hip_check(hipMemsetAsync(n_fb, 0, sizeof(int32_t), s), "hipMemsetAsync"));
-  if (max_nq > 0) {
-    hipLaunchKernelGGL(split_rows_kernel, dim3(ceil_div(max_nq, 8), n_frames), dim3(256), 0, s, des_q, D, q_off,
-                       n_frames, qsplit, qnorm, (long long)qrows);
-    KCMC_TRY(launch_check("split_rows_kernel"));
+  KCMC_TRY(workspace_alloc(ctx, &ws, cnt_bytes + fb_bytes + norm_bytes + img_bytes, s));
+  char* w = static_cast<char*>(ws);
+  int32_t* fb_cnt = reinterpret_cast<int32_t*>(w);
+  int32_t* fb = reinterpret_cast<int32_t*>(w + cnt_bytes);
+  unsigned* Kbits = reinterpret_cast<unsigned*>(w + cnt_bytes + fb_bytes);
+  float* tile_max = reinterpret_cast<float*>(w + cnt_bytes + fb_bytes + 256);
+  uint8_t* img = reinterpret_cast<uint8_t*>(w + cnt_bytes + fb_bytes + norm_bytes);
+  KCMC_TRY(hip_check(hipMemsetAsync(fb_cnt, 0, (size_t)n_frames * sizeof(int32_t), s), "hipMemsetAsync"));
+  KCMC_TRY(hip_check(hipMemsetAsync(Kbits, 0, sizeof(unsigned), s), "hipMemsetAsync"));
+  hipLaunchKernelGGL(tpl_norm_max_kernel, dim3(ceil_div(n_tpl, 8)), dim3(256), 0, s, des_tpl, n_tpl, D, Kbits);
+  KCMC_TRY(launch_check("tpl_norm_max_kernel"));
+  if (tpf > 0) {
+    hipLaunchKernelGGL(split_tiles_kernel, dim3(tpf, n_frames), dim3(256), 0, s, des_q, D, q_off, tpf, Kbits, img,
+                       tile_max);
+    KCMC_TRY(launch_check("split_tiles_kernel"));
   }
   hipLaunchKernelGGL(knn2_l2f32_kernel, dim3(ceil_div(n_tpl, kTplPerWG), n_frames), dim3(kThreads), 0, s, des_tpl,
-                     n_tpl, D, des_q, q_off, qsplit, qnorm, (long long)qrows, out_idx, out_dist, fb, n_fb);
+                     n_tpl, D, des_q, q_off, img, tpf, Kbits, tile_max, out_idx, out_dist, fb, fb_cnt);
   KCMC_TRY(launch_check("knn2_l2f32_kernel"));
-  hipLaunchKernelGGL(knn2_l2f32_fallback_kernel, dim3(512), dim3(256), 0, s, des_tpl, n_tpl, D, des_q, q_off, fb, n_fb,
-                     out_idx, out_dist);
+  hipLaunchKernelGGL(knn2_l2f32_fallback_kernel, dim3(n_frames, kFbSplit), dim3(kFbThreads), 0, s, des_tpl, n_tpl, D,
+                     des_q, q_off, fb, fb_cnt, out_idx, out_dist);
   KCMC_TRY(launch_check("knn2_l2f32_fallback_kernel"));
   return workspace_free(ctx, ws, s);
 }
