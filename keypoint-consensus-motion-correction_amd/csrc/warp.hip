@@ -296,6 +296,13 @@ __device__ __forceinline__ uint16_t round_q10(uint32_t S) {
 
 __device__ __forceinline__ uint32_t tap(const uint16_t* stile, int i) { return stile[i]; }
 
+// Bits 11-15 of v in one v_bfe_u32 (the backend otherwise selects a shift and a mask).
+__device__ __forceinline__ uint32_t bfe_11_5(uint32_t v) {
+  uint32_t r;
+  asm("v_bfe_u32 %0, %1, 11, 5" : "=v"(r) : "v"(v));
+  return r;
+}
+
 
 // Fast-path staging: chunk q = tid + 256k of the box in row-major order at kFastChunks
 // chunks per row (LDS offset 16q); chunks right of the box's own pitch are left unwritten
@@ -373,18 +380,34 @@ __device__ __forceinline__ void fast_rows(const uint16_t* stile, const int2* __r
   int2 org[Cfg::kTileH / 4];  // all row origins up front (scalar loads; the table is padded)
 #pragma unroll
   for (int i = 0; i < Cfg::kTileH / 4; ++i) org[i] = rt[i];
+  // Box-relative coordinates are carried scaled by 2^6: the tap's integer column / row
+  // (< 2^8 / 2^7 here) is then the high half of the word and the 1/32 fraction bits 11-15.
+  // One v_perm packs (column, row) as two u16 and one v_dot2_u32_u16 with (2, 2 * pitch)
+  // gives the tap's LDS byte offset (4 VALU per pixel fewer than shifts + mad).
+  // Exact: |X| < 2^18 before scaling, and two's-complement wrap-around commutes with << 6.
+  uint32_t ad6[2], bd6[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    ad6[p] = (uint32_t)ad[p] << 6;
+    bd6[p] = (uint32_t)bd[p] << 6;
+  }
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 pitch2 = {(unsigned short)2, (unsigned short)(2 * kFastPitch)};
+  const char* sbytes = reinterpret_cast<const char*>(stile);
 #pragma unroll
   for (int i = 0; i < Cfg::kTileH / 4; ++i) {
     const int y = yb + wave + 4 * i;  // wave-uniform
     if (!INTERIOR && y >= H) break;
-    const int X0 = org[i].x - ox, Y0 = org[i].y - oy;
+    const uint32_t X0 = (uint32_t)(org[i].x - ox) << 6, Y0 = (uint32_t)(org[i].y - oy) << 6;  // scalar
     uint32_t v[2][4], fx[2], fy[2];
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-      const int tX = X0 + ad[p], tY = Y0 + bd[p];
-      fx[p] = (tX >> 5) & 31;
-      fy[p] = (tY >> 5) & 31;
-      const uint16_t* t = stile + __umul24((uint32_t)(tY >> 10), (uint32_t)kFastPitch) + (uint32_t)(tX >> 10);
+      const uint32_t tX = X0 + ad6[p], tY = Y0 + bd6[p];
+      fx[p] = bfe_11_5(tX);
+      fy[p] = bfe_11_5(tY);
+      const uint32_t cr = __builtin_amdgcn_perm(tY, tX, 0x07060302u);  // (column, row) as u16 x 2
+      const uint32_t off = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, cr), pitch2, 0u, false);
+      const uint16_t* t = reinterpret_cast<const uint16_t*>(sbytes + off);
       v[p][0] = t[0];
       v[p][1] = t[1];
       v[p][2] = t[kFastPitch];
