@@ -8,12 +8,12 @@ K1 match (GPU) -> survivor bitmasks to host -> consensus (host, native) -> K2 RA
 Detection is not part of the path (no detector exists in this image; keypoints are
 synthetic, see kcmc_amd/synthetic.py).
 
-Steps are issued through pipeline.OverlappedSlabs, a software pipeline on one stream
-(device order match(k) -> warp(k-1) -> RANSAC(k); --pipeline-depth 3 for match(k) ->
-warp(k-2) -> RANSAC(k-1)): the host consensus of step k runs while step k-1's frames
-are warped; every step still runs every stage, and the pipeline is drained inside the
-timed region.  --serial runs the steps strictly one
-after another.
+Steps are issued through pipeline.OverlappedSlabs, a software pipeline (kernel stream:
+match(k) -> warp(k-1); RANSAC(k) on a second stream beside warp(k-1), --no-corun queues
+it behind the warp instead; --pipeline-depth 3 for match(k) -> warp(k-2) ->
+RANSAC(k-1)): the host consensus of step k runs while step k-1's frames are warped;
+every step still runs every stage, and the pipeline is drained inside the timed region.
+--serial runs the steps strictly one after another.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
@@ -350,6 +350,8 @@ def main():
                          "detection + the hot path (pipeline.align_frames); reported as `with_detection`")
     ap.add_argument("--pipeline-depth", type=int, default=2, choices=(2, 3),
                     help="slabs in flight in the pipelined schedule (pipeline.OverlappedSlabs depth)")
+    ap.add_argument("--no-corun", action="store_true",
+                    help="RANSAC behind the warp on the one kernel stream (OverlappedSlabs corun=False)")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
@@ -384,7 +386,7 @@ def main():
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s; {args.frames} frames {bc.H}x{bc.W}x{bc.C} on {dev}")
 
     ov = None if args.serial else pipeline.OverlappedSlabs(dev, cfg, counts=counts if world > 1 else None,
-                                                            depth=args.pipeline_depth)
+                                                            depth=args.pipeline_depth, corun=not args.no_corun)
 
     def step(timer):
         if ov is None:
@@ -446,7 +448,9 @@ def main():
         stage_ms["host_and_transfers"] = round(ms_step - match_ms - ransac_ms - warp_ms, 3)
     else:  # step k+1's match/consensus/RANSAC/post-processing overlap step k's warp
         stage_ms["schedule"] = ("pipelined: match(k) -> warp(k-1) -> RANSAC(k)" if args.pipeline_depth == 2 else
-                                "pipelined: match(k) -> warp(k-2) -> RANSAC(k-1)") + " on one stream, host consensus under the warp"
+                                "pipelined: match(k) -> warp(k-2) -> RANSAC(k-1)") + (
+                                    " on one stream" if args.no_corun else ", RANSAC on a second stream beside the warp"
+                                ) + ", host consensus under the warp"
         stage_ms["step_minus_warp"] = round(ms_step - warp_ms, 3)
     result = {
         "metric": METRIC,

@@ -250,18 +250,27 @@ class _SlabInFlight:
     params_host: Optional[torch.Tensor] = None
     params_ready: Optional[torch.cuda.Event] = None
     aligned: Optional[torch.Tensor] = None
+    matched: Optional[torch.cuda.Event] = None   # end of match(k) on the kernel stream (corun)
+    fitted_ev: Optional[torch.cuda.Event] = None  # end of RANSAC(k) on the analysis stream (corun)
 
 
 class OverlappedSlabs:
-    """Streams slabs through the hot path as a software pipeline on one stream.
+    """Streams slabs through the hot path as a software pipeline.
 
     submit(slab k) queues, in this device order (``depth=2``, the default),
 
-        match(k) -> warp(k-1) -> RANSAC(k)
+        kernel stream:    match(k) -> warp(k-1) -> [waits RANSAC(k)] -> warp(k) ...
+        analysis stream:              RANSAC(k)   (beside warp(k-1))
 
     with every transfer on a side stream: the host enqueues match(k) and the warp of the
     slab fitted last time, then waits for slab k's survivor bitmasks (VA:224-286
-    consensus) while warp(k-1) keeps the device busy, and queues RANSAC(k) behind it.
+    consensus) while warp(k-1) keeps the device busy, and queues RANSAC(k) on the
+    analysis stream, where it shares the CUs with warp(k-1) (``corun``, the default).
+    The warp is bound by HBM at the speed of a plain copy, so the FP64 RANSAC work mostly
+    fits beside it (c2: the warp slows by ~0.18 ms and 0.23 ms of RANSAC leave the step);
+    the match stays on the kernel stream (its persistent large-LDS workgroups starve
+    beside the warp's tiles and delay the consensus).  ``corun=False`` queues RANSAC(k)
+    behind warp(k-1) on the one kernel stream, so a step costs the sum of its kernels.
     ``depth=3`` queues match(k) -> warp(k-2) -> RANSAC(k-1) instead, so the consensus uses
     bitmasks that were ready a whole step earlier; same-box A/B
     found it no faster at c2 and slower at c3, so it is opt-in.  The warp of a slab reads
@@ -269,10 +278,7 @@ class OverlappedSlabs:
     reference's post-processing (VA:143-145) hands a frame with a model its own
     parameters, so only frames without a model need the host (NaN-gap interpolation); the
     warp writes zeros for those and they are warped again, with the filled maps, once the
-    host has them.  The kernels never share the CUs with each other (co-resident analysis
-    kernels slowed the warp by as much as they ran, and a large-LDS match workgroup
-    starves behind the warp's tiles), so a step costs the sum of its kernels unless the
-    host is slower.  With frame_downsample_rate > 1 every full-rate frame's map comes from
+    host has them.  With frame_downsample_rate > 1 every full-rate frame's map comes from
     the host interpolation, and the warp of slab k waits for it.  Every slab runs every
     stage and its results equal ``align_slab``'s.
 
@@ -292,7 +298,7 @@ class OverlappedSlabs:
     """
 
     def __init__(self, device, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
-                 counts: Optional[List[int]] = None, group=None, depth: int = 2):
+                 counts: Optional[List[int]] = None, group=None, depth: int = 2, corun: bool = True):
         if depth not in (2, 3):
             raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
         self.depth = depth
@@ -308,6 +314,11 @@ class OverlappedSlabs:
         self.group = group
         self.stream = torch.cuda.Stream(self.dev)
         self.copy = torch.cuda.Stream(self.dev)  # bitmask / point-list / params / map transfers
+        # corun: RANSAC(k) on an analysis stream, beside warp(k-1) instead of behind it (the
+        # warp of slab k waits for it).  Same-box A/B: faster at c2, c3
+        # and c5; the match stays on the kernel stream (beside the warp it starves).
+        self.corun = bool(corun)
+        self.ana = torch.cuda.Stream(self.dev) if self.corun else None
         self._matched: Optional[_SlabInFlight] = None  # match queued, consensus pending
         self._fitted: Optional[_SlabInFlight] = None   # RANSAC queued, warp pending
 
@@ -357,7 +368,11 @@ class OverlappedSlabs:
         else:
             f0 = 0
             keep_h, keep_ready = _d2h_async(match.keep_bits, self.copy)
-        return _SlabInFlight(inp, out, f0, match, keep_h, keep_ready)
+        p = _SlabInFlight(inp, out, f0, match, keep_h, keep_ready)
+        if self.corun:
+            p.matched = torch.cuda.Event()
+            p.matched.record()
+        return p
 
     def _fit(self, p: _SlabInFlight, mark) -> _SlabInFlight:
         """The consensus (host) and RANSAC (device) of a matched slab."""
@@ -369,10 +384,27 @@ class OverlappedSlabs:
         # the global consensus; with counts, point lists of this rank's frames only
         p.cons = consensus_stage(p.keep_host.numpy(), n_tpl, n_all, cfg, self.logger if self._rank() == 0 else None,
                                  frames=(p.f0, p.f0 + n_local) if self._sharded() else None)
+        if self.corun:
+            with torch.cuda.stream(self.ana):
+                self.ana.wait_event(p.matched)
+                for t in (p.match.kp_ordered, p.inp.kp_tpl):
+                    t.record_stream(self.ana)
+                self._fit_device(p, mark)
+                for t in vars(p.rr).values():
+                    if isinstance(t, torch.Tensor):
+                        t.record_stream(self.stream)
+                p.fitted_ev = torch.cuda.Event()
+                p.fitted_ev.record(self.ana)
+        else:
+            self._fit_device(p, mark)
+        return p
+
+    def _fit_device(self, p: _SlabInFlight, mark) -> None:
+        """RANSAC of a slab whose consensus is known, on the current stream."""
         pt_idx = p.cons.pt_idx if p.cons.pt_idx.size else np.zeros(1, np.int32)
         lists = tuple(_h2d_async((p.cons.pt_off, pt_idx), self.dev, self.copy))
         mark("r0")
-        p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, cfg, lists_dev=lists)
+        p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, lists_dev=lists)
         mark("r1")
         if self._sharded():
             from .distributed import _all_gather_rows
@@ -381,9 +413,10 @@ class OverlappedSlabs:
                                                        self.copy)
         else:
             p.params_host, p.params_ready = _d2h_async(p.rr.params, self.copy)
-        return p
 
     def _warp_device_maps(self, p: _SlabInFlight, mark) -> None:
+        if p.fitted_ev is not None:
+            self.stream.wait_event(p.fitted_ev)
         mark("w0")
         p.aligned = warp_frames(p.inp.frames, p.rr.params, out=p.out)
         mark("w1")
@@ -391,6 +424,8 @@ class OverlappedSlabs:
     def _finish(self, p: _SlabInFlight, mark) -> SlabResult:
         """Host post-processing of slab p (VA:143-145) and the warps that need its maps."""
         p.params_ready.synchronize()
+        if p.fitted_ev is not None:
+            self.stream.wait_event(p.fitted_ev)
         affines, skipped, interpolated, eu = postprocess_affines(p.params_host.numpy(), self.cfg)
         n = p.inp.frames.shape[0]
         local = np.asarray(affines[p.f0:p.f0 + n], dtype=np.float64)
@@ -432,6 +467,8 @@ class OverlappedSlabs:
 
     def synchronize(self) -> None:
         self.stream.synchronize()
+        if self.ana is not None:
+            self.ana.synchronize()
         self.copy.synchronize()
 
 
