@@ -96,6 +96,60 @@ __device__ __forceinline__ double pw_leaf(const Model& m, const Pts& P, int star
   return res;
 }
 
+// Phase A of the scoring (see the kernel): the inlier count through the squared
+// distance (r < thresh <=> q < tq, tq = the smallest double whose correctly rounded root
+// is >= thresh; the q of every point is computed exactly as resid2 computes it) and an
+// fp32 estimate of S = sum r_k^2: sum_k (float)q_k in sequence.  r_k^2 = q_k (1 + d),
+// |d| <= 3 2^-53, numpy's pairwise sum adds <= N 2^-53 and the fp32 sum of N
+// conversions <= (N + 1) 2^-24, so for S32 >= 1e-30 (no fp32 underflow matters)
+// |S - S32| <= (N + 2) 2^-23 S32, used with a 2x margin.
+__device__ __forceinline__ float score_fast(const Model& m, const Pts& P, int N, double tq, int& cnt) {
+  float S = 0.f;
+  for (int k = 0; k < N; ++k) {
+    const double x = P.sx[k], y = P.sy[k];
+    const double xp = fma(y, -m.s, x * m.c) + m.tx;
+    const double yp = fma(y, m.c, x * m.s) + m.ty;
+    const double ex = xp - P.dx[k], ey = yp - P.dy[k];
+    const double q = ex * ex + ey * ey;
+    cnt += (q < tq) ? 1 : 0;
+    S += (float)q;
+  }
+  return S;
+}
+
+// numpy's pairwise leaf (pw_leaf) over points [start, start + n), n <= 128, evaluated by
+// one whole wave: the lanes write r_k^2 to the wave's LDS row `vals`, lanes j < 8 run
+// accumulator j's sequential sum, and every lane then finishes the same combine and
+// remainder (wave-uniform result).  Bit-identical to pw_leaf.
+__device__ __forceinline__ double wave_leaf(const Model& m, const Pts& P, int start, int n, double thresh,
+                                            double* vals, int lane) {
+  for (int k = lane; k < n; k += 64) {
+    int c = 0;
+    vals[k] = resid2(m, P, start + k, thresh, c);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double res = 0.0;
+  if (n < 8) {
+    for (int i = 0; i < n; ++i) res += vals[i];
+  } else {
+    const int j = lane & 7;
+    const int nfull = n - (n % 8);
+    double r = vals[j];
+    for (int i = j + 8; i < nfull; i += 8) r += vals[i];
+    double rj[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rj[q] = __shfl(r, q);
+    res = ((rj[0] + rj[1]) + (rj[2] + rj[3])) + ((rj[4] + rj[5]) + (rj[6] + rj[7]));
+    for (int i = nfull; i < n; ++i) res += vals[i];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();  // vals is rewritten by the next leaf
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return res;
+}
+
 // For N > 128 the numpy pairwise order comes from the per-frame split Plan
 // (ransac_common.h); invalid trials (NaN S, or 0 inliers with S = inf) never win.
 // LARGE = false handles frames with N <= 128 (one pairwise leaf, fully in registers)
@@ -105,10 +159,12 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
     const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint32_t* __restrict__ hyp,
     const int32_t* __restrict__ hyp_off, int hyp_off_len,
-    int T, double thresh, double rate, int n_skip, double* __restrict__ out_params,
+    int T, double thresh, double tq, double rate, int n_skip, double* __restrict__ out_params,
     uint8_t* __restrict__ out_inl, int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ double red[kThreads / 64 * 4];
+  __shared__ int s_cnt[kThreads / 64];
+  __shared__ double s_min[kThreads / 64];
   __shared__ int s_best[kThreads / 64 * 2];
   __shared__ double s_bestS[kThreads / 64];
   __shared__ int s_any_zero;
@@ -136,14 +192,15 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
   }
 
   // LDS: sx, sy, dx, dy [N] f64 | trial S [T] f64 | [LARGE: stack [kMaxStack][256] f64]
-  //      | trial count [T] i32 | inlier flags [N] u8
+  //      | per-wave leaf values [4][128] f64 | trial count [T] i32 | inlier flags [N] u8
   double* sx = smem;
   double* sy = sx + N;
   double* dxs = sy + N;
   double* dys = dxs + N;
   double* tS = dys + N;
   double* stk = tS + T;
-  int* tC = reinterpret_cast<int*>(stk + (LARGE ? kMaxStack * kThreads : 0));
+  double* wvals = stk + (LARGE ? kMaxStack * kThreads : 0);
+  int* tC = reinterpret_cast<int*>(wvals + kThreads / 64 * 128);
   uint8_t* inl = reinterpret_cast<uint8_t*>(tC + T);
   if (LARGE && tid == 0) {
     s_plan.n = 0;
@@ -169,40 +226,126 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
 
   const Pts P{sx, sy, dxs, dys};
   const uint32_t* H = hyp + hoff;
+
+  // ---- phase A: every trial's inlier count (exact, through q < tq) and fp32 S estimate.
+  // Then the best count is known exactly, and only trials at that count whose S can be
+  // within the estimates' error of the smallest one need the exact S (phase B, one whole
+  // wave per candidate).  Frames where that does not hold -- no trial with inliers, an
+  // estimate outside [1e-30, 1e30] (so also every S == 0, skimage's early exit), or a
+  // NaN tq -- score every trial exactly (the original single-phase loop).
+  const bool fast = tq == tq;  // NaN: exact scoring only (threshold outside the fast range)
+  int mcount = -1, flag = fast ? 0 : 1;
+  if (fast) {
+    for (int t = tid; t < T; t += kThreads) {
+      const uint32_t pr = H[t];
+      const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
+      const Model m = fit2(sx[i], sy[i], sx[j], sy[j], dxs[i], dys[i], dxs[j], dys[j]);
+      int cnt = -1;
+      float S32 = NAN;
+      if (m.ok) {
+        cnt = 0;
+        S32 = score_fast(m, P, N, tq, cnt);
+        if (!(S32 >= 1e-30f && S32 <= 1e30f)) flag = 1;
+      }
+      tC[t] = cnt;
+      tS[t] = (double)S32;
+      mcount = max(mcount, cnt);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mcount = max(mcount, __shfl_xor(mcount, o));
+    flag |= __shfl_xor(flag, o);
+  }
+  if (lane == 0) s_cnt[wave] = (mcount + 1) | (flag << 30);  // counts <= kMaxN
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) {
+    const int v = s_cnt[w];
+    flag |= v >> 30;
+    mcount = max(mcount, (v & 0x3fffffff) - 1);
+  }
+  const bool exact = flag != 0 || mcount <= 0;
+
   int bc = -1, bt = INT_MAX;
   double bS = INFINITY;
   bool any_zero = false;
-  for (int t = tid; t < T; t += kThreads) {
-    const uint32_t pr = H[t];
-    const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
-    const Model m = fit2(sx[i], sy[i], sx[j], sy[j], dxs[i], dys[i], dxs[j], dys[j]);
-    int cnt = 0;
-    double S = NAN;
-    if (m.ok) {
-      if (!LARGE) {
-        S = pw_leaf(m, P, 0, N, thresh, cnt);
-      } else {
-        int sp = 0;
-        for (int l = 0; l < s_plan.n; ++l) {
-          stk[sp++ * kThreads + tid] = pw_leaf(m, P, s_plan.start[l], s_plan.len[l], thresh, cnt);
-          for (int c = s_plan.pops[l]; c > 0; --c) {
-            const double b = stk[--sp * kThreads + tid];
-            const double a = stk[(sp - 1) * kThreads + tid];
-            stk[(sp - 1) * kThreads + tid] = a + b;
+  if (exact) {
+    for (int t = tid; t < T; t += kThreads) {
+      const uint32_t pr = H[t];
+      const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
+      const Model m = fit2(sx[i], sy[i], sx[j], sy[j], dxs[i], dys[i], dxs[j], dys[j]);
+      int cnt = 0;
+      double S = NAN;
+      if (m.ok) {
+        if (!LARGE) {
+          S = pw_leaf(m, P, 0, N, thresh, cnt);
+        } else {
+          int sp = 0;
+          for (int l = 0; l < s_plan.n; ++l) {
+            stk[sp++ * kThreads + tid] = pw_leaf(m, P, s_plan.start[l], s_plan.len[l], thresh, cnt);
+            for (int c = s_plan.pops[l]; c > 0; --c) {
+              const double b = stk[--sp * kThreads + tid];
+              const double a = stk[(sp - 1) * kThreads + tid];
+              stk[(sp - 1) * kThreads + tid] = a + b;
+            }
           }
+          S = stk[tid];
         }
-        S = stk[tid];
+      }
+      tS[t] = S;
+      tC[t] = cnt;
+      const bool valid = !isnan(S) && (cnt > 0 || S < INFINITY);
+      if (valid) {
+        if (S <= 0.0) any_zero = true;
+        if (better(cnt, S, t, bc, bS, bt)) {
+          bc = cnt;
+          bS = S;
+          bt = t;
+        }
       }
     }
-    tS[t] = S;
-    tC[t] = cnt;
-    const bool valid = !isnan(S) && (cnt > 0 || S < INFINITY);
-    if (valid) {
-      if (S <= 0.0) any_zero = true;
-      if (better(cnt, S, t, bc, bS, bt)) {
-        bc = cnt;
-        bS = S;
-        bt = t;
+  } else {
+    const double eps = (double)(N + 2) * 0x1p-22;
+    double lm = INFINITY;
+    for (int t = tid; t < T; t += kThreads)
+      if (tC[t] == mcount) lm = fmin(lm, tS[t] * (1.0 + eps));
+    for (int o = 32; o > 0; o >>= 1) lm = fmin(lm, __shfl_xor(lm, o));
+    if (lane == 0) s_min[wave] = lm;
+    __syncthreads();
+    const double minhi = fmin(fmin(s_min[0], s_min[1]), fmin(s_min[2], s_min[3]));
+    double* vals = wvals + wave * 128;
+    double* wstk = stk + wave * kMaxStack;  // LARGE: the wave's combine stack (uniform values)
+    // phase B: this wave's candidate trials (t = t0 + lane), each scored by the whole wave
+    for (int t0 = wave * 64; t0 < T; t0 += kThreads) {
+      const int t = t0 + lane;
+      uint64_t cand = __ballot(t < T && tC[t] == mcount && tS[t] * (1.0 - eps) <= minhi);
+      while (cand) {
+        const int tc = t0 + __builtin_ctzll(cand);
+        cand &= cand - 1;
+        const uint32_t pr = H[tc];
+        const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
+        const Model m = fit2(sx[i], sy[i], sx[j], sy[j], dxs[i], dys[i], dxs[j], dys[j]);
+        double S;
+        if (!LARGE) {
+          S = wave_leaf(m, P, 0, N, thresh, vals, lane);
+        } else {
+          int sp = 0;
+          for (int l = 0; l < s_plan.n; ++l) {
+            const double v = wave_leaf(m, P, s_plan.start[l], s_plan.len[l], thresh, vals, lane);
+            wstk[sp++] = v;
+            for (int c = s_plan.pops[l]; c > 0; --c) {
+              const double b = wstk[--sp];
+              const double a = wstk[sp - 1];
+              wstk[sp - 1] = a + b;
+            }
+          }
+          S = wstk[0];
+        }
+        if (!isnan(S) && better(mcount, S, tc, bc, bS, bt)) {  // wave-uniform
+          bc = mcount;
+          bS = S;
+          bt = tc;
+        }
       }
     }
   }
@@ -323,6 +466,19 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
   (void)nin_local;
 }
 
+// tq = the smallest double whose correctly rounded square root is >= thresh, so that
+// sqrt(q) < thresh <=> q < tq for every q (the root is monotone; NaN compares false
+// either way).  The kernel's sqrt_resid is the correctly rounded root for q >= 2^-767,
+// so thresholds whose tq falls below that (or non-finite / non-positive ones) return NaN:
+// exact scoring only.
+double inlier_bound(double thresh) {
+  if (!(thresh > 0x1p-380 && thresh < 0x1p500)) return NAN;
+  double q = thresh * thresh;
+  while (std::sqrt(q) < thresh) q = std::nextafter(q, INFINITY);
+  for (double p = std::nextafter(q, 0.0); std::sqrt(p) >= thresh; p = std::nextafter(q, 0.0)) q = p;
+  return q;
+}
+
 }  // namespace
 }  // namespace kcmc
 
@@ -344,21 +500,23 @@ extern "C" int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src, const double*
     return fail(KCMC_EINVAL, "kcmc_ransac_rigid: hypothesis tables not prepared for trials=" +
                                  std::to_string(trials) + " (call kcmc_ransac_prepare)");
   const int n_small = need < 128 ? need : 128;
-  const size_t lds_small =
-      (size_t)n_small * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) + (size_t)n_small + 16;
+  const size_t wvals = (size_t)kThreads / 64 * 128 * sizeof(double);
+  const size_t lds_small = (size_t)n_small * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) +
+                           wvals + (size_t)n_small + 16;
   const size_t lds_large = (size_t)need * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) +
-                           (size_t)kMaxStack * kThreads * sizeof(double) + (size_t)need + 16;
+                           (size_t)kMaxStack * kThreads * sizeof(double) + wvals + (size_t)need + 16;
+  const double tq = inlier_bound(thresh);
   if ((max_n > 128 ? lds_large : lds_small) > 150 * 1024)
     return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_rigid: max_n/trials exceed the LDS budget");
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(ransac_rigid_kernel<false>, dim3(n_frames), dim3(kThreads), lds_small, s, src, dst, pt_idx,
-                     pt_off, src_frame_stride, ctx->hyp, ctx->hyp_off, ctx->hyp_off_len, trials, thresh, rate, n_skip, out_params,
-                     out_inliers, out_n_inliers, out_best_trial);
+                     pt_off, src_frame_stride, ctx->hyp, ctx->hyp_off, ctx->hyp_off_len, trials, thresh, tq, rate, n_skip,
+                     out_params, out_inliers, out_n_inliers, out_best_trial);
   KCMC_TRY(launch_check("ransac_rigid_kernel<small>"));
   if (max_n > 128) {
     hipLaunchKernelGGL(ransac_rigid_kernel<true>, dim3(n_frames), dim3(kThreads), lds_large, s, src, dst, pt_idx,
-                       pt_off, src_frame_stride, ctx->hyp, ctx->hyp_off, ctx->hyp_off_len, trials, thresh, rate, n_skip, out_params,
-                       out_inliers, out_n_inliers, out_best_trial);
+                       pt_off, src_frame_stride, ctx->hyp, ctx->hyp_off, ctx->hyp_off_len, trials, thresh, tq, rate, n_skip,
+                       out_params, out_inliers, out_n_inliers, out_best_trial);
     KCMC_TRY(launch_check("ransac_rigid_kernel<large>"));
   }
   return KCMC_OK;

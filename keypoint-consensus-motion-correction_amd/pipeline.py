@@ -338,7 +338,7 @@ class OverlappedSlabs:
     def submit(self, inp: SlabInputs, out: Optional[torch.Tensor] = None,
                mark: Optional[Callable[[str], None]] = None) -> Optional[SlabResult]:
         mark = mark or (lambda name: None)
-        self.stream.wait_stream(torch.cuda.current_stream(self.dev))
+        self._wait_current()
         with torch.cuda.stream(self.stream):
             for t in (inp.frames, out):
                 if t is not None:
@@ -354,6 +354,18 @@ class OverlappedSlabs:
                     self._fitted = self._fit(self._matched, mark)  # RANSAC(k-1) after warp(k-2)
                 self._matched = new
             return self._finish(fitted, mark) if fitted is not None else None
+
+    def _wait_current(self) -> None:
+        """Order the kernel stream after the caller's stream (the slab's inputs), but only
+        when the caller's stream still has work queued: a cross-stream wait that is already
+        satisfied still costs the device tens of microseconds."""
+        cur = torch.cuda.current_stream(self.dev)
+        if cur == self.stream:
+            return
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        if not ev.query():
+            self.stream.wait_event(ev)
 
     def _match(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
         mark("m0")
@@ -416,16 +428,20 @@ class OverlappedSlabs:
 
     def _warp_device_maps(self, p: _SlabInFlight, mark) -> None:
         if p.fitted_ev is not None:
-            self.stream.wait_event(p.fitted_ev)
+            # RANSAC(k) ran beside warp(k-1) on the analysis stream: the host waits for it
+            # (it has nothing else to do before it blocks on this step's bitmasks) instead
+            # of queueing a cross-stream wait, which leaves the device idle for tens of
+            # microseconds even when RANSAC finished long before
+            p.fitted_ev.synchronize()
         mark("w0")
         p.aligned = warp_frames(p.inp.frames, p.rr.params, out=p.out)
         mark("w1")
 
     def _finish(self, p: _SlabInFlight, mark) -> SlabResult:
         """Host post-processing of slab p (VA:143-145) and the warps that need its maps."""
-        p.params_ready.synchronize()
+        p.params_ready.synchronize()  # after RANSAC(k): its parameters are on the host
         if p.fitted_ev is not None:
-            self.stream.wait_event(p.fitted_ev)
+            p.fitted_ev.synchronize()
         affines, skipped, interpolated, eu = postprocess_affines(p.params_host.numpy(), self.cfg)
         n = p.inp.frames.shape[0]
         local = np.asarray(affines[p.f0:p.f0 + n], dtype=np.float64)
