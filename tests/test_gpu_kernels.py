@@ -249,6 +249,41 @@ def test_ransac_inlier_threshold_boundary(dev, thresh):
     assert 36 <= ni < 60
 
 
+@pytest.mark.parametrize("thresh", [2.0, 1e-120, 5e-5])
+def test_ransac_two_phase_ties_and_exact_fallback(dev, thresh):
+    """Phase A (counts through q < tq, fp32 S estimates) hands phase B every trial whose S
+    can tie the best: near-ties (a nearly noise-free inlier set: many two-point models
+    with S within 1e-9 relative), exact ties (duplicated points give identical models:
+    the lower trial wins), N > 128 (the wave-evaluated pairwise plan) -- and the frames it
+    cannot certify fall back to exact scoring: a threshold whose tq is outside the range
+    (1e-120), no trial with inliers (5e-5 on noisy data), exact data (S == 0)."""
+    rng = np.random.default_rng(int(-np.log10(thresh)) + 31)
+    tpls, qs = [], []
+    for N, noise in [(40, 1e-9), (90, 1e-6), (90, 0.3), (150, 1e-7), (300, 0.5), (12, 0.0)]:
+        tpl = rng.uniform(0, 1000, (N, 2))
+        A = synthetic.rigid(rng.normal(0, 0.02), rng.normal(0, 5), rng.normal(0, 5))
+        q = (tpl - A[:, 2]) @ A[:, :2] + rng.normal(0, noise, (N, 2)) if noise else tpl - np.array([3.0, 1.0])
+        if N == 90 and noise == 0.3:  # duplicates: swapped / repeated pairs fit identical models
+            q[45:], tpl[45:] = q[:45], tpl[:45]
+        tpls.append(tpl)
+        qs.append(q)
+    off, params, inl, nin, best = _ransac_t(dev, tpls, qs, thresh)
+    for f in range(len(qs)):
+        p, i_ref, bt, ni = oracle.ransac_rigid(qs[f], tpls[f], thresh=thresh)
+        assert best[f] == bt, f
+        assert nin[f] == ni, f
+        assert np.array_equal(inl[off[f]:off[f + 1]], i_ref), f
+        np.testing.assert_allclose(params[f], p, rtol=1e-10, atol=1e-10, equal_nan=True)
+
+
+def _ransac_t(dev, tpls, qs, thresh):
+    off = _csr(qs)
+    r = stages.ransac_rigid(_t(np.concatenate(qs).reshape(-1, 2), dev), _t(np.concatenate(tpls).reshape(-1, 2), dev),
+                            _t(off, dev), off, residual_threshold=thresh)
+    return off, r.params.cpu().numpy(), r.inliers.cpu().numpy().astype(bool), r.n_inliers.cpu().numpy(), \
+        r.best_trial.cpu().numpy()
+
+
 def test_ransac_gather_mode_matches_contiguous(dev):
     rng = np.random.default_rng(23)
     n_tpl, F = 60, 7
