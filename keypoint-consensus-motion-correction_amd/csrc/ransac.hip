@@ -117,39 +117,6 @@ __device__ __forceinline__ float score_fast(const Model& m, const Pts& P, int N,
   return S;
 }
 
-// numpy's pairwise leaf (pw_leaf) over points [start, start + n), n <= 128, evaluated by
-// one whole wave: the lanes write r_k^2 to the wave's LDS row `vals`, lanes j < 8 run
-// accumulator j's sequential sum, and every lane then finishes the same combine and
-// remainder (wave-uniform result).  Bit-identical to pw_leaf.
-__device__ __forceinline__ double wave_leaf(const Model& m, const Pts& P, int start, int n, double thresh,
-                                            double* vals, int lane) {
-  for (int k = lane; k < n; k += 64) {
-    int c = 0;
-    vals[k] = resid2(m, P, start + k, thresh, c);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  double res = 0.0;
-  if (n < 8) {
-    for (int i = 0; i < n; ++i) res += vals[i];
-  } else {
-    const int j = lane & 7;
-    const int nfull = n - (n % 8);
-    double r = vals[j];
-    for (int i = j + 8; i < nfull; i += 8) r += vals[i];
-    double rj[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) rj[q] = __shfl(r, q);
-    res = ((rj[0] + rj[1]) + (rj[2] + rj[3])) + ((rj[4] + rj[5]) + (rj[6] + rj[7]));
-    for (int i = nfull; i < n; ++i) res += vals[i];
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();  // vals is rewritten by the next leaf
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  return res;
-}
-
 // For N > 128 the numpy pairwise order comes from the per-frame split Plan
 // (ransac_common.h); invalid trials (NaN S, or 0 inliers with S = inf) never win.
 // LARGE = false handles frames with N <= 128 (one pairwise leaf, fully in registers)
@@ -245,7 +212,7 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
       if (m.ok) {
         cnt = 0;
         S32 = score_fast(m, P, N, tq, cnt);
-        if (!(S32 >= 1e-30f && S32 <= 1e30f)) flag = 1;
+        if (!s32_certain(S32)) flag = 1;
       }
       tC[t] = cnt;
       tS[t] = (double)S32;
@@ -305,7 +272,7 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
       }
     }
   } else {
-    const double eps = (double)(N + 2) * 0x1p-22;
+    const double eps = s32_eps(N);
     double lm = INFINITY;
     for (int t = tid; t < T; t += kThreads)
       if (tC[t] == mcount) lm = fmin(lm, tS[t] * (1.0 + eps));
@@ -325,22 +292,12 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
         const uint32_t pr = H[tc];
         const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
         const Model m = fit2(sx[i], sy[i], sx[j], sy[j], dxs[i], dys[i], dxs[j], dys[j]);
-        double S;
-        if (!LARGE) {
-          S = wave_leaf(m, P, 0, N, thresh, vals, lane);
-        } else {
-          int sp = 0;
-          for (int l = 0; l < s_plan.n; ++l) {
-            const double v = wave_leaf(m, P, s_plan.start[l], s_plan.len[l], thresh, vals, lane);
-            wstk[sp++] = v;
-            for (int c = s_plan.pops[l]; c > 0; --c) {
-              const double b = wstk[--sp];
-              const double a = wstk[sp - 1];
-              wstk[sp - 1] = a + b;
-            }
-          }
-          S = wstk[0];
-        }
+        const double S = wave_pairwise<LARGE>(
+            [&](int k) {
+              int c = 0;
+              return resid2(m, P, k, thresh, c);
+            },
+            N, s_plan, vals, wstk, lane);
         if (!isnan(S) && better(mcount, S, tc, bc, bS, bt)) {  // wave-uniform
           bc = mcount;
           bS = S;
@@ -464,19 +421,6 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
     out_best[f] = best_t;
   }
   (void)nin_local;
-}
-
-// tq = the smallest double whose correctly rounded square root is >= thresh, so that
-// sqrt(q) < thresh <=> q < tq for every q (the root is monotone; NaN compares false
-// either way).  The kernel's sqrt_resid is the correctly rounded root for q >= 2^-767,
-// so thresholds whose tq falls below that (or non-finite / non-positive ones) return NaN:
-// exact scoring only.
-double inlier_bound(double thresh) {
-  if (!(thresh > 0x1p-380 && thresh < 0x1p500)) return NAN;
-  double q = thresh * thresh;
-  while (std::sqrt(q) < thresh) q = std::nextafter(q, INFINITY);
-  for (double p = std::nextafter(q, 0.0); std::sqrt(p) >= thresh; p = std::nextafter(q, 0.0)) q = p;
-  return q;
 }
 
 }  // namespace

@@ -4,6 +4,7 @@
 #pragma once
 
 #include <climits>
+#include <cmath>
 #include <cstdint>
 
 #include "kcmc_internal.h"
@@ -75,6 +76,72 @@ __device__ __forceinline__ bool better(int c, double S, int t, int bc, double bS
   if (S != bS) return S < bS;
   return t < bt;
 }
+
+// tq = the smallest double whose correctly rounded square root is >= thresh, so that
+// sqrt(q) < thresh <=> q < tq for every q (the root is monotone; NaN compares false
+// either way): the scoring kernels' phase A counts inliers without the root.
+// sqrt_resid is the correctly rounded root for q >= 2^-767, so thresholds whose tq falls
+// below that (or non-finite / non-positive ones) return NaN: exact scoring only.
+inline double inlier_bound(double thresh) {
+  if (!(thresh > 0x1p-380 && thresh < 0x1p500)) return NAN;
+  double q = thresh * thresh;
+  while (std::sqrt(q) < thresh) q = std::nextafter(q, INFINITY);
+  for (double p = std::nextafter(q, 0.0); std::sqrt(p) >= thresh; p = std::nextafter(q, 0.0)) q = p;
+  return q;
+}
+
+// Phase B of the scoring kernels: numpy's pairwise leaf (8 strided accumulators for
+// n >= 8, sequential below; n <= 128) over r2(start + k), evaluated by one whole wave:
+// the lanes write the values to the wave's LDS row `vals`, lanes j < 8 run accumulator
+// j's sequential sum, and every lane finishes the same combine and remainder
+// (wave-uniform result, bit-identical to a one-thread pw_leaf).
+template <class R2>
+__device__ __forceinline__ double wave_leaf(R2 r2, int start, int n, double* vals, int lane) {
+  for (int k = lane; k < n; k += 64) vals[k] = r2(start + k);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double res = 0.0;
+  if (n < 8) {
+    for (int i = 0; i < n; ++i) res += vals[i];
+  } else {
+    const int j = lane & 7;
+    const int nfull = n - (n % 8);
+    double r = vals[j];
+    for (int i = j + 8; i < nfull; i += 8) r += vals[i];
+    double rj[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rj[q] = __shfl(r, q);
+    res = ((rj[0] + rj[1]) + (rj[2] + rj[3])) + ((rj[4] + rj[5]) + (rj[6] + rj[7]));
+    for (int i = nfull; i < n; ++i) res += vals[i];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();  // vals is rewritten by the next leaf
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return res;
+}
+
+// The exact S of one trial by one wave: a single leaf for N <= 128, else numpy's split
+// plan with the combine stack in the wave's LDS slots `wstk` (uniform values).
+template <bool LARGE, class R2>
+__device__ __forceinline__ double wave_pairwise(R2 r2, int N, const Plan& plan, double* vals, double* wstk, int lane) {
+  if (!LARGE) return wave_leaf(r2, 0, N, vals, lane);
+  int sp = 0;
+  for (int l = 0; l < plan.n; ++l) {
+    wstk[sp++] = wave_leaf(r2, plan.start[l], plan.len[l], vals, lane);
+    for (int c = plan.pops[l]; c > 0; --c) {
+      const double b = wstk[--sp];
+      const double a = wstk[sp - 1];
+      wstk[sp - 1] = a + b;
+    }
+  }
+  return wstk[0];
+}
+
+// Phase A's error bound (the kernels' comment): |S - S32| <= eps S32 for S32 in
+// [1e-30, 1e30], with a 2x margin.
+__device__ __forceinline__ double s32_eps(int N) { return (double)(N + 2) * 0x1p-22; }
+__device__ __forceinline__ bool s32_certain(float S32) { return S32 >= 1e-30f && S32 <= 1e30f; }
 
 __device__ inline double block_sum(double v, double* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

@@ -271,6 +271,29 @@ __device__ __forceinline__ double pw_leaf(const double (&h)[9], const Pts& P, in
   return res;
 }
 
+// Phase A of the scoring (the rigid kernel's, ransac.hip): the exact inlier count through
+// q < tq (q computed as resid2 computes it) and the fp32 estimate S32 = sum (float)q_k.
+template <int MODEL>
+__device__ __forceinline__ float score_fast(const double (&h)[9], const Pts& P, int N, double tq, int& cnt) {
+  float S = 0.f;
+  for (int k = 0; k < N; ++k) {
+    const double x = P.sx[k], y = P.sy[k];
+    double X = fma(y, h[1], x * h[0]) + h[2];
+    double Y = fma(y, h[4], x * h[3]) + h[5];
+    if (MODEL == KCMC_MODEL_PROJECTIVE) {
+      double w = fma(y, h[7], x * h[6]) + h[8];
+      if (w == 0.0) w = DBL_EPSILON;
+      X = X / w;
+      Y = Y / w;
+    }
+    const double ex = X - P.dx[k], ey = Y - P.dy[k];
+    const double q = ex * ex + ey * ey;
+    cnt += (q < tq) ? 1 : 0;
+    S += (float)q;
+  }
+  return S;
+}
+
 template <int MODEL>
 __device__ __forceinline__ HModel fit_trial(const Pts& P, uint64_t pr) {
   if constexpr (MODEL == KCMC_MODEL_AFFINE) {
@@ -307,11 +330,13 @@ template <int MODEL, bool LARGE>
 __global__ __launch_bounds__(kThreads) void ransac_model_score_kernel(
     const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint64_t* __restrict__ hyp,
-    const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, int n_skip,
+    const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, double tq, int n_skip,
     double* out_params, double* best_model, uint8_t* __restrict__ out_inl,
     int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
   constexpr int K = MODEL == KCMC_MODEL_AFFINE ? 3 : 4;
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int s_cnt[kThreads / 64];
+  __shared__ double s_min[kThreads / 64];
   __shared__ int s_best[kThreads / 64 * 2];
   __shared__ double s_bestS[kThreads / 64];
   __shared__ int s_any_zero;
@@ -340,14 +365,15 @@ __global__ __launch_bounds__(kThreads) void ransac_model_score_kernel(
   }
 
   // LDS: sx, sy, dx, dy [N] f64 | trial S [T] f64 | [LARGE: stack [kMaxStack][256] f64]
-  //      | trial count [T] i32
+  //      | per-wave leaf values [4][128] f64 | trial count [T] i32
   double* sx = smem;
   double* sy = sx + N;
   double* dxs = sy + N;
   double* dys = dxs + N;
   double* tS = dys + N;
   double* stk = tS + T;
-  int* tC = reinterpret_cast<int*>(stk + (LARGE ? kMaxStack * kThreads : 0));
+  double* wvals = stk + (LARGE ? kMaxStack * kThreads : 0);
+  int* tC = reinterpret_cast<int*>(wvals + kThreads / 64 * 128);
   if (LARGE && tid == 0) {
     s_plan.n = 0;
     plan_gen<kPwDepth>(s_plan, 0, N);
@@ -359,40 +385,109 @@ __global__ __launch_bounds__(kThreads) void ransac_model_score_kernel(
 
   const Pts P{sx, sy, dxs, dys};
   const uint64_t* H = hyp + hoff;
+
+  // ---- two-phase scoring, as the rigid kernel (ransac.hip): phase A = exact counts and
+  // fp32 S estimates for every trial; phase B = numpy's pairwise S, one wave per trial,
+  // for the trials at the best count whose S can tie the smallest; frames the estimates
+  // cannot decide score every trial exactly.
+  const bool fast = tq == tq;
+  int mcount = -1, flag = fast ? 0 : 1;
+  if (fast) {
+    for (int t = tid; t < T; t += kThreads) {
+      const HModel m = fit_trial<MODEL>(P, H[t]);
+      int cnt = -1;
+      float S32 = NAN;
+      if (m.ok) {
+        cnt = 0;
+        S32 = score_fast<MODEL>(m.h, P, N, tq, cnt);
+        if (!s32_certain(S32)) flag = 1;
+      }
+      tC[t] = cnt;
+      tS[t] = (double)S32;
+      mcount = max(mcount, cnt);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mcount = max(mcount, __shfl_xor(mcount, o));
+    flag |= __shfl_xor(flag, o);
+  }
+  if (lane == 0) s_cnt[wave] = (mcount + 1) | (flag << 30);  // counts <= kMaxN
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) {
+    const int v = s_cnt[w];
+    flag |= v >> 30;
+    mcount = max(mcount, (v & 0x3fffffff) - 1);
+  }
+  const bool exact = flag != 0 || mcount <= 0;
+
   int bc = -1, bt = INT_MAX;
   double bS = INFINITY;
   bool any_zero = false;
-  for (int t = tid; t < T; t += kThreads) {
-    const HModel m = fit_trial<MODEL>(P, H[t]);
-    int cnt = 0;
-    double S = NAN;
-    if (m.ok) {
-      if (!LARGE) {
-        S = pw_leaf<MODEL>(m.h, P, 0, N, thresh, cnt);
-      } else {
-        int sp = 0;
-        for (int l = 0; l < s_plan.n; ++l) {
-          stk[sp++ * kThreads + tid] = pw_leaf<MODEL>(m.h, P, s_plan.start[l], s_plan.len[l], thresh, cnt);
-          for (int c = s_plan.pops[l]; c > 0; --c) {
-            const double b = stk[--sp * kThreads + tid];
-            const double a = stk[(sp - 1) * kThreads + tid];
-            stk[(sp - 1) * kThreads + tid] = a + b;
+  if (exact) {
+    for (int t = tid; t < T; t += kThreads) {
+      const HModel m = fit_trial<MODEL>(P, H[t]);
+      int cnt = 0;
+      double S = NAN;
+      if (m.ok) {
+        if (!LARGE) {
+          S = pw_leaf<MODEL>(m.h, P, 0, N, thresh, cnt);
+        } else {
+          int sp = 0;
+          for (int l = 0; l < s_plan.n; ++l) {
+            stk[sp++ * kThreads + tid] = pw_leaf<MODEL>(m.h, P, s_plan.start[l], s_plan.len[l], thresh, cnt);
+            for (int c = s_plan.pops[l]; c > 0; --c) {
+              const double b = stk[--sp * kThreads + tid];
+              const double a = stk[(sp - 1) * kThreads + tid];
+              stk[(sp - 1) * kThreads + tid] = a + b;
+            }
           }
+          S = stk[tid];
         }
-        S = stk[tid];
+      }
+      tS[t] = S;
+      tC[t] = cnt;
+      // skipped trials (estimate() False) and NaN scores never win; with 0 inliers a
+      // trial wins only with S < inf (skimage's strict comparisons against (0, inf))
+      const bool valid = m.ok && !isnan(S) && (cnt > 0 || S < INFINITY);
+      if (valid) {
+        if (S <= 0.0) any_zero = true;
+        if (better(cnt, S, t, bc, bS, bt)) {
+          bc = cnt;
+          bS = S;
+          bt = t;
+        }
       }
     }
-    tS[t] = S;
-    tC[t] = cnt;
-    // skipped trials (estimate() False) and NaN scores never win; with 0 inliers a
-    // trial wins only with S < inf (skimage's strict comparisons against (0, inf))
-    const bool valid = m.ok && !isnan(S) && (cnt > 0 || S < INFINITY);
-    if (valid) {
-      if (S <= 0.0) any_zero = true;
-      if (better(cnt, S, t, bc, bS, bt)) {
-        bc = cnt;
-        bS = S;
-        bt = t;
+  } else {
+    const double eps = s32_eps(N);
+    double lm = INFINITY;
+    for (int t = tid; t < T; t += kThreads)
+      if (tC[t] == mcount) lm = fmin(lm, tS[t] * (1.0 + eps));
+    for (int o = 32; o > 0; o >>= 1) lm = fmin(lm, __shfl_xor(lm, o));
+    if (lane == 0) s_min[wave] = lm;
+    __syncthreads();
+    const double minhi = fmin(fmin(s_min[0], s_min[1]), fmin(s_min[2], s_min[3]));
+    double* vals = wvals + wave * 128;
+    double* wstk = stk + wave * kMaxStack;  // LARGE: the wave's combine stack
+    for (int t0 = wave * 64; t0 < T; t0 += kThreads) {
+      const int t = t0 + lane;
+      uint64_t cand = __ballot(t < T && tC[t] == mcount && tS[t] * (1.0 - eps) <= minhi);
+      while (cand) {
+        const int tc = t0 + __builtin_ctzll(cand);
+        cand &= cand - 1;
+        const HModel m = fit_trial<MODEL>(P, H[tc]);  // ok: it has a count
+        const double S = wave_pairwise<LARGE>(
+            [&](int k) {
+              int c = 0;
+              return resid2<MODEL>(m.h, P, k, thresh, c);
+            },
+            N, s_plan, vals, wstk, lane);
+        if (!isnan(S) && better(mcount, S, tc, bc, bS, bt)) {  // wave-uniform
+          bc = mcount;
+          bS = S;
+          bt = tc;
+        }
       }
     }
   }
@@ -724,11 +819,14 @@ extern "C" int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src, co
                                  " (call kcmc_ransac_prepare_samples)");
   const int need = max_n < ms + 1 ? ms + 1 : max_n;
   const int n_small = need < 128 ? need : 128;
-  const size_t lds_small = (size_t)n_small * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) + 16;
-  const size_t lds_large = (size_t)need * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) +
+  const size_t wvals = (size_t)kThreads / 64 * 128 * sizeof(double);
+  const size_t lds_small =
+      (size_t)n_small * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) + wvals + 16;
+  const size_t lds_large = (size_t)need * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) + wvals +
                            (size_t)kMaxStack * kThreads * sizeof(double) + 16;
   if ((max_n > 128 ? lds_large : lds_small) > 150 * 1024)
     return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_model: max_n/trials exceed the LDS budget");
+  const double tq = inlier_bound(thresh);
   hipStream_t s = (hipStream_t)stream;
   // The scoring kernel's best hypothesis model goes straight into out_params: the refit
   // reads a frame's entries before it overwrites them (one wave per frame), and frames
@@ -739,21 +837,21 @@ extern "C" int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src, co
   if (model == KCMC_MODEL_AFFINE) {
     hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, false>), dim3(n_frames), dim3(kThreads),
                        lds_small, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
-                       trials, thresh, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
+                       trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
     if (max_n > 128)
       hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, true>), dim3(n_frames), dim3(kThreads),
                          lds_large, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
-                         trials, thresh, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
+                         trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
     hipLaunchKernelGGL((ransac_model_refit_kernel<KCMC_MODEL_AFFINE>), refit_grid, dim3(256), 0, s, src, dst, pt_idx,
                        pt_off, src_frame_stride, out_inliers, out_n_inliers, best_model, n_frames, rate, out_params);
   } else {
     hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_PROJECTIVE, false>), dim3(n_frames), dim3(kThreads),
                        lds_small, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
-                       trials, thresh, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
+                       trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
     if (max_n > 128)
       hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_PROJECTIVE, true>), dim3(n_frames), dim3(kThreads),
                          lds_large, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
-                         trials, thresh, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
+                         trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
     hipLaunchKernelGGL((ransac_model_refit_kernel<KCMC_MODEL_PROJECTIVE>), refit_grid, dim3(256), 0, s, src, dst,
                        pt_idx, pt_off, src_frame_stride, out_inliers, out_n_inliers, best_model, n_frames, rate,
                        out_params);

@@ -85,6 +85,45 @@ def test_ransac_model_bit_exact_selection_vs_oracle(dev, model):
 
 
 @pytest.mark.parametrize("model", MODELS)
+@pytest.mark.parametrize("thresh", [2.0, 1e-120, 5e-5])
+def test_ransac_model_two_phase_ties_and_exact_fallback(dev, model, thresh):
+    """The two-phase scoring (counts through q < tq and fp32 S estimates, then numpy's
+    pairwise S for the trials that can tie) against the oracle: nearly noise-free inlier
+    sets (S near-ties), duplicated points (exact ties), N > 128, and the frames that fall
+    back to exact scoring (threshold 1e-120: tq out of range; 5e-5: no inliers on noisy
+    frames; exact integer data: S == 0)."""
+    rng = np.random.default_rng(81 if model == "affine" else 82)
+    tpls, qs = [], []
+    for N, noise in [(40, 1e-9), (90, 1e-6), (90, 0.3), (150, 1e-7), (12, 0.0)]:
+        tpl = rng.uniform(0, 1000, (N, 2))
+        Hm = np.eye(3)
+        Hm[:2, :2] += rng.normal(0, 0.01, (2, 2))
+        Hm[:2, 2] = rng.normal(0, 5, 2)
+        if model == "projective":
+            Hm[2, :2] = rng.normal(0, 1e-5, 2)
+        if noise:
+            q = oracle._apply_h(np.linalg.inv(Hm), tpl) + rng.normal(0, noise, (N, 2))
+        else:
+            tpl = np.round(tpl)
+            q = tpl - np.array([3.0, 1.0])
+        if N == 90 and noise == 0.3:
+            q[45:], tpl[45:] = q[:45], tpl[:45]
+        tpls.append(tpl)
+        qs.append(q)
+    off = _csr(qs)
+    r = stages.ransac_model(_t(np.concatenate(qs), dev), _t(np.concatenate(tpls), dev), _t(off, dev), off,
+                            model=model, residual_threshold=thresh, n_skip=3)
+    params, inl = r.params.cpu().numpy(), r.inliers.cpu().numpy().astype(bool)
+    nin, best = r.n_inliers.cpu().numpy(), r.best_trial.cpu().numpy()
+    for f in range(len(qs)):
+        p, i_ref, bt, ni = oracle.ransac_model(qs[f], tpls[f], model, thresh=thresh)
+        assert best[f] == bt, f
+        assert nin[f] == ni, f
+        assert np.array_equal(inl[off[f]:off[f + 1]], i_ref), f
+        np.testing.assert_allclose(params[f], p, rtol=1e-8, atol=1e-9, equal_nan=True, err_msg=str(f))
+
+
+@pytest.mark.parametrize("model", MODELS)
 def test_ransac_model_skips_degenerate_and_scales(dev, model):
     rng = np.random.default_rng(73)
     tpl = rng.uniform(0, 100, (12, 2))
