@@ -474,25 +474,34 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
 }
 
 // Exact brute force for the rows phase 1 could not certify: frame f's listed template
-// rows (fb[f * n_tpl + k], k < fb_cnt[f]) in batches of up to kFbBatch, batch y of a
-// frame on workgroup (f, y mod kFbSplit).  Every frame row is read once per batch and
-// scored against the batch's rows (in LDS) -- each distance one lane's sequential fp64
-// sum, the build's definition -- then a wave-wide and a workgroup-wide lexicographic
-// top-2 merge per listed row.
+// rows (fb[f * n_tpl + k], k < fb_cnt[f]) in batches of up to kFbBatch.  Workgroup
+// (f, y, z) scans slice y of the frame's rows for batches z, z + kFbLanes, ... (so a
+// frame with a few listed rows still spreads over kFbSplit workgroups, and one with many
+// over kFbSplit x kFbLanes); each distance is one lane's sequential
+// fp64 sum (the build's definition), then a wave-wide and a workgroup-wide lexicographic
+// top-2 merge per listed row, and the slices' top-2 meet in two 64-bit keys per listed
+// row, (dist bits << 32 | index) -- u64 order is the (dist, index) order -- through
+// atomicMin: the key that loses at the first slot (max(old, new)) goes to the second,
+// so the second slot ends as the smallest key that ever lost = the second smallest.
+// knn2_l2f32_fallback_out_kernel writes the results.
 constexpr int kFbThreads = 256;
 constexpr int kFbBatch = 4;
-constexpr int kFbSplit = 8;
+constexpr int kFbSplit = 16;  // frame-row slices per frame
+constexpr int kFbLanes = 4;   // batch lanes: workgroup (f, y, z) takes batches z, z + kFbLanes, ...
 
 template <int NB>
-__device__ __forceinline__ void fb_scan(const float (*sa)[kDP], const float* __restrict__ frame, int n_q, int D,
-                                        bool v4, int tid, float (&d0)[kFbBatch], int (&j0)[kFbBatch],
+__device__ __forceinline__ void fb_scan(const float (*sa)[kDP], const float* __restrict__ frame, int j_lo, int j_hi,
+                                        int D, bool v4, int tid, float (&d0)[kFbBatch], int (&j0)[kFbBatch],
                                         float (&d1)[kFbBatch], int (&j1)[kFbBatch]) {
-  for (int j = tid; j < n_q; j += kFbThreads) {
+  for (int j = j_lo + tid; j < j_hi; j += kFbThreads) {
     const float* row = frame + (size_t)j * D;
     double S[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) S[b] = 0.0;
     if (v4) {
+      // unrolled so that the loads of several pieces of the row are in flight together
+      // (one lane walks a whole row: each load is its own cache line)
+#pragma unroll 8
       for (int k = 0; k < D; k += 4) {
         const float4 y = *reinterpret_cast<const float4*>(row + k);
 #pragma unroll
@@ -523,22 +532,28 @@ __device__ __forceinline__ void fb_scan(const float (*sa)[kDP], const float* __r
   }
 }
 
+__device__ __forceinline__ unsigned long long fb_key(float d, int j) {
+  return ((unsigned long long)__float_as_uint(d) << 32) | (uint32_t)j;
+}
+
 __global__ __launch_bounds__(kFbThreads) void knn2_l2f32_fallback_kernel(const float* __restrict__ des_tpl, int n_tpl,
                                                                          int D, const float* __restrict__ des_q,
                                                                          const int32_t* __restrict__ q_off,
                                                                          const int32_t* __restrict__ fb,
                                                                          const int32_t* __restrict__ fb_cnt,
-                                                                         int32_t* __restrict__ out_idx,
-                                                                         float* __restrict__ out_dist) {
+                                                                         unsigned long long* __restrict__ fb_keys) {
   __shared__ __attribute__((aligned(16))) float sa[kFbBatch][kDP];
   __shared__ float sd[kFbThreads / 64][kFbBatch][2];
   __shared__ int sj[kFbThreads / 64][kFbBatch][2];
   const int f = blockIdx.x;
   const int cnt = fb_cnt[f];
+  if (cnt <= (int)blockIdx.z * kFbBatch) return;  // the whole workgroup: no batch for it
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q_begin = q_off[f], n_q = q_off[f + 1] - q_begin;
+  const int j_lo = (int)((long long)n_q * blockIdx.y / kFbSplit);
+  const int j_hi = (int)((long long)n_q * (blockIdx.y + 1) / kFbSplit);
   const bool v4 = (D & 3) == 0 && (reinterpret_cast<uintptr_t>(des_q) & 15) == 0;
-  for (int k0 = blockIdx.y * kFbBatch; k0 < cnt; k0 += kFbSplit * kFbBatch) {
+  for (int k0 = blockIdx.z * kFbBatch; k0 < cnt; k0 += kFbLanes * kFbBatch) {
     const int nb = min(kFbBatch, cnt - k0);
     __syncthreads();  // the previous batch's merge is done with sa / sd / sj
     for (int e = tid; e < kFbBatch * kDP; e += kFbThreads) {
@@ -555,10 +570,10 @@ __global__ __launch_bounds__(kFbThreads) void knn2_l2f32_fallback_kernel(const f
     }
     const float* frame = des_q + (size_t)q_begin * D;
     switch (nb) {  // workgroup-uniform
-      case 1: fb_scan<1>(sa, frame, n_q, D, v4, tid, d0, j0, d1, j1); break;
-      case 2: fb_scan<2>(sa, frame, n_q, D, v4, tid, d0, j0, d1, j1); break;
-      case 3: fb_scan<3>(sa, frame, n_q, D, v4, tid, d0, j0, d1, j1); break;
-      default: fb_scan<4>(sa, frame, n_q, D, v4, tid, d0, j0, d1, j1); break;
+      case 1: fb_scan<1>(sa, frame, j_lo, j_hi, D, v4, tid, d0, j0, d1, j1); break;
+      case 2: fb_scan<2>(sa, frame, j_lo, j_hi, D, v4, tid, d0, j0, d1, j1); break;
+      case 3: fb_scan<3>(sa, frame, j_lo, j_hi, D, v4, tid, d0, j0, d1, j1); break;
+      default: fb_scan<4>(sa, frame, j_lo, j_hi, D, v4, tid, d0, j0, d1, j1); break;
     }
 #pragma unroll
     for (int b = 0; b < kFbBatch; ++b) {
@@ -583,11 +598,38 @@ __global__ __launch_bounds__(kFbThreads) void knn2_l2f32_fallback_kernel(const f
       for (int v = 1; v < kFbThreads / 64; ++v)
         for (int k = 0; k < 2; ++k)
           if (sj[v][b][k] >= 0) top2_insert_exact(e0, m0, e1, m1, sd[v][b][k], sj[v][b][k]);
-      const size_t o = ((size_t)f * n_tpl + fb[(size_t)f * n_tpl + k0 + b]) * 2;
-      out_idx[o] = m0;
-      out_idx[o + 1] = m1;
-      out_dist[o] = e0;
-      out_dist[o + 1] = e1;
+      unsigned long long* key = fb_keys + 2 * ((size_t)f * n_tpl + k0 + b);
+      if (m0 >= 0) {
+        const unsigned long long k = fb_key(e0, m0);
+        const unsigned long long o = atomicMin(&key[0], k);
+        atomicMin(&key[1], o > k ? o : k);
+      }
+      if (m1 >= 0) {
+        const unsigned long long k = fb_key(e1, m1);
+        const unsigned long long o = atomicMin(&key[0], k);
+        atomicMin(&key[1], o > k ? o : k);
+      }
+    }
+  }
+}
+
+// The listed rows' merged keys -> out_idx / out_dist (no key: index -1, FLT_MAX).
+__global__ __launch_bounds__(256) void knn2_l2f32_fallback_out_kernel(int n_tpl, const int32_t* __restrict__ fb,
+                                                                      const int32_t* __restrict__ fb_cnt,
+                                                                      const unsigned long long* __restrict__ fb_keys,
+                                                                      int32_t* __restrict__ out_idx,
+                                                                      float* __restrict__ out_dist) {
+  const int f = blockIdx.x;
+  const int cnt = fb_cnt[f];
+  for (int k = threadIdx.x; k < cnt; k += 256) {
+    const size_t slot = (size_t)f * n_tpl + k;
+    const size_t o = ((size_t)f * n_tpl + fb[slot]) * 2;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const unsigned long long key = fb_keys[2 * slot + r];
+      const bool ok = key != ~0ull;
+      out_idx[o + r] = ok ? (int32_t)(uint32_t)key : -1;
+      out_dist[o + r] = ok ? __uint_as_float((uint32_t)(key >> 32)) : FLT_MAX;
     }
   }
 }
@@ -616,14 +658,16 @@ int launch_knn_f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const 
   const size_t fb_bytes = (rows * sizeof(int32_t) + 255) & ~(size_t)255;
   const size_t norm_bytes = (256 + (size_t)n_frames * tpf * sizeof(float) + 255) & ~(size_t)255;
   const size_t img_bytes = (size_t)n_frames * tpf * kImgBytes;
+  const size_t key_bytes = rows * 2 * sizeof(unsigned long long);  // the fallback's merged top-2 keys
   void* ws = nullptr;
-  KCMC_TRY(workspace_alloc(ctx, &ws, cnt_bytes + fb_bytes + norm_bytes + img_bytes, s));
+  KCMC_TRY(workspace_alloc(ctx, &ws, cnt_bytes + fb_bytes + norm_bytes + img_bytes + key_bytes, s));
   char* w = static_cast<char*>(ws);
   int32_t* fb_cnt = reinterpret_cast<int32_t*>(w);
   int32_t* fb = reinterpret_cast<int32_t*>(w + cnt_bytes);
   unsigned* Kbits = reinterpret_cast<unsigned*>(w + cnt_bytes + fb_bytes);
   float* tile_max = reinterpret_cast<float*>(w + cnt_bytes + fb_bytes + 256);
   uint8_t* img = reinterpret_cast<uint8_t*>(w + cnt_bytes + fb_bytes + norm_bytes);
+  unsigned long long* fb_keys = reinterpret_cast<unsigned long long*>(w + cnt_bytes + fb_bytes + norm_bytes + img_bytes);
   KCMC_TRY(hip_check(hipMemsetAsync(fb_cnt, 0, (size_t)n_frames * sizeof(int32_t), s), "hipMemsetAsync"));
   KCMC_TRY(hip_check(hipMemsetAsync(Kbits, 0, sizeof(unsigned), s), "hipMemsetAsync"));
   hipLaunchKernelGGL(tpl_norm_max_kernel, dim3(ceil_div(n_tpl, 8)), dim3(256), 0, s, des_tpl, n_tpl, D, Kbits);
@@ -636,9 +680,13 @@ int launch_knn_f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const 
   hipLaunchKernelGGL(knn2_l2f32_kernel, dim3(ceil_div(n_tpl, kTplPerWG), n_frames), dim3(kThreads), 0, s, des_tpl,
                      n_tpl, D, des_q, q_off, img, tpf, Kbits, tile_max, out_idx, out_dist, fb, fb_cnt);
   KCMC_TRY(launch_check("knn2_l2f32_kernel"));
-  hipLaunchKernelGGL(knn2_l2f32_fallback_kernel, dim3(n_frames, kFbSplit), dim3(kFbThreads), 0, s, des_tpl, n_tpl, D,
-                     des_q, q_off, fb, fb_cnt, out_idx, out_dist);
+  KCMC_TRY(hip_check(hipMemsetAsync(fb_keys, 0xff, key_bytes, s), "hipMemsetAsync"));
+  hipLaunchKernelGGL(knn2_l2f32_fallback_kernel, dim3(n_frames, kFbSplit, kFbLanes), dim3(kFbThreads), 0, s, des_tpl, n_tpl, D,
+                     des_q, q_off, fb, fb_cnt, fb_keys);
   KCMC_TRY(launch_check("knn2_l2f32_fallback_kernel"));
+  hipLaunchKernelGGL(knn2_l2f32_fallback_out_kernel, dim3(n_frames), dim3(256), 0, s, n_tpl, fb, fb_cnt, fb_keys,
+                     out_idx, out_dist);
+  KCMC_TRY(launch_check("knn2_l2f32_fallback_out_kernel"));
   return workspace_free(ctx, ws, s);
 }
 

@@ -120,6 +120,10 @@ def test_ransac_model_two_phase_ties_and_exact_fallback(dev, model, thresh):
         assert best[f] == bt, f
         assert nin[f] == ni, f
         assert np.array_equal(inl[off[f]:off[f + 1]], i_ref), f
+        if model == "projective" and ni < 4:
+            # skimage's refit on < 4 inliers is underdetermined (a 3-D null space of the
+            # 2N x 9 system): its params are whatever LAPACK's SVD returns, unpinned
+            continue
         np.testing.assert_allclose(params[f], p, rtol=1e-8, atol=1e-9, equal_nan=True, err_msg=str(f))
 
 
