@@ -123,10 +123,13 @@ class StageTimer:
     def __init__(self):
         self.ev = {}
 
-    def mark(self, name):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        self.ev.setdefault(name, []).append(e)
+    def mark(self, name, ev=None):
+        """ev: a timing event the pipeline already recorded at this position (shared marker
+        packet); None: record one on the current stream."""
+        if ev is None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+        self.ev.setdefault(name, []).append(ev)
 
     def elapsed(self, a, b):
         return [x.elapsed_time(y) for x, y in zip(self.ev[a], self.ev[b])]

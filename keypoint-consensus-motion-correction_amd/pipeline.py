@@ -204,12 +204,14 @@ def align_slab(inp: SlabInputs, cfg: AlignConfig, logger: Optional[logging.Logge
                       rr if keep_intermediates else None, counts)
 
 
-def _d2h_async(t: torch.Tensor, copy: torch.cuda.Stream) -> Tuple[torch.Tensor, torch.cuda.Event]:
-    """Device->host copy of ``t`` (produced on the current stream) into pinned memory on
-    the side stream ``copy``, so that the kernel stream does not stop for it; the event
-    marks its end."""
-    produced = torch.cuda.Event()
-    produced.record()
+def _d2h_async(t: torch.Tensor, copy: torch.cuda.Stream,
+               produced: Optional[torch.cuda.Event] = None) -> Tuple[torch.Tensor, torch.cuda.Event]:
+    """Device->host copy of ``t`` (produced on the current stream; ``produced``: an event
+    already recorded after it) into pinned memory on the side stream ``copy``, so that the
+    kernel stream does not stop for it; the event marks its end."""
+    if produced is None:
+        produced = torch.cuda.Event()
+        produced.record()
     h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
     with torch.cuda.stream(copy):
         copy.wait_event(produced)
@@ -321,6 +323,22 @@ class OverlappedSlabs:
         self.ana = torch.cuda.Stream(self.dev) if self.corun else None
         self._matched: Optional[_SlabInFlight] = None  # match queued, consensus pending
         self._fitted: Optional[_SlabInFlight] = None   # RANSAC queued, warp pending
+        self._tail: Optional[torch.cuda.Event] = None   # an event at the kernel stream's tail
+
+    def _at_tail(self, mark, *names) -> torch.cuda.Event:
+        """One (timing) event at the kernel stream's current tail, shared by every wait,
+        transfer and mark at this position: each event record is a marker packet, and the
+        device spends ~10 us on every marker that sits between two kernels."""
+        if self._tail is None:
+            self._tail = torch.cuda.Event(enable_timing=True)
+            self._tail.record(self.stream)
+        for n in names:
+            mark(n, self._tail)
+        return self._tail
+
+    def _queued(self) -> None:
+        """Work was queued on the kernel stream: the tail event moves."""
+        self._tail = None
 
     def _sharded(self) -> bool:
         return self.counts is not None and len(self.counts) > 1
@@ -336,8 +354,11 @@ class OverlappedSlabs:
         return dist.get_rank(self.group)
 
     def submit(self, inp: SlabInputs, out: Optional[torch.Tensor] = None,
-               mark: Optional[Callable[[str], None]] = None) -> Optional[SlabResult]:
-        mark = mark or (lambda name: None)
+               mark: Optional[Callable[[str, Optional[torch.cuda.Event]], None]] = None) -> Optional[SlabResult]:
+        """``mark(name, event)``: stage marks m0/m1 (match), w0/w1 (warp) with an event the
+        pipeline recorded on the kernel stream at that position, r0/r1 (RANSAC) with None
+        (record one on the current stream if needed)."""
+        mark = mark or (lambda name, ev=None: None)
         self._wait_current()
         with torch.cuda.stream(self.stream):
             for t in (inp.frames, out):
@@ -366,24 +387,26 @@ class OverlappedSlabs:
         ev.record(cur)
         if not ev.query():
             self.stream.wait_event(ev)
+            self._queued()
 
     def _match(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
-        mark("m0")
+        self._at_tail(mark, "m0")
         match = match_stage(inp, self.cfg)
-        mark("m1")
+        self._queued()
+        matched = self._at_tail(mark, "m1")
         if self._sharded():
             from .distributed import _all_gather_rows
 
             rank = self._rank()
             f0 = sum(self.counts[:rank])
-            keep_h, keep_ready = _d2h_async(_all_gather_rows(match.keep_bits, self.counts, self.group), self.copy)
+            keep = _all_gather_rows(match.keep_bits, self.counts, self.group)
+            self._queued()  # the kernel stream waits for the collective
+            keep_h, keep_ready = _d2h_async(keep, self.copy, self._at_tail(mark))
         else:
             f0 = 0
-            keep_h, keep_ready = _d2h_async(match.keep_bits, self.copy)
+            keep_h, keep_ready = _d2h_async(match.keep_bits, self.copy, matched)
         p = _SlabInFlight(inp, out, f0, match, keep_h, keep_ready)
-        if self.corun:
-            p.matched = torch.cuda.Event()
-            p.matched.record()
+        p.matched = matched
         return p
 
     def _fit(self, p: _SlabInFlight, mark) -> _SlabInFlight:
@@ -415,16 +438,22 @@ class OverlappedSlabs:
         """RANSAC of a slab whose consensus is known, on the current stream."""
         pt_idx = p.cons.pt_idx if p.cons.pt_idx.size else np.zeros(1, np.int32)
         lists = tuple(_h2d_async((p.cons.pt_off, pt_idx), self.dev, self.copy))
-        mark("r0")
+        mark("r0", None)
         p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, lists_dev=lists)
-        mark("r1")
+        mark("r1", None)
+        if not self.corun:
+            self._queued()
+        # RANSAC's own stream: the kernel stream's tail (one shared event) unless corun
+        here = (lambda: None) if self.corun else (lambda: self._at_tail(mark))
         if self._sharded():
             from .distributed import _all_gather_rows
 
-            p.params_host, p.params_ready = _d2h_async(_all_gather_rows(p.rr.params, self.counts, self.group),
-                                                       self.copy)
+            params = _all_gather_rows(p.rr.params, self.counts, self.group)
+            if not self.corun:
+                self._queued()
+            p.params_host, p.params_ready = _d2h_async(params, self.copy, here())
         else:
-            p.params_host, p.params_ready = _d2h_async(p.rr.params, self.copy)
+            p.params_host, p.params_ready = _d2h_async(p.rr.params, self.copy, here())
 
     def _warp_device_maps(self, p: _SlabInFlight, mark) -> None:
         if p.fitted_ev is not None:
@@ -433,9 +462,10 @@ class OverlappedSlabs:
             # of queueing a cross-stream wait, which leaves the device idle for tens of
             # microseconds even when RANSAC finished long before
             p.fitted_ev.synchronize()
-        mark("w0")
+        self._at_tail(mark, "w0")
         p.aligned = warp_frames(p.inp.frames, p.rr.params, out=p.out)
-        mark("w1")
+        self._queued()
+        self._at_tail(mark, "w1")
 
     def _finish(self, p: _SlabInFlight, mark) -> SlabResult:
         """Host post-processing of slab p (VA:143-145) and the warps that need its maps."""
@@ -453,21 +483,23 @@ class OverlappedSlabs:
             for a, b in _runs(redo):
                 (m,) = _h2d_async((local[a:b],), self.dev, self.copy)
                 warp_frames(p.inp.frames[a:b], m, out=p.aligned[a:b])
+                self._queued()
             aligned = p.aligned
         else:
             (m,) = _h2d_async((local,), self.dev, self.copy)
-            mark("w0")
+            self._queued()
+            self._at_tail(mark, "w0")
             aligned = warp_frames(p.inp.frames, m, out=p.out)
-            mark("w1")
-        done = torch.cuda.Event()
-        done.record(self.stream)
+            self._queued()
+            self._at_tail(mark, "w1")
+        done = self._at_tail(mark)
         res = SlabResult(aligned, affines, eu, skipped, interpolated, match=p.match, consensus=p.cons, ransac=p.rr)
         res.extras["done"] = done
         return res
 
-    def flush(self, mark: Optional[Callable[[str], None]] = None) -> List[SlabResult]:
+    def flush(self, mark: Optional[Callable[[str, Optional[torch.cuda.Event]], None]] = None) -> List[SlabResult]:
         """Finish every slab still in flight; their results, oldest first."""
-        mark = mark or (lambda name: None)
+        mark = mark or (lambda name, ev=None: None)
         out: List[SlabResult] = []
         with torch.cuda.stream(self.stream):
             while self._fitted is not None or self._matched is not None:

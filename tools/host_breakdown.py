@@ -43,7 +43,7 @@ def main():
             t_start = time.perf_counter()
         t = {}
         t0 = time.perf_counter()
-        ov.submit(inp, out=out, mark=lambda n: t.__setitem__(n, time.perf_counter()))
+        ov.submit(inp, out=out, mark=lambda n, ev=None: t.__setitem__(n, time.perf_counter()))
         t["end"] = time.perf_counter()
         if s >= 2:
             keys = ["m0", "m1", "w0", "w1", "r0", "r1", "end"]
