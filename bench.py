@@ -355,6 +355,8 @@ def main():
                     help="slabs in flight in the pipelined schedule (pipeline.OverlappedSlabs depth)")
     ap.add_argument("--no-corun", action="store_true",
                     help="RANSAC behind the warp on the one kernel stream (OverlappedSlabs corun=False)")
+    ap.add_argument("--ransac-grid", type=int, default=None,
+                    help="workgroups of the RANSAC launches beside the warp (default 0: one per frame)")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
@@ -389,7 +391,8 @@ def main():
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s; {args.frames} frames {bc.H}x{bc.W}x{bc.C} on {dev}")
 
     ov = None if args.serial else pipeline.OverlappedSlabs(dev, cfg, counts=counts if world > 1 else None,
-                                                            depth=args.pipeline_depth, corun=not args.no_corun)
+                                                            depth=args.pipeline_depth, corun=not args.no_corun,
+                                                            ransac_grid=args.ransac_grid)
 
     def step(timer):
         if ov is None:

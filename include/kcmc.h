@@ -168,7 +168,14 @@ int kcmc_hypothesis_table(int n, int trials, uint32_t seed, int min_samples, int
  * point count that frame batch will run RANSAC on. */
 int kcmc_ransac_prepare(kcmc_ctx* ctx, const int32_t* n_values_host, int count, int trials, uint32_t seed);
 
-/* Batched rigid RANSAC, one frame per workgroup.
+/* RANSAC scoring launches (kcmc_ransac_rigid, kcmc_ransac_model) of this context use at
+ * most max_workgroups workgroups, each scoring frames g, g + max_workgroups, ... in turn
+ * (0, the default: one workgroup per frame).  Results do not depend on it; a narrow grid
+ * keeps RANSAC on a few CU slots when it runs beside another kernel (the warp).  Not
+ * stream-ordered: it applies to the calls made after it. */
+int kcmc_set_ransac_grid(kcmc_ctx* ctx, int max_workgroups);
+
+/* Batched rigid RANSAC, one frame per workgroup (see kcmc_set_ransac_grid).
  * Point k of frame f (k < N_f = pt_off[f+1]-pt_off[f]):
  *   pt_idx_dev == NULL: src = src_dev[pt_off[f]+k], dst = dst_dev[pt_off[f]+k]
  *   pt_idx_dev != NULL: q = pt_idx[pt_off[f]+k]; src = src_dev[f*src_frame_stride + q],

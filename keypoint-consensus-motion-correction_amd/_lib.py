@@ -36,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "kcmc_consensus_slice",
     "kcmc_hypothesis_table",
     "kcmc_ransac_prepare",
+    "kcmc_set_ransac_grid",
     "kcmc_ransac_rigid",
     "kcmc_ransac_prepare_samples",
     "kcmc_ransac_model",
@@ -88,6 +89,7 @@ _SIGNATURES = {
     "kcmc_consensus_slice": ([P, I, I, I, I, I, I, P, P, P, P, P], I),
     "kcmc_hypothesis_table": ([I, I, U32, I, P], I),
     "kcmc_ransac_prepare": ([P, P, I, I, U32], I),
+    "kcmc_set_ransac_grid": ([P, I], I),
     "kcmc_ransac_rigid": ([P, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, P], I),
     "kcmc_ransac_prepare_samples": ([P, I, P, I, I, U32], I),
     "kcmc_ransac_model": ([P, I, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, P], I),

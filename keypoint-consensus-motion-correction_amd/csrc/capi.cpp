@@ -164,6 +164,13 @@ static void free_tables(kcmc_ctx* ctx) {
   ctx->hyp_off_len = 0;
 }
 
+extern "C" int kcmc_set_ransac_grid(kcmc_ctx* ctx, int max_workgroups) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_set_ransac_grid: ctx is NULL");
+  if (max_workgroups < 0) return fail(KCMC_EINVAL, "kcmc_set_ransac_grid: max_workgroups < 0");
+  ctx->ransac_grid = max_workgroups;
+  return KCMC_OK;
+}
+
 extern "C" int kcmc_ransac_prepare(kcmc_ctx* ctx, const int32_t* n_values, int count, int trials, uint32_t seed) {
   if (!ctx) return fail(KCMC_EINVAL, "kcmc_ransac_prepare: ctx is NULL");
   if (count < 0 || (count > 0 && !n_values) || trials < 1)

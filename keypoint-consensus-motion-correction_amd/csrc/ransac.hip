@@ -122,8 +122,8 @@ __device__ __forceinline__ float score_fast(const Model& m, const Pts& P, int N,
 // LARGE = false handles frames with N <= 128 (one pairwise leaf, fully in registers)
 // and the NaN frames; LARGE = true handles 128 < N <= kMaxN through the split plan.
 template <bool LARGE>
-__global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
-    const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
+__device__ __forceinline__ void ransac_rigid_frame(
+    int f, const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint32_t* __restrict__ hyp,
     const int32_t* __restrict__ hyp_off, int hyp_off_len,
     int T, double thresh, double tq, double rate, int n_skip, double* __restrict__ out_params,
@@ -138,7 +138,6 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
   __shared__ int s_final_t;
   __shared__ Plan s_plan;
 
-  const int f = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int p0 = pt_off[f];
@@ -423,6 +422,23 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
   (void)nin_local;
 }
 
+// Workgroup g scores frames g, g + grid, ...: one workgroup per frame by default; a
+// narrower grid (kcmc_set_ransac_grid) keeps RANSAC on a few CU slots when it runs beside
+// the warp (OverlappedSlabs corun).
+template <bool LARGE>
+__global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
+    int n_frames, const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
+    const int32_t* __restrict__ pt_off, int src_stride, const uint32_t* __restrict__ hyp,
+    const int32_t* __restrict__ hyp_off, int hyp_off_len,
+    int T, double thresh, double tq, double rate, int n_skip, double* __restrict__ out_params,
+    uint8_t* __restrict__ out_inl, int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
+  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
+    ransac_rigid_frame<LARGE>(f, src, dst, pt_idx, pt_off, src_stride, hyp, hyp_off, hyp_off_len, T, thresh, tq, rate,
+                              n_skip, out_params, out_inl, out_nin, out_best);
+    __syncthreads();  // the frame's LDS is free for the next one
+  }
+}
+
 }  // namespace
 }  // namespace kcmc
 
@@ -453,12 +469,13 @@ extern "C" int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src, const double*
   if ((max_n > 128 ? lds_large : lds_small) > 150 * 1024)
     return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_rigid: max_n/trials exceed the LDS budget");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(ransac_rigid_kernel<false>, dim3(n_frames), dim3(kThreads), lds_small, s, src, dst, pt_idx,
+  const unsigned grid = (unsigned)(ctx->ransac_grid > 0 && ctx->ransac_grid < n_frames ? ctx->ransac_grid : n_frames);
+  hipLaunchKernelGGL(ransac_rigid_kernel<false>, dim3(grid), dim3(kThreads), lds_small, s, n_frames, src, dst, pt_idx,
                      pt_off, src_frame_stride, ctx->hyp, ctx->hyp_off, ctx->hyp_off_len, trials, thresh, tq, rate, n_skip,
                      out_params, out_inliers, out_n_inliers, out_best_trial);
   KCMC_TRY(launch_check("ransac_rigid_kernel<small>"));
   if (max_n > 128) {
-    hipLaunchKernelGGL(ransac_rigid_kernel<true>, dim3(n_frames), dim3(kThreads), lds_large, s, src, dst, pt_idx,
+    hipLaunchKernelGGL(ransac_rigid_kernel<true>, dim3(grid), dim3(kThreads), lds_large, s, n_frames, src, dst, pt_idx,
                        pt_off, src_frame_stride, ctx->hyp, ctx->hyp_off, ctx->hyp_off_len, trials, thresh, tq, rate, n_skip,
                        out_params, out_inliers, out_n_inliers, out_best_trial);
     KCMC_TRY(launch_check("ransac_rigid_kernel<large>"));

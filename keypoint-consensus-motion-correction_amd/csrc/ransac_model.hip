@@ -327,8 +327,8 @@ __device__ __forceinline__ void gather_point(const double* __restrict__ src, con
 // LARGE = false: frames with N <= 128 (one pairwise leaf) and the NaN frames;
 // LARGE = true: 128 < N <= kMaxN through the split plan.
 template <int MODEL, bool LARGE>
-__global__ __launch_bounds__(kThreads) void ransac_model_score_kernel(
-    const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
+__device__ __forceinline__ void ransac_model_score_frame(
+    int f, const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint64_t* __restrict__ hyp,
     const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, double tq, int n_skip,
     double* out_params, double* best_model, uint8_t* __restrict__ out_inl,
@@ -344,7 +344,6 @@ __global__ __launch_bounds__(kThreads) void ransac_model_score_kernel(
   __shared__ int s_final_c;
   __shared__ Plan s_plan;
 
-  const int f = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int p0 = pt_off[f];
@@ -628,6 +627,21 @@ __device__ __forceinline__ void smallest_eigvec(const double (&A)[n][n], double 
   }
 }
 
+// Workgroup g scores frames g, g + grid, ... (kcmc_set_ransac_grid; default one per frame).
+template <int MODEL, bool LARGE>
+__global__ __launch_bounds__(kThreads) void ransac_model_score_kernel(
+    int n_frames, const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
+    const int32_t* __restrict__ pt_off, int src_stride, const uint64_t* __restrict__ hyp,
+    const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, double tq, int n_skip,
+    double* out_params, double* best_model, uint8_t* __restrict__ out_inl,
+    int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
+  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
+    ransac_model_score_frame<MODEL, LARGE>(f, src, dst, pt_idx, pt_off, src_stride, hyp, hyp_off, hyp_off_len, T,
+                                           thresh, tq, n_skip, out_params, best_model, out_inl, out_nin, out_best);
+    __syncthreads();  // the frame's LDS is free for the next one
+  }
+}
+
 template <int MODEL>
 __global__ __launch_bounds__(256) void ransac_model_refit_kernel(
     const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
@@ -834,23 +848,24 @@ extern "C" int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src, co
   // allocation cost ~0.2 ms of host time per call.
   double* best_model = out_params;
   const dim3 refit_grid((unsigned)ceil_div(n_frames, 4));
+  const unsigned grid = (unsigned)(ctx->ransac_grid > 0 && ctx->ransac_grid < n_frames ? ctx->ransac_grid : n_frames);
   if (model == KCMC_MODEL_AFFINE) {
-    hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, false>), dim3(n_frames), dim3(kThreads),
-                       lds_small, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
+    hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, false>), dim3(grid), dim3(kThreads),
+                       lds_small, s, n_frames, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
                        trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
     if (max_n > 128)
-      hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, true>), dim3(n_frames), dim3(kThreads),
-                         lds_large, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
+      hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, true>), dim3(grid), dim3(kThreads),
+                         lds_large, s, n_frames, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
                          trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
     hipLaunchKernelGGL((ransac_model_refit_kernel<KCMC_MODEL_AFFINE>), refit_grid, dim3(256), 0, s, src, dst, pt_idx,
                        pt_off, src_frame_stride, out_inliers, out_n_inliers, best_model, n_frames, rate, out_params);
   } else {
-    hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_PROJECTIVE, false>), dim3(n_frames), dim3(kThreads),
-                       lds_small, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
+    hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_PROJECTIVE, false>), dim3(grid), dim3(kThreads),
+                       lds_small, s, n_frames, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
                        trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
     if (max_n > 128)
-      hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_PROJECTIVE, true>), dim3(n_frames), dim3(kThreads),
-                         lds_large, s, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
+      hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_PROJECTIVE, true>), dim3(grid), dim3(kThreads),
+                         lds_large, s, n_frames, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
                          trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
     hipLaunchKernelGGL((ransac_model_refit_kernel<KCMC_MODEL_PROJECTIVE>), refit_grid, dim3(256), 0, s, src, dst,
                        pt_idx, pt_off, src_frame_stride, out_inliers, out_n_inliers, best_model, n_frames, rate,

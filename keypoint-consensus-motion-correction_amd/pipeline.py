@@ -300,7 +300,8 @@ class OverlappedSlabs:
     """
 
     def __init__(self, device, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
-                 counts: Optional[List[int]] = None, group=None, depth: int = 2, corun: bool = True):
+                 counts: Optional[List[int]] = None, group=None, depth: int = 2, corun: bool = True,
+                 ransac_grid: Optional[int] = None):
         if depth not in (2, 3):
             raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
         self.depth = depth
@@ -321,6 +322,11 @@ class OverlappedSlabs:
         # and c5; the match stays on the kernel stream (beside the warp it starves).
         self.corun = bool(corun)
         self.ana = torch.cuda.Stream(self.dev) if self.corun else None
+        # RANSAC beside the warp on at most this many workgroups (each walks its share of
+        # the frames; 0 / None = one per frame).  Same-box A/B at c2:
+        # 128, 256 or 512 workgroups were no faster than one per frame, so the default
+        # stays one per frame.
+        self.ransac_grid = int(ransac_grid or 0) if self.corun else 0
         self._matched: Optional[_SlabInFlight] = None  # match queued, consensus pending
         self._fitted: Optional[_SlabInFlight] = None   # RANSAC queued, warp pending
         self._tail: Optional[torch.cuda.Event] = None   # an event at the kernel stream's tail
@@ -439,7 +445,8 @@ class OverlappedSlabs:
         pt_idx = p.cons.pt_idx if p.cons.pt_idx.size else np.zeros(1, np.int32)
         lists = tuple(_h2d_async((p.cons.pt_off, pt_idx), self.dev, self.copy))
         mark("r0", None)
-        p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, lists_dev=lists)
+        with stages.ransac_grid(self.dev, self.ransac_grid):
+            p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, lists_dev=lists)
         mark("r1", None)
         if not self.corun:
             self._queued()

@@ -13,6 +13,7 @@ Reference seams replaced (reference: /root/reference/VideoAligner.py):
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from dataclasses import dataclass
 from typing import Optional, Tuple
@@ -223,6 +224,21 @@ class RansacResult:
     inliers: torch.Tensor      # [P] u8 inlier mask of the best hypothesis (CSR like the points)
     n_inliers: torch.Tensor    # [F] i32
     best_trial: torch.Tensor   # [F] i32 (-1: none)
+
+
+@contextlib.contextmanager
+def ransac_grid(device, max_workgroups: int):
+    """RANSAC scoring launches on ``device`` inside the block use at most
+    ``max_workgroups`` workgroups, each scoring frames g, g + max_workgroups, ... (C ABI
+    kcmc_set_ransac_grid; 0 = one per frame, the default).  Results are identical; a narrow
+    grid keeps RANSAC on a few CU slots when it shares the device with the warp."""
+    ctx = _ctx(torch.device(device))
+    L = _lib.load()
+    _lib.check(L.kcmc_set_ransac_grid(ctx.handle, int(max_workgroups)))
+    try:
+        yield
+    finally:
+        _lib.check(L.kcmc_set_ransac_grid(ctx.handle, 0))
 
 
 def ransac_rigid(

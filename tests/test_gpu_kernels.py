@@ -483,3 +483,29 @@ def test_warp_multichannel_vector_staging(dev, shape):
     outp = stages.warp_perspective_u16(_t(imgs, dev), _t(Hs, dev)).cpu().numpy()
     for f in range(F):
         assert np.array_equal(outp[f], oracle.warp_perspective_u16(imgs[f], Hs[f])), f
+
+
+@pytest.mark.parametrize("grid", [1, 3, 64])
+def test_ransac_narrow_grid_matches_one_workgroup_per_frame(dev, grid):
+    """kcmc_set_ransac_grid: workgroups walking several frames each give exactly the
+    one-workgroup-per-frame results, rigid and extension models, N <= 128 and N > 128."""
+    rng = np.random.default_rng(41)
+    tpls, qs = [], []
+    for N in [2, 5, 40, 90, 127, 129, 300, 0, 60]:
+        tpl = rng.uniform(0, 1000, (N, 2))
+        A = synthetic.rigid(rng.normal(0, 0.02), rng.normal(0, 5), rng.normal(0, 5))
+        q = (tpl - A[:, 2]) @ A[:, :2] + rng.normal(0, 0.7, (N, 2))
+        tpls.append(tpl)
+        qs.append(q)
+    off = _csr(qs)
+    args = (_t(np.concatenate(qs).reshape(-1, 2), dev), _t(np.concatenate(tpls).reshape(-1, 2), dev), _t(off, dev), off)
+    runs = [lambda: stages.ransac_rigid(*args), lambda: stages.ransac_model(*args, model="affine"),
+            lambda: stages.ransac_model(*args, model="projective", n_skip=5)]
+    for run in runs:
+        ref = run()
+        with stages.ransac_grid(dev, grid):
+            got = run()
+        for a, b in [(ref.params, got.params), (ref.inliers, got.inliers), (ref.n_inliers, got.n_inliers),
+                     (ref.best_trial, got.best_trial)]:
+            assert torch.equal(a.nan_to_num(7.0) if a.is_floating_point() else a,
+                               b.nan_to_num(7.0) if b.is_floating_point() else b)
