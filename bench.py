@@ -178,21 +178,22 @@ def run_step(inp, cfg, out, timer=None, world=1, counts=None):
 
 
 def isolated_stage_ms(inp, cfg, out, reps=5):
-    """Each GPU stage alone on the current stream (median of `reps`, HIP events), after
-    the timed region: the kernels' own rates, without the warp/analysis overlap of the
-    timed steps.  RANSAC runs on this slab's own consensus."""
+    """Each GPU stage alone on the current stream, after the timed region: one warm-up
+    call, then `reps` calls back to back between two HIP events (the host queues ahead of
+    the device, so no host time is inside), averaged: the kernels' own rates, without the
+    warp/analysis overlap of the timed steps.  RANSAC runs on this slab's own consensus."""
     torch.cuda.synchronize()
 
     def timed(fn):
-        ts, r = [], None
+        r = fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         for _ in range(reps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
             r = fn()
-            e1.record()
-            e1.synchronize()
-            ts.append(e0.elapsed_time(e1))
-        return float(np.median(ts)), r
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps, r
 
     match_ms, m = timed(lambda: pipeline.match_stage(inp, cfg))
     keep = m.keep_bits.cpu().numpy()
@@ -485,6 +486,14 @@ def main():
         "ransac_mean_points": round(float(n_pts.mean()), 2),
         "stage_ms": stage_ms,
         "stage_ms_isolated": iso,
+        # the warp's own roofline: the same launch alone, back to back (the timed steps run
+        # RANSAC beside it, which `roofline` includes)
+        "roofline_isolated": {"kernel": "warp_plan_kernel + " + ("warp_perspective_u16_kernel"
+                                                               if cfg.ransac_model == "projective" else
+                                                               "warp_affine_u16_kernel"),
+                              "achieved": round(warp_bytes / (iso["warp"] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(warp_bytes / (iso["warp"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "avg_launch_ms": iso["warp"]},
         "roofline": {
             "kernel": (f"warp_perspective_u16_kernel<{bc.C}>" if bc.model == "projective"
                        else f"warp_affine_u16_kernel<{bc.C}>"),
