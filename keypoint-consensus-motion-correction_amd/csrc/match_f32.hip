@@ -226,7 +226,15 @@ __global__ __launch_bounds__(256) void split_tiles_kernel(const float* __restric
     split_bf16(w.w, hv[3], lv[3]);
     *reinterpret_cast<uint2*>(tile + (rr * kRowB + col) * 2) = *reinterpret_cast<const uint2*>(hv);
     *reinterpret_cast<uint2*>(tile + kImgLo + (rr * kRowB + col) * 2) = *reinterpret_cast<const uint2*>(lv);
+    // the rows' padding columns too: every cache line of the image is written whole
+    if (col == kDP - 4) {
+      *reinterpret_cast<uint4*>(tile + (rr * kRowB + kDP) * 2) = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(tile + kImgLo + (rr * kRowB + kDP) * 2) = make_uint4(0u, 0u, 0u, 0u);
+    }
   }
+  // and the image's tail after the C values
+  for (int e = kImgC + kTile * 4 + 16 * (int)threadIdx.x; e < kImgBytes; e += 16 * 256)
+    *reinterpret_cast<uint4*>(tile + e) = make_uint4(0u, 0u, 0u, 0u);
   tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
   if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = tmax;
   __syncthreads();
