@@ -445,22 +445,23 @@ class OverlappedSlabs:
         pt_idx = p.cons.pt_idx if p.cons.pt_idx.size else np.zeros(1, np.int32)
         lists = tuple(_h2d_async((p.cons.pt_off, pt_idx), self.dev, self.copy))
         mark("r0", None)
-        with stages.ransac_grid(self.dev, self.ransac_grid):
+        if self.ransac_grid:
+            with stages.ransac_grid(self.dev, self.ransac_grid):
+                p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, lists_dev=lists)
+        else:
             p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, lists_dev=lists)
         mark("r1", None)
-        if not self.corun:
-            self._queued()
-        # RANSAC's own stream: the kernel stream's tail (one shared event) unless corun
-        here = (lambda: None) if self.corun else (lambda: self._at_tail(mark))
+        params = p.rr.params
         if self._sharded():
             from .distributed import _all_gather_rows
 
-            params = _all_gather_rows(p.rr.params, self.counts, self.group)
-            if not self.corun:
-                self._queued()
-            p.params_host, p.params_ready = _d2h_async(params, self.copy, here())
-        else:
-            p.params_host, p.params_ready = _d2h_async(p.rr.params, self.copy, here())
+            params = _all_gather_rows(params, self.counts, self.group)
+        if self.corun:
+            produced = None  # _d2h_async records it on the analysis stream
+        else:  # RANSAC (and the gather) went onto the kernel stream: share its new tail event
+            self._queued()
+            produced = self._at_tail(mark)
+        p.params_host, p.params_ready = _d2h_async(params, self.copy, produced)
 
     def _warp_device_maps(self, p: _SlabInFlight, mark) -> None:
         if p.fitted_ev is not None:
