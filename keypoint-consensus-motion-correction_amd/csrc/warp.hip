@@ -766,15 +766,21 @@ __device__ __forceinline__ void invert_perspective(const double* S, double* M) {
 }
 
 // WarpPerspectiveInvoker's fixed-point source coordinate of output pixel (x, y), where
-// xo is the first column of x's bw0-wide block and x1 = x - xo.
+// xo is the first column of x's bw0-wide block and x1 = x - xo.  IN_RANGE: the tile's
+// plan has bounded every source coordinate of the tile within +-30000 px (a staged box),
+// so OpenCV's clamp to [INT_MIN, INT_MAX] is the identity and is left out.
+template <bool IN_RANGE = false>
 __device__ __forceinline__ void persp_coord(const double* M, int xo, int x1, int y, int& X, int& Y) {
   const double X0 = M[0] * xo + M[1] * y + M[2];
   const double Y0 = M[3] * xo + M[4] * y + M[5];
   const double W0 = M[6] * xo + M[7] * y + M[8];
   double w = W0 + M[6] * x1;
   w = w != 0.0 ? 32.0 / w : 0.0;
-  const double fX = fmax((double)INT_MIN, fmin((double)INT_MAX, (X0 + M[0] * x1) * w));
-  const double fY = fmax((double)INT_MIN, fmin((double)INT_MAX, (Y0 + M[3] * x1) * w));
+  double fX = (X0 + M[0] * x1) * w, fY = (Y0 + M[3] * x1) * w;
+  if (!IN_RANGE) {
+    fX = fmax((double)INT_MIN, fmin((double)INT_MAX, fX));
+    fY = fmax((double)INT_MIN, fmin((double)INT_MAX, fY));
+  }
   X = (int)__builtin_rint(fX);
   Y = (int)__builtin_rint(fY);
 }
@@ -877,7 +883,7 @@ __device__ __forceinline__ void persp_rows(const uint16_t* stile, const Box& box
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       int X, Y;
-      persp_coord(M, xo[p], x1[p], y, X, Y);
+      persp_coord<MODE == 0>(M, xo[p], x1[p], y, X, Y);
       if (MODE == 0) {
         const int fx = X & 31, fy = Y & 31;
         const int li = ((Y >> 5) - box.sy0) * box.pitch + ((X >> 5) - box.ax0);
