@@ -45,6 +45,10 @@ __global__ void fill_kernel(uint16_t* a, size_t n, uint32_t dist) {
   }
 }
 
+__global__ void tiny_kernel(unsigned* p) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) p[1] = p[0] + 1;
+}
+
 __global__ void diff_kernel(const uint16_t* a, const uint16_t* b, size_t n, unsigned long long* cnt) {
   unsigned long long c = 0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -135,6 +139,26 @@ int main(int argc, char** argv) {
     } else {
       CK(hipMemcpy(src, tex.data(), tex.size() * 2, hipMemcpyHostToDevice));
       for (int f = 1; f < F; ++f) CK(hipMemcpy(src + (size_t)f * H * W, src, tex.size() * 2, hipMemcpyDeviceToDevice));
+    }
+    if (getenv("LAB_GAP")) {  // kernel-boundary cost after a warp / after a copy (read with a kernel trace)
+      unsigned* tp = reinterpret_cast<unsigned*>(cnt);
+      hipEvent_t et, en;
+      CK(hipEventCreate(&et));
+      CK(hipEventCreateWithFlags(&en, hipEventDisableTiming));
+      for (int k = 0; k < 4; ++k) {
+        launch_warp<1>(src, dst, M, F, H, W, 0, ws, 0);
+        hipLaunchKernelGGL(tiny_kernel, dim3(1), dim3(64), 0, 0, tp);
+        launch_warp<1>(src, dst, M, F, H, W, 0, ws, 0);
+        CK(hipEventRecord(et, 0));  // a timing event between the warp and the next kernel
+        hipLaunchKernelGGL(tiny_kernel, dim3(1), dim3(64), 0, 0, tp);
+        launch_warp<1>(src, dst, M, F, H, W, 0, ws, 0);
+        CK(hipEventRecord(en, 0));  // a non-timing event
+        hipLaunchKernelGGL(tiny_kernel, dim3(1), dim3(64), 0, 0, tp);
+        hipLaunchKernelGGL(copy_kernel, dim3(8192), dim3(256), 0, 0, (const uint4*)src, (uint4*)dst2, n / 8);
+        hipLaunchKernelGGL(tiny_kernel, dim3(1), dim3(64), 0, 0, tp);
+      }
+      CK(hipDeviceSynchronize());
+      continue;
     }
     if (getenv("LAB_LIB")) {  // the library's own configuration (BlockCfg), 3 repeats + output checksum
       for (int k = 0; k < 3; ++k)
