@@ -1,7 +1,13 @@
-mkdir -p gpurun_out/h3
-timeout -k 10 200 python -u -m pytest tests/test_gpu_pipeline.py -x -q --timeout 120 --timeout-method thread > gpurun_out/h3/tests.log 2>&1 || { tail -30 gpurun_out/h3/tests.log; exit 1; }
-tail -1 gpurun_out/h3/tests.log
-for cfg in c2 c3 c5; do for r in 1 2; do for c in 0 1 2; do
-  timeout -k 10 200 python bench.py --cpu-sample 0 --config $cfg --corun $c > gpurun_out/h3/b.json || exit 1
-  python -c "import json;d=json.load(open('gpurun_out/h3/b.json'));print('$cfg corun $c', d['value'],d['ms_per_step'],d['stage_ms']['warp'])"
+#!/bin/bash
+# Same-box A/B of the two schedules of OverlappedSlabs (RANSAC beside the warp, the
+# default, vs behind it on the kernel stream) on c2 / c3 / c5, two rounds each:
+#   bash tools/corun_ab.sh [out_dir]
+# (the round-2 A/B also ran a third variant with the match beside the warp, since
+# removed: DESIGN.md section 6)
+set -u
+OUT=${1:-gpurun_out/corun_ab}
+mkdir -p "$OUT"
+for cfg in c2 c3 c5; do for r in 1 2; do for v in "" "--no-corun"; do
+  timeout -k 10 200 python bench.py --cpu-sample 0 --config $cfg $v > "$OUT/b.json" || exit 1
+  python -c "import json;d=json.load(open('$OUT/b.json'));print('$cfg ${v:-corun}', d['value'], d['ms_per_step'], d['stage_ms']['warp'])"
 done; done; done
