@@ -10,8 +10,8 @@ synthetic, see kcmc_amd/synthetic.py).
 
 Steps are issued through pipeline.OverlappedSlabs, a software pipeline (kernel stream:
 match(k) -> warp(k-1); RANSAC(k) on a second stream beside warp(k-1), --no-corun queues
-it behind the warp instead; --pipeline-depth 3 for match(k) -> warp(k-2) ->
-RANSAC(k-1)): the host consensus of step k runs while step k-1's frames are warped;
+it behind the warp instead; depth 3, the default for c3, orders match(k) -> warp(k-2)
+-> RANSAC(k-1)): the host consensus of step k runs while step k-1's frames are warped;
 every step still runs every stage, and the pipeline is drained inside the timed region.
 --serial runs the steps strictly one after another.
 
@@ -59,6 +59,9 @@ class BenchConfig:
     frames_per_gpu: int
     cpu_sample: int
     descriptor: str = "u8"
+    # slabs in flight (pipeline.OverlappedSlabs depth): 3 where the host's per-step work
+    # (consensus + launch chain, ~0.9 ms) is as long as the warp it hides under (c3)
+    pipeline_depth: int = 2
 
 
 # BASELINE.json configs.  c2 (configs[1]) is the headline line; the others are the
@@ -70,7 +73,7 @@ CONFIGS = {
                       1080, 1920, 1, 500, 32, 100, "euclidean", 2000, 240),
     "c3": BenchConfig("c3", "BASELINE config[2]: 512x512 two-photon-style u16, 20000 frames over 8 GPUs (2500 per GPU), "
                       "n_tpl=500, D=61 B (AKAZE-sized), affine RANSAC 1000 trials, n_kp_global=50",
-                      512, 512, 1, 500, 61, 50, "affine", 2500, 60),
+                      512, 512, 1, 500, 61, 50, "affine", 2500, 60, pipeline_depth=3),
     "c4": BenchConfig("c4", "BASELINE config[3]: 4K RGB u16 (2160x3840x3), 5000 frames over 8 GPUs (625 per GPU), "
                       "4096 keypoints/frame template, D=61 B, affine RANSAC 1000 trials, n_kp_global=500",
                       2160, 3840, 3, 4096, 61, 500, "affine", 625, 4),
@@ -352,8 +355,9 @@ def main():
     ap.add_argument("--detect", action="store_true",
                     help="also time align from raw uint16 frames on the device: normalisation + ORB-style "
                          "detection + the hot path (pipeline.align_frames); reported as `with_detection`")
-    ap.add_argument("--pipeline-depth", type=int, default=2, choices=(2, 3),
-                    help="slabs in flight in the pipelined schedule (pipeline.OverlappedSlabs depth)")
+    ap.add_argument("--pipeline-depth", type=int, default=None, choices=(2, 3),
+                    help="slabs in flight in the pipelined schedule (pipeline.OverlappedSlabs depth; "
+                         "default: the config's, 3 for c3 and 2 otherwise)")
     ap.add_argument("--no-corun", action="store_true",
                     help="RANSAC behind the warp on the one kernel stream (OverlappedSlabs corun=False)")
     ap.add_argument("--ransac-grid", type=int, default=None,
@@ -364,6 +368,8 @@ def main():
     bc = CONFIGS[args.config]
     if args.frames is None:
         args.frames = bc.frames_per_gpu
+    if args.pipeline_depth is None:
+        args.pipeline_depth = bc.pipeline_depth
     if args.cpu_sample is None:
         args.cpu_sample = bc.cpu_sample * max(1, args.cpu_procs) // 2
 
