@@ -385,15 +385,16 @@ class OverlappedSlabs:
     def _wait_current(self) -> None:
         """Order the kernel stream after the caller's stream (the slab's inputs), but only
         when the caller's stream still has work queued: a cross-stream wait that is already
-        satisfied still costs the device tens of microseconds."""
+        satisfied still costs the device tens of microseconds.  The stream itself is asked
+        (hipStreamQuery): recording a probe event on it every submit delayed the next match
+        by ~11 us after the warp (`tools/gap_probe.py`: 41.5 -> 30.4 us)."""
         cur = torch.cuda.current_stream(self.dev)
-        if cur == self.stream:
+        if cur == self.stream or cur.query():
             return
         ev = torch.cuda.Event()
         ev.record(cur)
-        if not ev.query():
-            self.stream.wait_event(ev)
-            self._queued()
+        self.stream.wait_event(ev)
+        self._queued()
 
     def _match(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
         self._at_tail(mark, "m0")
