@@ -8,7 +8,8 @@
 variants: base (OverlappedSlabs as shipped), nowait (no check of the caller's stream per
 submit), notiming (the kernel-stream tail events without timing), both, squery (the
 caller's stream asked with hipStreamQuery instead of an event recorded on it), onstream
-(the caller on a stream of its own instead of the null stream)."""
+(the caller on a stream of its own instead of the null stream), lazytail (no event
+between the warp and the next match)."""
 import csv
 import glob
 import os
@@ -66,6 +67,15 @@ def main():
         pipeline.OverlappedSlabs._wait_current = _wait_current
     if variant == "onstream":  # the caller runs on a stream of its own (not the null stream)
         side = torch.cuda.Stream()
+    if variant == "lazytail":  # an event at the kernel stream's tail only behind the match
+        def _at_tail(self, mark, *names):
+            if "m1" not in names:
+                return torch.cuda.Event()  # never recorded: waits and queries on it pass
+            if self._tail is None:
+                self._tail = torch.cuda.Event()
+                self._tail.record(self.stream)
+            return self._tail
+        pipeline.OverlappedSlabs._at_tail = _at_tail
     if variant in ("notiming", "both"):
         def _at_tail(self, mark, *names):
             if self._tail is None:
