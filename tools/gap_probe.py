@@ -9,7 +9,8 @@ variants: base (OverlappedSlabs as shipped), nowait (no check of the caller's st
 submit), notiming (the kernel-stream tail events without timing), both, squery (the
 caller's stream asked with hipStreamQuery instead of an event recorded on it), onstream
 (the caller on a stream of its own instead of the null stream), lazytail (no event
-between the warp and the next match)."""
+between the warp and the next match), tiny (a small elementwise kernel before each
+match: is the idle time the warp's or the knn2's?)."""
 import csv
 import glob
 import os
@@ -28,18 +29,27 @@ def report(root):
                 for r in csv.DictReader(f):
                     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
         rows.sort()
-        gaps = []
-        warp_end = None
+        gaps, first = [], []
+        warp_end = prev_end = None
         for s, e, n in rows:
             if "warp_affine_u16_kernel" in n:
                 warp_end = e
-            elif "knn2_l2u8_kernel" in n and warp_end is not None:
-                gaps.append((s - warp_end) / 1e3)
+                first.append(None)
+            elif warp_end is not None and first and first[-1] is None and "ransac" not in n and "copyBuffer" not in n:
+                first[-1] = (n.replace("void ", "").replace("(anonymous namespace)::", "")[:28], (s - warp_end) / 1e3)
+            if "knn2_l2u8_kernel" in n and warp_end is not None:
+                gaps.append(((s - warp_end) / 1e3, (s - prev_end) / 1e3))
                 warp_end = None
+            if "ransac" not in n and "copyBuffer" not in n:
+                prev_end = e
         g = np.array(gaps[2:]) if len(gaps) > 3 else np.array(gaps)
         if g.size:
-            print(f"{os.path.basename(d):10s} warp end -> knn2 start: median {np.median(g):6.1f} us, "
-                  f"min {g.min():6.1f}, max {g.max():6.1f} (n={g.size})")
+            print(f"{os.path.basename(d):10s} warp end -> knn2 start: median {np.median(g[:, 0]):6.1f} us, "
+                  f"min {g[:, 0].min():6.1f}, max {g[:, 0].max():6.1f} (n={len(g)}); "
+                  f"idle right before knn2 {np.median(g[:, 1]):6.1f} us")
+            fk = [x for x in first[2:] if x is not None]
+            if fk:
+                print(f"{'':10s} first kernel after the warp: {fk[0][0]}, median {np.median([x[1] for x in fk]):6.1f} us")
 
 
 def main():
@@ -76,6 +86,14 @@ def main():
                 self._tail.record(self.stream)
             return self._tail
         pipeline.OverlappedSlabs._at_tail = _at_tail
+    if variant == "tiny":  # a tiny elementwise kernel right before every match
+        tiny = torch.zeros(64, device="cuda")
+        match_stage = pipeline.match_stage
+
+        def _match_stage(inp, cfg):
+            tiny.add_(1)
+            return match_stage(inp, cfg)
+        pipeline.match_stage = _match_stage
     if variant in ("notiming", "both"):
         def _at_tail(self, mark, *names):
             if self._tail is None:
