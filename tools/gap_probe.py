@@ -10,7 +10,8 @@ submit), notiming (the kernel-stream tail events without timing), both, squery (
 caller's stream asked with hipStreamQuery instead of an event recorded on it), onstream
 (the caller on a stream of its own instead of the null stream), lazytail (no event
 between the warp and the next match), tiny (a small elementwise kernel before each
-match: is the idle time the warp's or the knn2's?)."""
+match: is the idle time the warp's or the knn2's?), nocorun (RANSAC behind the warp on
+the kernel stream: nothing runs beside the warp)."""
 import csv
 import glob
 import os
@@ -27,15 +28,16 @@ def report(root):
         for p in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
             with open(p) as f:
                 for r in csv.DictReader(f):
-                    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+                    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"]))
         rows.sort()
         gaps, first = [], []
         warp_end = prev_end = None
-        for s, e, n in rows:
+        warp_q = None
+        for s, e, n, q in rows:
             if "warp_affine_u16_kernel" in n:
-                warp_end = e
+                warp_end, warp_q = e, q
                 first.append(None)
-            elif warp_end is not None and first and first[-1] is None and "ransac" not in n and "copyBuffer" not in n:
+            elif warp_end is not None and first and first[-1] is None and q == warp_q:
                 first[-1] = (n.replace("void ", "").replace("(anonymous namespace)::", "")[:28], (s - warp_end) / 1e3)
             if "knn2_l2u8_kernel" in n and warp_end is not None:
                 gaps.append(((s - warp_end) / 1e3, (s - prev_end) / 1e3))
@@ -107,7 +109,7 @@ def main():
     inp, _ = bench.make_inputs(bc, bc.frames_per_gpu, 0, dev)
     out = torch.empty_like(inp.frames)
     cfg = pipeline.AlignConfig(n_kp_global=bc.n_kp_global, ransac_model=bc.model)
-    ov = pipeline.OverlappedSlabs(dev, cfg)
+    ov = pipeline.OverlappedSlabs(dev, cfg, corun=variant != "nocorun")
     torch.cuda.synchronize()
     with torch.cuda.stream(side if variant == "onstream" else torch.cuda.current_stream()):
         for _ in range(steps):
