@@ -43,6 +43,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
 I8_PEAK_TOPS = 5000.0  # dense i8 MFMA: 2x the bf16 rate per clock (MI355X_MICROARCH.md)
 TRIALS = 1000
+ISOLATED_HEAD_START_CYCLES = 2_000_000  # spin ahead of the isolated match / RANSAC reps
 
 
 @dataclass
@@ -182,15 +183,21 @@ def run_step(inp, cfg, out, timer=None, world=1, counts=None):
 
 def isolated_stage_ms(inp, cfg, out, reps=5):
     """Each GPU stage alone on the current stream, after the timed region: one warm-up
-    call, then `reps` calls back to back between two HIP events (the host queues ahead of
-    the device, so no host time is inside), averaged: the kernels' own rates, without the
-    warp/analysis overlap of the timed steps.  RANSAC runs on this slab's own consensus."""
+    call, then `reps` calls back to back between two HIP events, averaged: the kernels'
+    own rates, without the warp/analysis overlap of the timed steps.  For the short match
+    and RANSAC calls a spin kernel ahead of the first event keeps the device busy while the
+    host queues them, so no host launch time is inside (a RANSAC launch chain once read
+    0.44 instead of 0.17 ms).  The spin is short (0.85 ms at 2.4 GHz): behind an 8 ms one
+    the warp ran 3.5 instead of 3.3 ms.  The 3 ms warp needs none; the host outruns it.
+    RANSAC runs on this slab's own consensus."""
     torch.cuda.synchronize()
 
-    def timed(fn):
+    def timed(fn, head_start=True):
         r = fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if head_start:
+            torch.cuda._sleep(ISOLATED_HEAD_START_CYCLES)
         e0.record()
         for _ in range(reps):
             r = fn()
@@ -205,7 +212,7 @@ def isolated_stage_ms(inp, cfg, out, reps=5):
     ransac_ms, rr = timed(lambda: pipeline.ransac_stage(m, inp.kp_tpl, cons, cfg, lists_dev=lists))
     affines = pipeline.postprocess_affines(rr.params.cpu().numpy(), cfg)[0]
     a_dev = torch.from_numpy(np.ascontiguousarray(affines[: inp.frames.shape[0]])).to(inp.frames.device)
-    warp_ms, _ = timed(lambda: pipeline.warp_frames(inp.frames, a_dev, out=out))
+    warp_ms, _ = timed(lambda: pipeline.warp_frames(inp.frames, a_dev, out=out), head_start=False)
     return {"match": round(match_ms, 4), "ransac": round(ransac_ms, 4), "warp": round(warp_ms, 4)}, cons
 
 
