@@ -140,56 +140,37 @@ class StageTimer:
 
 
 def run_step(inp, cfg, out, timer=None, world=1, counts=None):
-    """One pass of the hot path (single GPU or this rank's share of a sharded run)."""
+    """One pass of the hot path, strictly in order (--serial; single GPU or this rank's
+    share of a sharded run through distributed.align_sharded)."""
+    if world > 1:
+        res = kdist.align_sharded(inp, cfg, counts=counts)
+        return res.consensus, None
+    mark = timer.mark if timer else (lambda name, ev=None: None)
     n_tpl = inp.des_tpl.shape[0]
-    if timer:
-        timer.mark("m0")
+    mark("m0")
     m = pipeline.match_stage(inp, cfg)
-    if timer:
-        timer.mark("m1")
-    if world > 1:
-        keep_all = kdist._all_gather_rows(m.keep_bits, counts).cpu().numpy()
-        n_all = sum(counts)
-    else:
-        keep_all = m.keep_bits.cpu().numpy()
-        n_all = keep_all.shape[0]
-    frames = None
-    if world > 1:
-        rank = torch.distributed.get_rank()
-        frames = (sum(counts[:rank]), sum(counts[:rank]) + counts[rank])
-    cons = pipeline.consensus_stage(keep_all, n_tpl, n_all, cfg, frames=frames)
-    if timer:
-        timer.mark("r0")
+    mark("m1")
+    cons = pipeline.device_consensus(m, n_tpl, inp.q_off.numel() - 1, cfg)
+    mark("r0")
     rr = pipeline.ransac_stage(m, inp.kp_tpl, cons, cfg)
-    if timer:
-        timer.mark("r1")
-    if world > 1:
-        params = kdist._all_gather_rows(rr.params, counts).cpu().numpy()
-    else:
-        params = rr.params.cpu().numpy()
-    affines, skipped, interp, eu = pipeline.postprocess_affines(params, cfg)
-    if world > 1:
-        rank = torch.distributed.get_rank()
-        f0 = sum(counts[:rank])
-        affines = affines[f0:f0 + counts[rank]]
+    mark("r1")
+    affines, skipped, interp, eu = pipeline.postprocess_affines(rr.params.cpu().numpy(), cfg)
     a_dev = torch.from_numpy(np.ascontiguousarray(affines[: inp.frames.shape[0]])).to(inp.frames.device)
-    if timer:
-        timer.mark("w0")
+    mark("w0")
     pipeline.warp_frames(inp.frames, a_dev, out=out)
-    if timer:
-        timer.mark("w1")
+    mark("w1")
     return cons, rr
 
 
-def isolated_stage_ms(inp, cfg, out, reps=5):
-    """Each GPU stage alone on the current stream, after the timed region: one warm-up
-    call, then `reps` calls back to back between two HIP events, averaged: the kernels'
-    own rates, without the warp/analysis overlap of the timed steps.  For the short match
-    and RANSAC calls a spin kernel ahead of the first event keeps the device busy while the
-    host queues them, so no host launch time is inside (a RANSAC launch chain once read
-    0.44 instead of 0.17 ms).  The spin is short (0.85 ms at 2.4 GHz): behind an 8 ms one
-    the warp ran 3.5 instead of 3.3 ms.  The 3 ms warp needs none; the host outruns it.
-    RANSAC runs on this slab's own consensus."""
+def isolated_stage_ms(inp, cfg, out, reps=7):
+    """Each GPU stage alone on the current stream, after the timed region, one warm-up
+    call first.  Match, the device consensus (vote + merge + lookup) and RANSAC: `reps`
+    calls back to back between two HIP events, averaged, behind a spin kernel that keeps
+    the device busy while the host queues them (no host launch time inside: a RANSAC launch
+    chain once read 0.44 instead of 0.17 ms; the spin is short, 0.85 ms at 2.4 GHz).  The
+    consensus includes its host merge (the device waits for it).  Warp: a HIP event pair
+    around every launch and the MEDIAN launch (per-dispatch, like rocprofv3's kernel trace;
+    the back-to-back average of round 2 read 7-10 % above the in-step launches)."""
     torch.cuda.synchronize()
 
     def timed(fn, head_start=True):
@@ -205,15 +186,27 @@ def isolated_stage_ms(inp, cfg, out, reps=5):
         e1.synchronize()
         return e0.elapsed_time(e1) / reps, r
 
+    def per_dispatch_median(fn):
+        fn()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a, b in evs:
+            a.record()
+            fn()
+            b.record()
+        torch.cuda.synchronize()
+        return float(np.median([a.elapsed_time(b) for a, b in evs]))
+
+    n_tpl = inp.des_tpl.shape[0]
+    n_frames = inp.q_off.numel() - 1
     match_ms, m = timed(lambda: pipeline.match_stage(inp, cfg))
-    keep = m.keep_bits.cpu().numpy()
-    cons = pipeline.consensus_stage(keep, inp.des_tpl.shape[0], keep.shape[0], cfg)
-    lists = pipeline.consensus_to_device(cons, inp.frames.device)  # uploaded outside the timed calls
-    ransac_ms, rr = timed(lambda: pipeline.ransac_stage(m, inp.kp_tpl, cons, cfg, lists_dev=lists))
+    cons_ms, cons = timed(lambda: pipeline.device_consensus(m, n_tpl, n_frames, cfg))
+    ransac_ms, rr = timed(lambda: pipeline.ransac_stage(m, inp.kp_tpl, cons, cfg))
     affines = pipeline.postprocess_affines(rr.params.cpu().numpy(), cfg)[0]
     a_dev = torch.from_numpy(np.ascontiguousarray(affines[: inp.frames.shape[0]])).to(inp.frames.device)
-    warp_ms, _ = timed(lambda: pipeline.warp_frames(inp.frames, a_dev, out=out), head_start=False)
-    return {"match": round(match_ms, 4), "ransac": round(ransac_ms, 4), "warp": round(warp_ms, 4)}, cons
+    warp_ms = per_dispatch_median(lambda: pipeline.warp_frames(inp.frames, a_dev, out=out))
+    return {"match": round(match_ms, 4), "consensus": round(cons_ms, 4), "ransac": round(ransac_ms, 4),
+            "warp": round(warp_ms, 4)}, cons
 
 
 def _cpu_pool(procs: int, initargs):
@@ -453,8 +446,6 @@ def main():
     match_ms = float(np.mean(timer.elapsed("m0", "m1")))
     ransac_ms = float(np.mean(timer.elapsed("r0", "r1")))
     n_pts = np.diff(cons.pt_off)
-    if len(n_pts) > args.frames:  # overlapped multi-rank steps return the global consensus
-        n_pts = n_pts[rank * args.frames:(rank + 1) * args.frames]
     n_ransac = int((n_pts >= cfg.effective_frame_skip).sum())
     iso, iso_cons = isolated_stage_ms(inp, cfg, out)
     iso_pts = np.diff(iso_cons.pt_off)
@@ -467,10 +458,10 @@ def main():
     if ov is None:
         stage_ms["host_and_transfers"] = round(ms_step - match_ms - ransac_ms - warp_ms, 3)
     else:  # step k+1's match/consensus/RANSAC/post-processing overlap step k's warp
-        stage_ms["schedule"] = ("pipelined: match(k) -> warp(k-1) -> RANSAC(k)" if args.pipeline_depth == 2 else
-                                "pipelined: match(k) -> warp(k-2) -> RANSAC(k-1)") + (
+        stage_ms["schedule"] = ("pipelined: match+vote(k) -> warp(k-1) -> lookup+RANSAC(k)" if args.pipeline_depth == 2 else
+                                "pipelined: match+vote(k) -> warp(k-2) -> lookup+RANSAC(k-1)") + (
                                     " on one stream" if args.no_corun else ", RANSAC on a second stream beside the warp"
-                                ) + ", host consensus under the warp"
+                                ) + ", host consensus merge under the warp"
         stage_ms["step_minus_warp"] = round(ms_step - warp_ms, 3)
     result = {
         "metric": METRIC,
@@ -483,7 +474,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("u16 frames; " + ("f32 MFMA match + f64 re-rank" if bc.descriptor == "f32" else "i8 MFMA match")
+        "dtype": ("u16 frames; " + ("f32 descriptors: bf16x3 MFMA candidate search + exact f64 re-rank"
+                                    if bc.descriptor == "f32" else "u8 descriptors: i8 MFMA exact integer distances")
                   + ", f64 RANSAC, f32 warp weights"),
         "data": "synthetic (seeded jittered 1080p texture + ORB-shaped keypoints; no detector in image)",
         "config": {
@@ -499,14 +491,14 @@ def main():
         "ransac_mean_points": round(float(n_pts.mean()), 2),
         "stage_ms": stage_ms,
         "stage_ms_isolated": iso,
-        # the warp's own roofline: the same launch alone, back to back (the timed steps run
-        # RANSAC beside it, which `roofline` includes)
+        # the warp's own roofline: the same launch alone, median of per-dispatch HIP event
+        # pairs (the timed steps run RANSAC beside it, which `roofline` includes)
         "roofline_isolated": {"kernel": "warp_plan_kernel + " + ("warp_perspective_u16_kernel"
                                                                if cfg.ransac_model == "projective" else
                                                                "warp_affine_u16_kernel"),
                               "achieved": round(warp_bytes / (iso["warp"] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": round(warp_bytes / (iso["warp"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                              "avg_launch_ms": iso["warp"]},
+                              "median_launch_ms": iso["warp"]},
         "roofline": {
             "kernel": (f"warp_perspective_u16_kernel<{bc.C}>" if bc.model == "projective"
                        else f"warp_affine_u16_kernel<{bc.C}>"),

@@ -13,6 +13,9 @@
  *   kcmc_knn2_l2u8         <- cv2.BFMatcher().knnMatch(..., k=2) alone (VA:194-195).
  *   kcmc_consensus         <- _get_consensus_kps + _lookup_consensus_kps (VA:224-286),
  *                             host-only, reproducing CPython set/Counter ordering.
+ *   kcmc_consensus_vote / _merge / _lookup  <- the same consensus in three parts, the
+ *                             per-frame parts on the device (frame-sharded jobs exchange
+ *                             only the O(n_tpl) votes).
  *   kcmc_ransac_rigid      <- _compute_euclidean_affine (VA:288-323), i.e. skimage 0.18.3
  *                             ransac(EuclideanTransform, 2, 2, max_trials, random_state).
  *   kcmc_warp_affine_u16   <- _apply_affine (VA:455-458): cv2.warpAffine(img, M, (W,H),
@@ -40,6 +43,7 @@
 #ifndef KCMC_H_
 #define KCMC_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -62,6 +66,10 @@ typedef void* kcmc_stream_t; /* hipStream_t */
 
 int kcmc_abi_version(void);
 const char* kcmc_last_error(void);
+
+/* hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, stream): the pinned-host <-> device
+ * transfers of a pipelined caller (e.g. kcmc_amd.pipeline) without a runtime binding of its own. */
+int kcmc_memcpy_async(void* dst, const void* src, size_t bytes, kcmc_stream_t stream);
 
 /* Create / destroy the per-device context (holds the uploaded RANSAC hypothesis
  * tables).  `device` is a HIP device ordinal. */
@@ -155,6 +163,48 @@ int kcmc_consensus_slice(const uint32_t* keep_bits_host, int n_frames, int n_tpl
                          int32_t* out_votes_host, int* out_n_consensus, int32_t* out_pt_off_host,
                          int32_t* out_pt_idx_host);
 
+/* ------------------------------------- keypoint consensus in three parts (VA:224-286)
+ * The same consensus split so that each rank of a frame-sharded job works on its own
+ * frames and exchanges O(n_tpl) numbers instead of every frame's bitmask:
+ *   vote   (per rank)   votes [2, n_tpl] i64: row 0 = Counter count of every template over
+ *                        the rank's frames (VA:239); row 1 = its first-occurrence key
+ *                        (frame_base + f) << 32 | slot, f the first frame whose set holds it
+ *                        and slot its position in that CPython set's table (iteration order),
+ *                        INT64_MAX if no frame holds it.
+ *   merge  (host)       counts summed over ranks, keys min'ed: Counter.most_common(n_kp_global)
+ *                        (VA:240) and the iteration order of set(consensus) (VA:248).
+ *   lookup (per rank)   list(consensus_set.intersection(frame_set)) per frame (VA:274) as the
+ *                        CSR RANSAC point lists.
+ * frame_base = global index of the rank's first frame (0 on one device). */
+int kcmc_consensus_vote(kcmc_ctx* ctx, const uint32_t* keep_bits_dev, int n_frames, int n_tpl,
+                        long long frame_base, int64_t* out_votes_dev, kcmc_stream_t stream);
+int kcmc_consensus_vote_host(const uint32_t* keep_bits_host, int n_frames, int n_tpl, long long frame_base,
+                             int64_t* out_votes_host);
+/* votes_host [world, 2, n_tpl] (the ranks' vote outputs, any order).  out_consensus_host /
+ * out_votes_host [n_kp_global] as kcmc_consensus; out_cons_pack_host [n_kp_global + ceil(n_tpl/32)]
+ * i32: set(consensus)'s iteration order in [0, nc), its bitmask (u32 words) in [nc, nc + words)
+ * -- the input of kcmc_consensus_lookup.  KCMC_EALIGN if fewer than n_min templates were voted. */
+int kcmc_consensus_merge(const int64_t* votes_host, int world, int n_tpl, int n_kp_global, int n_min,
+                         int32_t* out_consensus_host, int32_t* out_votes_host, int* out_n_consensus,
+                         int32_t* out_cons_pack_host);
+/* Device lookup: cons_pack_dev = kcmc_consensus_merge's pack (nc entries + bitmask words);
+ * out_pt_off_dev [n_frames + 1], out_pt_idx_dev [n_frames * nc]; scratch_dev of at least
+ * kcmc_consensus_lookup_scratch_bytes(n_frames, nc) bytes (CPython set emulation tables of the
+ * frames whose order is not ascending). */
+long long kcmc_consensus_lookup_scratch_bytes(int n_frames, int nc);
+int kcmc_consensus_lookup(kcmc_ctx* ctx, const uint32_t* keep_bits_dev, int n_frames, int n_tpl,
+                          const int32_t* cons_pack_dev, int nc, int32_t* out_pt_off_dev,
+                          int32_t* out_pt_idx_dev, void* scratch_dev, kcmc_stream_t stream);
+int kcmc_consensus_lookup_host(const uint32_t* keep_bits_host, int n_frames, int n_tpl,
+                               const int32_t* cons_iter_host, int nc, int32_t* out_pt_off_host,
+                               int32_t* out_pt_idx_host);
+
+/* The boundary of a slab's RANSAC output for NaN-gap filling across ranks (VA:347-407):
+ * params_dev [n_frames, E] f64 (E = 6 for [F,2,3], 9 for [F,3,3]); out_dev [2 + 2E] f64 =
+ * (first frame without NaN or -1, last such frame or -1, its E params, the last one's E params). */
+int kcmc_params_boundary(kcmc_ctx* ctx, const double* params_dev, int n_frames, int E, double* out_dev,
+                         kcmc_stream_t stream);
+
 /* --------------------------------------------------------------- K2: RANSAC
  * The seeded sample stream skimage 0.18.3 consumes: trial t of a frame with n points
  * uses np.random.RandomState(seed).choice(n, min_samples, replace=False) drawn t+1-th
@@ -196,6 +246,15 @@ int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src_dev, const double* dst_de
                       double spatial_rate, int n_skip, double* out_params_dev,
                       uint8_t* out_inliers_dev, int32_t* out_n_inliers_dev,
                       int32_t* out_best_trial_dev, kcmc_stream_t stream);
+/* kcmc_ransac_rigid with the scoring grid given per call (max_workgroups, 0 = one workgroup
+ * per frame) instead of the context-wide kcmc_set_ransac_grid value: safe when several
+ * callers share the context. */
+int kcmc_ransac_rigid_grid(kcmc_ctx* ctx, const double* src_dev, const double* dst_dev,
+                           const int32_t* pt_idx_dev, const int32_t* pt_off_dev, int src_frame_stride,
+                           int n_frames, int max_n, int trials, double residual_threshold,
+                           double spatial_rate, int n_skip, double* out_params_dev,
+                           uint8_t* out_inliers_dev, int32_t* out_n_inliers_dev,
+                           int32_t* out_best_trial_dev, int max_workgroups, kcmc_stream_t stream);
 
 /* ------------------------------------------------- K2 extension: affine / projective
  * The reference only fits EuclideanTransform (VA:311).  BASELINE configs 3-5 need the
@@ -226,6 +285,13 @@ int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src_dev, const dou
                       double spatial_rate, int n_skip, double* out_params_dev,
                       uint8_t* out_inliers_dev, int32_t* out_n_inliers_dev,
                       int32_t* out_best_trial_dev, kcmc_stream_t stream);
+/* kcmc_ransac_model with a per-call scoring grid (see kcmc_ransac_rigid_grid). */
+int kcmc_ransac_model_grid(kcmc_ctx* ctx, int model, const double* src_dev, const double* dst_dev,
+                           const int32_t* pt_idx_dev, const int32_t* pt_off_dev, int src_frame_stride,
+                           int n_frames, int max_n, int trials, double residual_threshold,
+                           double spatial_rate, int n_skip, double* out_params_dev,
+                           uint8_t* out_inliers_dev, int32_t* out_n_inliers_dev,
+                           int32_t* out_best_trial_dev, int max_workgroups, kcmc_stream_t stream);
 
 /* ------------------------------------------------------------------ K3: warp
  * cv2.warpAffine(frame, M_f, (W, H), flags=INTER_LINEAR [| WARP_INVERSE_MAP]) for

@@ -24,6 +24,7 @@ ABI_VERSION = 1
 EXPORTED_SYMBOLS = (
     "kcmc_abi_version",
     "kcmc_last_error",
+    "kcmc_memcpy_async",
     "kcmc_create",
     "kcmc_destroy",
     "kcmc_knn2_l2u8",
@@ -34,12 +35,21 @@ EXPORTED_SYMBOLS = (
     "kcmc_match_frames_hamming",
     "kcmc_consensus",
     "kcmc_consensus_slice",
+    "kcmc_consensus_vote",
+    "kcmc_consensus_vote_host",
+    "kcmc_consensus_merge",
+    "kcmc_consensus_lookup_scratch_bytes",
+    "kcmc_consensus_lookup",
+    "kcmc_consensus_lookup_host",
+    "kcmc_params_boundary",
     "kcmc_hypothesis_table",
     "kcmc_ransac_prepare",
     "kcmc_set_ransac_grid",
     "kcmc_ransac_rigid",
+    "kcmc_ransac_rigid_grid",
     "kcmc_ransac_prepare_samples",
     "kcmc_ransac_model",
+    "kcmc_ransac_model_grid",
     "kcmc_warp_affine_u16",
     "kcmc_warp_perspective_u16",
     "kcmc_histogram_u16",
@@ -73,10 +83,12 @@ P = ctypes.c_void_p
 I = ctypes.c_int
 D = ctypes.c_double
 U32 = ctypes.c_uint32
+LL = ctypes.c_longlong
 
 _SIGNATURES = {
     "kcmc_abi_version": ([], I),
     "kcmc_last_error": ([], ctypes.c_char_p),
+    "kcmc_memcpy_async": ([P, P, ctypes.c_size_t, P], I),
     "kcmc_create": ([I, ctypes.POINTER(P)], I),
     "kcmc_destroy": ([P], I),
     "kcmc_knn2_l2u8": ([P, P, I, I, P, P, I, I, P, P, P], I),
@@ -87,12 +99,21 @@ _SIGNATURES = {
     "kcmc_match_frames_hamming": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
     "kcmc_consensus": ([P, I, I, I, I, P, P, P, P, P], I),
     "kcmc_consensus_slice": ([P, I, I, I, I, I, I, P, P, P, P, P], I),
+    "kcmc_consensus_vote": ([P, P, I, I, LL, P, P], I),
+    "kcmc_consensus_vote_host": ([P, I, I, LL, P], I),
+    "kcmc_consensus_merge": ([P, I, I, I, I, P, P, P, P], I),
+    "kcmc_consensus_lookup_scratch_bytes": ([I, I], LL),
+    "kcmc_consensus_lookup": ([P, P, I, I, P, I, P, P, P, P], I),
+    "kcmc_consensus_lookup_host": ([P, I, I, P, I, P, P], I),
+    "kcmc_params_boundary": ([P, P, I, I, P, P], I),
     "kcmc_hypothesis_table": ([I, I, U32, I, P], I),
     "kcmc_ransac_prepare": ([P, P, I, I, U32], I),
     "kcmc_set_ransac_grid": ([P, I], I),
     "kcmc_ransac_rigid": ([P, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, P], I),
+    "kcmc_ransac_rigid_grid": ([P, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, I, P], I),
     "kcmc_ransac_prepare_samples": ([P, I, P, I, I, U32], I),
     "kcmc_ransac_model": ([P, I, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, P], I),
+    "kcmc_ransac_model_grid": ([P, I, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, I, P], I),
     "kcmc_warp_affine_u16": ([P, P, P, P, I, I, I, I, I, P], I),
     "kcmc_warp_perspective_u16": ([P, P, P, P, I, I, I, I, I, P], I),
     "kcmc_histogram_u16": ([P, P, ctypes.c_ulonglong, I, I, P, P], I),
@@ -162,6 +183,7 @@ class Context:
 
     def __init__(self, device: int):
         self.device = device
+        self.ransac_grid = 0  # the context-wide kcmc_set_ransac_grid value (stages.ransac_grid)
         self._h = P()
         check(load().kcmc_create(device, ctypes.byref(self._h)))
 

@@ -10,7 +10,7 @@ interpolation lerps arccos/arcsin of the four rotation entries independently
 """
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -126,6 +126,68 @@ def interpolate_linear(maps: np.ndarray) -> Tuple[np.ndarray, List[int]]:
     if last < n - 1:
         m[last + 1 :] = m[last]
     return m, interpolated
+
+
+def _fill_span(m: np.ndarray, xs: np.ndarray, lerp: bool) -> Tuple[np.ndarray, List[int]]:
+    """The gap filling of interpolate_affines (lerp=True, VA:347-407) / interpolate_linear
+    over rows m whose global frame indices are xs (consecutive, at least one row without
+    NaN): leading rows take the first model (reported), interior gaps are interpolated
+    between their two neighbours at their global indices (reported), trailing rows take the
+    last model (not reported, VA:400).  Returns (filled rows, reported global indices)."""
+    missing = _nan_rows(m)
+    present = np.flatnonzero(~missing)
+    reported: List[int] = []
+    first = int(present[0])
+    if first > 0:
+        m[:first] = m[first]
+        reported += xs[:first].tolist()
+    for g in np.flatnonzero(np.diff(present) > 1):
+        lo, hi = int(present[g]), int(present[g + 1])
+        x_lo, x_hi = int(xs[lo]), int(xs[hi])
+        gx = xs[lo + 1 : hi]
+        if lerp:
+            m[lo + 1 : hi] = _lerp_gap(m[lo], m[hi], x_lo, x_hi, gx)
+        else:
+            t = (gx.astype(np.float64) - x_lo) / float(x_hi - x_lo)
+            m[lo + 1 : hi] = m[lo][None] + (m[hi] - m[lo])[None] * t[:, None, None]
+        reported += gx.tolist()
+    last = int(present[-1])
+    if last < len(m) - 1:
+        m[last + 1 :] = m[last]
+    return m, reported
+
+
+def fill_gaps_slab(params: np.ndarray, f0: int, prev: Optional[Tuple[int, np.ndarray]],
+                   nxt: Optional[Tuple[int, np.ndarray]], lerp: bool) -> Tuple[np.ndarray, List[int], List[int]]:
+    """NaN-gap filling of one rank's frames [f0, f0 + n) of a frame-sharded job (frame
+    downsample rate 1), equal to the rows [f0, f0 + n) of interpolate_affines /
+    interpolate_linear over all frames: ``prev`` = (global index, model) of the last frame
+    with a model before f0 on any rank, ``nxt`` the first one after the slab (None: there
+    is none).  Only those two neighbours cross ranks, so a rank's work is O(its frames).
+    Returns (filled [n, ...], skipped global indices (VA:339), reported interpolated
+    global indices of this slab).  AlignmentError when no frame of the job has a model."""
+    m = np.array(params, dtype=np.float64, copy=True)
+    n = len(m)
+    skipped = (np.flatnonzero(_nan_rows(m)) + f0).tolist() if n else []
+    if not skipped:
+        return m, [], []
+    rows, xs, lo = [m], [np.arange(f0, f0 + n)], 0
+    if prev is not None:
+        rows.insert(0, np.asarray(prev[1], dtype=np.float64).reshape((1,) + m.shape[1:]))
+        xs.insert(0, np.array([prev[0]]))
+        lo = 1
+    if nxt is not None:
+        rows.append(np.asarray(nxt[1], dtype=np.float64).reshape((1,) + m.shape[1:]))
+        xs.append(np.array([nxt[0]]))
+    ext, gx = np.concatenate(rows), np.concatenate(xs)
+    if _nan_rows(ext).all():
+        raise AlignmentError(
+            "No transformations were calculated because too few keypoints were identified "
+            "(probably because too few keypoints were identified)"
+        )
+    ext, reported = _fill_span(ext, gx, lerp)
+    lo_x, hi_x = f0, f0 + n
+    return ext[lo : lo + n], skipped, [x for x in reported if lo_x <= x < hi_x]
 
 
 def euclidean_transforms(affines: np.ndarray) -> np.ndarray:

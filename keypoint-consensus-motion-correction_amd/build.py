@@ -17,7 +17,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 REPO = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libkcmc.so")
 OFFLOAD_ARCH = os.environ.get("KCMC_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["capi.cpp", "hostalg.cpp", "match.hip", "match_f32.hip", "match_hamming.hip", "normalize.hip", "orb.hip", "pyramid.hip", "ransac.hip", "ransac_model.hip", "warp.hip"]
+SOURCES = ["capi.cpp", "consensus.hip", "hostalg.cpp", "match.hip", "match_f32.hip", "match_hamming.hip", "normalize.hip", "orb.hip", "pyramid.hip", "ransac.hip", "ransac_model.hip", "warp.hip"]
 HEADERS = ["kcmc_internal.h", "ransac_common.h", os.path.join("..", "..", "include", "kcmc.h")]
 
 COMMON_FLAGS = [

@@ -38,6 +38,12 @@ extern "C" int kcmc_abi_version(void) { return KCMC_ABI_VERSION; }
 
 extern "C" const char* kcmc_last_error(void) { return g_last_error.c_str(); }
 
+extern "C" int kcmc_memcpy_async(void* dst, const void* src, size_t bytes, kcmc_stream_t stream) {
+  if (bytes == 0) return KCMC_OK;
+  if (!dst || !src) return fail(KCMC_EINVAL, "kcmc_memcpy_async: NULL pointer");
+  return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)stream), "hipMemcpyAsync");
+}
+
 extern "C" int kcmc_create(int device, kcmc_ctx** out) {
   if (!out) return fail(KCMC_EINVAL, "kcmc_create: out is NULL");
   int n = 0;

@@ -169,6 +169,12 @@ class PySet {
     for (int64_t k : table_)
       if (k != kEmpty) f(k);
   }
+  // f(key, slot) in iteration (= slot) order
+  template <class F>
+  void for_each_slot(F&& f) const {
+    for (size_t s = 0; s < table_.size(); ++s)
+      if (table_[s] != kEmpty) f(table_[s], s);
+  }
 
  private:
   static constexpr size_t kLinearProbes = 9;
@@ -408,27 +414,32 @@ extern "C" int kcmc_hypothesis_table(int n, int trials, uint32_t seed, int min_s
   return hypothesis_table_impl(n, trials, seed, min_samples, out_host);
 }
 
-extern "C" int kcmc_consensus_slice(const uint32_t* keep_bits, int n_frames, int n_tpl, int n_kp_global,
-                                    int n_min, int f_begin, int f_end, int32_t* out_consensus,
-                                    int32_t* out_votes, int* out_n_consensus, int32_t* out_pt_off,
-                                    int32_t* out_pt_idx) {
-  if (n_frames < 0 || n_tpl < 0 || n_kp_global < 0 || (!keep_bits && n_frames > 0) ||
-      !out_n_consensus || !out_pt_off || f_begin < 0 || f_end < f_begin || f_end > n_frames)
-    return fail(KCMC_EINVAL, "kcmc_consensus: bad arguments");
+// ------------------------------------------------------------- consensus, in three parts
+// The consensus of VA:224-286 split so that a frame-sharded job exchanges O(n_tpl) data per
+// rank instead of every frame's bitmask:
+//   vote   (per rank, over its own frames)  Counter counts + each template's first occurrence
+//   merge  (every rank, O(world * n_tpl))   Counter.most_common + set(consensus) iteration order
+//   lookup (per rank, over its own frames)  list(consensus & frame_set) per frame (VA:274)
+// The device kernels (consensus.hip) compute vote and lookup with the same definitions.
+namespace kcmc {
+
+// kp_idxs = set([m.queryIdx for m in distance_matches]) (VA:214): insertions in ascending
+// template order.
+static PySet frame_set_of(const uint32_t* w, int words) {
+  PySet s;
+  for (int k = 0; k < words; ++k)
+    for (uint32_t b = w[k]; b; b &= b - 1) s.add(32 * k + __builtin_ctz(b));
+  return s;
+}
+
+// votes [2][n_tpl]: row 0 = Counter count of every template over frames [0, n_frames); row 1
+// = its first-occurrence key (frame_base + f) << 32 | slot: f the first frame whose set holds
+// it, slot its position in that set's table (iteration order = slot order), INT64_MAX if no
+// frame holds it.  Counter([x for s in kp_idxs_list for x in s]) (VA:239) inserts keys in
+// exactly the order of these keys, so merging ranks = summing counts + taking the min key.
+int vote_impl(const uint32_t* keep_bits, int n_frames, int n_tpl, int64_t frame_base, int64_t* out) {
   const int words = (n_tpl + 31) / 32;
   auto frame_bits = [&](int f) { return keep_bits + (size_t)f * words; };
-  // kp_idxs = set([m.queryIdx for m in distance_matches]) (VA:214): insertions in
-  // ascending template order.  Only needed where its iteration order is observable.
-  auto frame_set = [&](int f) {
-    PySet s;
-    const uint32_t* w = frame_bits(f);
-    for (int k = 0; k < words; ++k)
-      for (uint32_t b = w[k]; b; b &= b - 1) s.add(32 * k + __builtin_ctz(b));
-    return s;
-  };
-  // Counter([x for s in kp_idxs_list for x in s]) (VA:239): vote counts, and the
-  // first-occurrence order (dict insertion order) -- a frame's set iteration order only
-  // matters for the elements it contributes first, so only those frames are replayed.
   // Vertical counting in byte lanes: spread[byte] holds the byte's 8 bits as 8 bytes of
   // 0/1, so one 64-bit add counts 8 template indices; flushed every 255 frames.
   static const std::array<uint64_t, 256> spread = [] {
@@ -439,8 +450,7 @@ extern "C" int kcmc_consensus_slice(const uint32_t* keep_bits, int n_frames, int
   }();
   std::vector<int32_t> count((size_t)words * 32, 0);
   std::vector<uint32_t> seen((size_t)words, 0u), any((size_t)words, 0u);
-  // frames [fb, fe) into cnt / anym; integer sums, so splitting the frames over threads
-  // (the all-gathered bitmasks of a multi-GPU job: 16 000 frames at 8 GPUs) is exact
+  // frames [fb, fe) into cnt / anym; integer sums, so splitting the frames over threads is exact
   auto vote = [&](int fb, int fe, int32_t* cnt, uint32_t* anym) {
     std::vector<uint64_t> acc((size_t)words * 4, 0);
     auto flush = [&] {
@@ -479,55 +489,99 @@ extern "C" int kcmc_consensus_slice(const uint32_t* keep_bits, int n_frames, int
       for (size_t q = 0; q < any.size(); ++q) any[q] |= any_p[(size_t)t * any.size() + q];
     }
   }
+  for (int t = 0; t < n_tpl; ++t) {
+    out[t] = count[(size_t)t];
+    out[n_tpl + t] = INT64_MAX;
+  }
+  // a frame's set iteration order only matters for the keys it holds first: only those
+  // frames are replayed
   size_t remaining = 0;
   for (int k = 0; k < words; ++k) remaining += (size_t)__builtin_popcount(any[(size_t)k]);
-  std::vector<int32_t> order;
-  order.reserve(remaining);
   for (int f = 0; f < n_frames && remaining; ++f) {
     const uint32_t* w = frame_bits(f);
     bool fresh = false;
     for (int k = 0; k < words && !fresh; ++k) fresh = (w[k] & ~seen[(size_t)k]) != 0;
     if (!fresh) continue;
-    frame_set(f).for_each([&](int64_t key) {
+    frame_set_of(w, words).for_each_slot([&](int64_t key, size_t slot) {
       uint32_t& sw = seen[(size_t)(key >> 5)];
       const uint32_t bit = 1u << (key & 31);
       if (!(sw & bit)) {
         sw |= bit;
-        order.push_back((int32_t)key);
+        out[n_tpl + key] = ((frame_base + f) << 32) | (int64_t)slot;
         --remaining;
       }
     });
   }
-  // most_common(n) == stable sort by count desc over first-occurrence order (heapq.nlargest).
-  std::stable_sort(order.begin(), order.end(),
-                   [&](int32_t a, int32_t b) { return count[(size_t)a] > count[(size_t)b]; });
+  return KCMC_OK;
+}
+
+// votes [world][2][n_tpl] -> the consensus (Counter.most_common(n_kp_global) order + counts)
+// and the iteration order of set(consensus) (VA:248).  out_cons_pack [n_kp_global + words]:
+// the set's iteration order in [0, nc), its bitmask (words u32) in [nc, nc + words).
+int merge_impl(const int64_t* votes, int world, int n_tpl, int n_kp_global, int n_min, int32_t* out_consensus,
+               int32_t* out_votes, int* out_n, int32_t* out_cons_pack) {
+  std::vector<int64_t> cnt((size_t)n_tpl, 0), key((size_t)n_tpl, INT64_MAX);
+  for (int r = 0; r < world; ++r) {
+    const int64_t* v = votes + (size_t)r * 2 * (size_t)n_tpl;
+    for (int t = 0; t < n_tpl; ++t) {
+      cnt[(size_t)t] += v[t];
+      key[(size_t)t] = std::min(key[(size_t)t], v[n_tpl + t]);
+    }
+  }
+  std::vector<int32_t> order;
+  for (int t = 0; t < n_tpl; ++t) {
+    if (cnt[(size_t)t] < 0) return fail(KCMC_EINVAL, "kcmc_consensus_merge: negative vote count");
+    if (cnt[(size_t)t] == 0) continue;
+    if (key[(size_t)t] == INT64_MAX)
+      return fail(KCMC_EINVAL, "kcmc_consensus_merge: a voted template has no first-occurrence key");
+    order.push_back(t);
+  }
+  // most_common(n) == sort by count desc over first-occurrence order (heapq.nlargest is
+  // stable); first-occurrence keys are distinct
+  std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    return cnt[(size_t)a] != cnt[(size_t)b] ? cnt[(size_t)a] > cnt[(size_t)b] : key[(size_t)a] < key[(size_t)b];
+  });
   const int nc = std::min<int>(n_kp_global, (int)order.size());
-  *out_n_consensus = nc;
+  *out_n = nc;
   for (int k = 0; k < nc; ++k) {
     if (out_consensus) out_consensus[k] = order[(size_t)k];
-    if (out_votes) out_votes[k] = count[(size_t)order[(size_t)k]];
+    if (out_votes) out_votes[k] = (int32_t)cnt[(size_t)order[(size_t)k]];
   }
   if (nc < n_min)
     return fail(KCMC_EALIGN,
                 "Too few keypoints found. Try a higher quality video, or decrease "
                 "`VideoAligner.N_KP_GLOBAL_MIN`");
-  // consensus_idxs = set(consensus_idxs) (VA:248)
-  PySet cons;
-  for (int k = 0; k < nc; ++k) cons.add(order[(size_t)k]);
-  std::vector<int32_t> cons_iter;
-  cons_iter.reserve((size_t)nc);
-  cons.for_each([&](int64_t key) { cons_iter.push_back((int32_t)key); });
+  if (out_cons_pack) {
+    PySet cons;
+    for (int k = 0; k < nc; ++k) cons.add(order[(size_t)k]);
+    int n = 0;
+    cons.for_each([&](int64_t k) { out_cons_pack[n++] = (int32_t)k; });
+    const int words = (n_tpl + 31) / 32;
+    uint32_t* bits = reinterpret_cast<uint32_t*>(out_cons_pack + nc);
+    for (int k = 0; k < words; ++k) bits[k] = 0u;
+    for (int k = 0; k < nc; ++k) bits[order[(size_t)k] >> 5] |= 1u << (order[(size_t)k] & 31);
+  }
+  return KCMC_OK;
+}
+
+// list(consensus_idxs.intersection(kp_idxs_list[f])) (VA:274) for frames [f_begin, f_end):
+// out_pt_off [f_end - f_begin + 1] (from 0), out_pt_idx [(f_end - f_begin) * nc].
+// set_intersection iterates the smaller set (the frame's when len(frame) <= len(consensus))
+// and inserts the hits into a fresh set, whose iteration order is the result.
+int lookup_impl(const uint32_t* keep_bits, int f_begin, int f_end, int n_tpl, const int32_t* cons_iter, int nc,
+                int32_t* out_pt_off, int32_t* out_pt_idx) {
+  const int words = (n_tpl + 31) / 32;
+  auto frame_bits = [&](int f) { return keep_bits + (size_t)f * words; };
   std::vector<uint32_t> cons_bits((size_t)words, 0u);
-  for (int32_t key : cons_iter) cons_bits[(size_t)(key >> 5)] |= 1u << (key & 31);
-  // list(consensus_idxs.intersection(kp_idxs_list[i])) (VA:274): set_intersection
-  // iterates the smaller set (the frame's when len(frame) <= len(consensus)) and
-  // inserts the hits into a fresh set, whose iteration order is the result.
-  //
-  // Shortcut: without deletions a set's table size after m insertions depends on m
-  // only (table_size_after), and when every key is below that size each key sits in
-  // its own home slot (hash(i) = i), so the iteration order is ascending whatever the
-  // insertion and resize history.  Only frames whose result keeps a key >= its final
-  // table size replay the insertions.
+  for (int k = 0; k < nc; ++k) {
+    const int32_t key = cons_iter[k];
+    if (key < 0 || key >= n_tpl) return fail(KCMC_EINVAL, "consensus lookup: consensus index out of range");
+    cons_bits[(size_t)(key >> 5)] |= 1u << (key & 31);
+  }
+  // Shortcut: without deletions a set's table size after m insertions depends on m only
+  // (PySet::table_sizes), and when every key is below that size each key sits in its own
+  // home slot (hash(i) = i), so the iteration order is ascending whatever the insertion and
+  // resize history.  Only frames whose result keeps a key >= its final table size replay.
   const std::vector<size_t> tsize = PySet::table_sizes((size_t)nc);
   const int nf = f_end - f_begin;
   // per-frame results into a [nf, nc] scratch (no per-frame allocation), compacted below
@@ -565,16 +619,20 @@ extern "C" int kcmc_consensus_slice(const uint32_t* keep_bits, int n_frames, int
     if (flen > (size_t)nc && (size_t)nc <= 1228) {
       // the common replay: iterate the consensus set, insert the frame's keys
       SmallPySet result;
-      for (int32_t key : cons_iter)
+      for (int k = 0; k < nc; ++k) {
+        const int32_t key = cons_iter[k];
         if ((w[key >> 5] >> (key & 31)) & 1u) result.add(key);
+      }
       result.for_each([&](int32_t key) { L[n++] = key; });
     } else {
       PySet result;
       if (flen > (size_t)nc) {
-        for (int32_t key : cons_iter)
+        for (int k = 0; k < nc; ++k) {
+          const int32_t key = cons_iter[k];
           if ((w[key >> 5] >> (key & 31)) & 1u) result.add(key);
+        }
       } else {
-        frame_set(f).for_each([&](int64_t key) {
+        frame_set_of(w, words).for_each([&](int64_t key) {
           if ((cons_bits[(size_t)(key >> 5)] >> (key & 31)) & 1u) result.add(key);
         });
       }
@@ -590,6 +648,49 @@ extern "C" int kcmc_consensus_slice(const uint32_t* keep_bits, int n_frames, int
     out_pt_off[r + 1] = out_pt_off[r] + len[(size_t)r];
   }
   return KCMC_OK;
+}
+
+}  // namespace kcmc
+
+extern "C" int kcmc_consensus_vote_host(const uint32_t* keep_bits, int n_frames, int n_tpl, long long frame_base,
+                                        int64_t* out_votes) {
+  if (n_frames < 0 || n_tpl < 0 || (!keep_bits && n_frames > 0 && n_tpl > 0) || (!out_votes && n_tpl > 0) ||
+      frame_base < 0 || frame_base + (long long)n_frames > (long long)INT32_MAX)
+    return fail(KCMC_EINVAL, "kcmc_consensus_vote_host: bad arguments");
+  return vote_impl(keep_bits, n_frames, n_tpl, (int64_t)frame_base, out_votes);
+}
+
+extern "C" int kcmc_consensus_merge(const int64_t* votes, int world, int n_tpl, int n_kp_global, int n_min,
+                                    int32_t* out_consensus, int32_t* out_votes, int* out_n_consensus,
+                                    int32_t* out_cons_pack) {
+  if (world < 1 || n_tpl < 0 || n_kp_global < 0 || (!votes && n_tpl > 0) || !out_n_consensus)
+    return fail(KCMC_EINVAL, "kcmc_consensus_merge: bad arguments");
+  return merge_impl(votes, world, n_tpl, n_kp_global, n_min, out_consensus, out_votes, out_n_consensus,
+                    out_cons_pack);
+}
+
+extern "C" int kcmc_consensus_lookup_host(const uint32_t* keep_bits, int n_frames, int n_tpl, const int32_t* cons_iter,
+                                          int nc, int32_t* out_pt_off, int32_t* out_pt_idx) {
+  if (n_frames < 0 || n_tpl < 0 || nc < 0 || (!keep_bits && n_frames > 0 && n_tpl > 0) ||
+      (!cons_iter && nc > 0) || !out_pt_off)
+    return fail(KCMC_EINVAL, "kcmc_consensus_lookup_host: bad arguments");
+  return lookup_impl(keep_bits, 0, n_frames, n_tpl, cons_iter, nc, out_pt_off, out_pt_idx);
+}
+
+extern "C" int kcmc_consensus_slice(const uint32_t* keep_bits, int n_frames, int n_tpl, int n_kp_global,
+                                    int n_min, int f_begin, int f_end, int32_t* out_consensus,
+                                    int32_t* out_votes, int* out_n_consensus, int32_t* out_pt_off,
+                                    int32_t* out_pt_idx) {
+  if (n_frames < 0 || n_tpl < 0 || n_kp_global < 0 || (!keep_bits && n_frames > 0) ||
+      !out_n_consensus || !out_pt_off || f_begin < 0 || f_end < f_begin || f_end > n_frames)
+    return fail(KCMC_EINVAL, "kcmc_consensus: bad arguments");
+  std::vector<int64_t> votes((size_t)2 * (size_t)n_tpl);
+  KCMC_TRY(vote_impl(keep_bits, n_frames, n_tpl, 0, votes.data()));
+  const int words = (n_tpl + 31) / 32;
+  std::vector<int32_t> pack((size_t)n_kp_global + (size_t)words);
+  KCMC_TRY(merge_impl(votes.data(), 1, n_tpl, n_kp_global, n_min, out_consensus, out_votes, out_n_consensus,
+                      pack.data()));
+  return lookup_impl(keep_bits, f_begin, f_end, n_tpl, pack.data(), *out_n_consensus, out_pt_off, out_pt_idx);
 }
 
 extern "C" int kcmc_consensus(const uint32_t* keep_bits, int n_frames, int n_tpl, int n_kp_global,

@@ -444,10 +444,10 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
 
 using namespace kcmc;
 
-extern "C" int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src, const double* dst, const int32_t* pt_idx,
+static int ransac_rigid_impl(kcmc_ctx* ctx, const double* src, const double* dst, const int32_t* pt_idx,
                                  const int32_t* pt_off, int src_frame_stride, int n_frames, int max_n, int trials,
                                  double thresh, double rate, int n_skip, double* out_params, uint8_t* out_inliers,
-                                 int32_t* out_n_inliers, int32_t* out_best_trial, kcmc_stream_t stream) {
+                                 int32_t* out_n_inliers, int32_t* out_best_trial, int max_workgroups, kcmc_stream_t stream) {
   if (!ctx) return fail(KCMC_EINVAL, "kcmc_ransac_rigid: ctx is NULL");
   if (n_frames < 0 || max_n < 0 || trials < 1) return fail(KCMC_EINVAL, "kcmc_ransac_rigid: bad sizes");
   if (n_frames == 0) return KCMC_OK;
@@ -469,7 +469,7 @@ extern "C" int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src, const double*
   if ((max_n > 128 ? lds_large : lds_small) > 150 * 1024)
     return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_rigid: max_n/trials exceed the LDS budget");
   hipStream_t s = (hipStream_t)stream;
-  const unsigned grid = (unsigned)(ctx->ransac_grid > 0 && ctx->ransac_grid < n_frames ? ctx->ransac_grid : n_frames);
+  const unsigned grid = (unsigned)(max_workgroups > 0 && max_workgroups < n_frames ? max_workgroups : n_frames);
   hipLaunchKernelGGL(ransac_rigid_kernel<false>, dim3(grid), dim3(kThreads), lds_small, s, n_frames, src, dst, pt_idx,
                      pt_off, src_frame_stride, ctx->hyp, ctx->hyp_off, ctx->hyp_off_len, trials, thresh, tq, rate, n_skip,
                      out_params, out_inliers, out_n_inliers, out_best_trial);
@@ -481,4 +481,19 @@ extern "C" int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src, const double*
     KCMC_TRY(launch_check("ransac_rigid_kernel<large>"));
   }
   return KCMC_OK;
+}
+
+extern "C" int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src, const double* dst, const int32_t* pt_idx,
+                                 const int32_t* pt_off, int src_frame_stride, int n_frames, int max_n, int trials,
+                                 double thresh, double rate, int n_skip, double* out_params, uint8_t* out_inliers,
+                                 int32_t* out_n_inliers, int32_t* out_best_trial, kcmc_stream_t stream) {
+  return ransac_rigid_impl(ctx, src, dst, pt_idx, pt_off, src_frame_stride, n_frames, max_n, trials, thresh, rate, n_skip, out_params, out_inliers, out_n_inliers, out_best_trial, ctx ? ctx->ransac_grid : 0, stream);
+}
+
+extern "C" int kcmc_ransac_rigid_grid(kcmc_ctx* ctx, const double* src, const double* dst, const int32_t* pt_idx,
+                                 const int32_t* pt_off, int src_frame_stride, int n_frames, int max_n, int trials,
+                                 double thresh, double rate, int n_skip, double* out_params, uint8_t* out_inliers,
+                                 int32_t* out_n_inliers, int32_t* out_best_trial, int max_workgroups, kcmc_stream_t stream) {
+  if (max_workgroups < 0) return fail(KCMC_EINVAL, "kcmc_ransac_rigid_grid: max_workgroups < 0");
+  return ransac_rigid_impl(ctx, src, dst, pt_idx, pt_off, src_frame_stride, n_frames, max_n, trials, thresh, rate, n_skip, out_params, out_inliers, out_n_inliers, out_best_trial, max_workgroups, stream);
 }

@@ -809,11 +809,11 @@ __global__ __launch_bounds__(256) void ransac_model_refit_kernel(
 
 using namespace kcmc;
 
-extern "C" int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src, const double* dst,
+static int ransac_model_impl(kcmc_ctx* ctx, int model, const double* src, const double* dst,
                                  const int32_t* pt_idx, const int32_t* pt_off, int src_frame_stride, int n_frames,
                                  int max_n, int trials, double thresh, double rate, int n_skip, double* out_params,
                                  uint8_t* out_inliers, int32_t* out_n_inliers, int32_t* out_best_trial,
-                                 kcmc_stream_t stream) {
+                                 int max_workgroups, kcmc_stream_t stream) {
   if (!ctx) return fail(KCMC_EINVAL, "kcmc_ransac_model: ctx is NULL");
   if (model != KCMC_MODEL_AFFINE && model != KCMC_MODEL_PROJECTIVE)
     return fail(KCMC_EINVAL, "kcmc_ransac_model: model must be KCMC_MODEL_AFFINE or KCMC_MODEL_PROJECTIVE "
@@ -848,7 +848,7 @@ extern "C" int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src, co
   // allocation cost ~0.2 ms of host time per call.
   double* best_model = out_params;
   const dim3 refit_grid((unsigned)ceil_div(n_frames, 4));
-  const unsigned grid = (unsigned)(ctx->ransac_grid > 0 && ctx->ransac_grid < n_frames ? ctx->ransac_grid : n_frames);
+  const unsigned grid = (unsigned)(max_workgroups > 0 && max_workgroups < n_frames ? max_workgroups : n_frames);
   if (model == KCMC_MODEL_AFFINE) {
     hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, false>), dim3(grid), dim3(kThreads),
                        lds_small, s, n_frames, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
@@ -872,4 +872,21 @@ extern "C" int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src, co
                        out_params);
   }
   return launch_check("ransac_model kernels");
+}
+
+extern "C" int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src, const double* dst,
+                                 const int32_t* pt_idx, const int32_t* pt_off, int src_frame_stride, int n_frames,
+                                 int max_n, int trials, double thresh, double rate, int n_skip, double* out_params,
+                                 uint8_t* out_inliers, int32_t* out_n_inliers, int32_t* out_best_trial,
+                                 kcmc_stream_t stream) {
+  return ransac_model_impl(ctx, model, src, dst, pt_idx, pt_off, src_frame_stride, n_frames, max_n, trials, thresh, rate, n_skip, out_params, out_inliers, out_n_inliers, out_best_trial, ctx ? ctx->ransac_grid : 0, stream);
+}
+
+extern "C" int kcmc_ransac_model_grid(kcmc_ctx* ctx, int model, const double* src, const double* dst,
+                                 const int32_t* pt_idx, const int32_t* pt_off, int src_frame_stride, int n_frames,
+                                 int max_n, int trials, double thresh, double rate, int n_skip, double* out_params,
+                                 uint8_t* out_inliers, int32_t* out_n_inliers, int32_t* out_best_trial,
+                                 int max_workgroups, kcmc_stream_t stream) {
+  if (max_workgroups < 0) return fail(KCMC_EINVAL, "kcmc_ransac_model_grid: max_workgroups < 0");
+  return ransac_model_impl(ctx, model, src, dst, pt_idx, pt_off, src_frame_stride, n_frames, max_n, trials, thresh, rate, n_skip, out_params, out_inliers, out_n_inliers, out_best_trial, max_workgroups, stream);
 }

@@ -94,21 +94,42 @@ def log_frame_counts(logger: logging.Logger, counts: np.ndarray, first_index: in
         )
 
 
-def match_stage(inp: SlabInputs, cfg: AlignConfig) -> stages.MatchResult:
+def _nomark(name, ev=None):
+    return None
+
+
+def match_stage(inp: SlabInputs, cfg: AlignConfig, stream: Optional[int] = None) -> stages.MatchResult:
     return stages.match_frames(inp.des_tpl, inp.kp_tpl, inp.des_q, inp.kp_q, inp.q_off, inp.q_off_host,
-                               ratio=cfg.ratio, d_lo=cfg.d_lo, d_hi=cfg.d_hi, norm=cfg.match_norm)
+                               ratio=cfg.ratio, d_lo=cfg.d_lo, d_hi=cfg.d_hi, norm=cfg.match_norm, stream=stream)
+
+
+def _log_rates(logger: Optional[logging.Logger], votes: np.ndarray, n_frames: int) -> None:
+    if logger is not None and logger.isEnabledFor(logging.INFO):
+        rates = np.array(votes, dtype=np.int64) / n_frames
+        logger.info(f"top n keypoints match rates: {rates}")
+
+
+def _log_low_counts(logger: Optional[logging.Logger], ns: np.ndarray, cfg: AlignConfig, first_index: int = 0) -> None:
+    """VA:279-283: frames whose consensus point list is shorter than N_KP_FRAME_SKIP."""
+    if logger is None or not logger.isEnabledFor(logging.INFO):
+        return
+    for i in np.flatnonzero(ns < cfg.n_kp_frame_skip):
+        logger.info(
+            f"transform for frame {int(i) + first_index} not estimated due to low keypoint count: "
+            f"({int(ns[i])}). Will be interpolated based on other frames instead"
+        )
 
 
 def consensus_stage(keep_bits_host: np.ndarray, n_tpl: int, n_frames: int, cfg: AlignConfig,
                     logger: Optional[logging.Logger] = None,
                     frames: Optional[Tuple[int, int]] = None) -> stages.Consensus:
-    """VA:224-286.  With ``frames`` = (f_begin, f_end) the point lists are made for those
-    frames only (a rank's share of a frame-sharded job; pt_off starts at 0), the
-    consensus and the per-frame log lines still cover every frame."""
+    """VA:224-286 on the host from every frame's survivor bitmask.  With ``frames`` =
+    (f_begin, f_end) the point lists are made for those frames only (pt_off starts at 0);
+    the consensus and the per-frame log lines still cover every frame.  The pipelines use
+    the device consensus (device_consensus / OverlappedSlabs) instead."""
     cons = stages.consensus(keep_bits_host, n_tpl, cfg.n_kp_global, cfg.n_kp_global_min, frames=frames)
+    _log_rates(logger, cons.votes, n_frames)
     if logger is not None and logger.isEnabledFor(logging.INFO):
-        rates = np.array(cons.votes, dtype=np.int64) / n_frames
-        logger.info(f"top n keypoints match rates: {rates}")
         if frames is None:
             ns = np.diff(cons.pt_off)
         else:  # every frame's point count = |consensus set & frame set|, from the bitmasks
@@ -117,16 +138,42 @@ def consensus_stage(keep_bits_host: np.ndarray, n_tpl: int, n_frames: int, cfg: 
             for k in np.asarray(cons.order, dtype=np.int64):
                 cbits[k >> 5] |= np.uint32(1) << np.uint32(k & 31)
             ns = np.unpackbits((kb & cbits).view(np.uint8), axis=1).sum(axis=1)
-        for i in np.flatnonzero(ns < cfg.n_kp_frame_skip):
-            logger.info(
-                f"transform for frame {int(i)} not estimated due to low keypoint count: "
-                f"({int(ns[i])}). Will be interpolated based on other frames instead"
-            )
+        _log_low_counts(logger, ns, cfg)
+    return cons
+
+
+def choose_consensus(votes_host: np.ndarray, n_tpl: int, n_frames: int, cfg: AlignConfig,
+                     logger: Optional[logging.Logger] = None,
+                     pack_out: Optional[np.ndarray] = None) -> stages.ConsensusChoice:
+    """VA:224-249 from the (merged) votes of every frame: Counter.most_common order,
+    AlignmentError below N_KP_GLOBAL_MIN, the match-rate log line, set(consensus) order."""
+    choice = stages.consensus_merge(votes_host, n_tpl, cfg.n_kp_global, cfg.n_kp_global_min, pack_out)
+    _log_rates(logger, choice.votes, n_frames)
+    return choice
+
+
+def lookup_stage(match: stages.MatchResult, n_tpl: int, choice: stages.ConsensusChoice, pack_dev: torch.Tensor,
+                 stream: Optional[int] = None) -> stages.Consensus:
+    """VA:251-286 on the device: every frame's RANSAC point list (CSR, device)."""
+    pt_off, pt_idx = stages.consensus_lookup(match.keep_bits, n_tpl, pack_dev, choice.nc, stream=stream)
+    return stages.Consensus(choice.order, choice.votes, pt_off_dev=pt_off, pt_idx_dev=pt_idx)
+
+
+def device_consensus(match: stages.MatchResult, n_tpl: int, n_frames: int, cfg: AlignConfig,
+                     logger: Optional[logging.Logger] = None) -> stages.Consensus:
+    """The whole consensus (VA:224-286) of one slab with the per-frame parts on the device
+    (vote, lookup) and only the O(n_tpl) votes on the host (synchronous)."""
+    votes = stages.consensus_vote(match.keep_bits, n_tpl)
+    choice = choose_consensus(votes.cpu().numpy(), n_tpl, n_frames, cfg, logger)
+    pack_dev = torch.from_numpy(choice.pack).to(match.keep_bits.device)
+    cons = lookup_stage(match, n_tpl, choice, pack_dev)
+    if logger is not None and logger.isEnabledFor(logging.INFO):
+        _log_low_counts(logger, np.diff(cons.pt_off), cfg)
     return cons
 
 
 def consensus_to_device(cons: stages.Consensus, dev) -> Tuple[torch.Tensor, torch.Tensor]:
-    """The consensus point lists (pt_off, pt_idx) as device tensors.  Stream-ordered
+    """Host consensus point lists (pt_off, pt_idx) as device tensors.  Stream-ordered
     copies from pinned staging (the caching host allocator keeps the staging alive until
     the copy has run): a pageable copy would block the host until the stream drains."""
     pt_off = torch.from_numpy(cons.pt_off).pin_memory().to(dev, non_blocking=True)
@@ -134,25 +181,54 @@ def consensus_to_device(cons: stages.Consensus, dev) -> Tuple[torch.Tensor, torc
     return pt_off, pt_idx.pin_memory().to(dev, non_blocking=True)
 
 
+def prepare_ransac(device, cfg: AlignConfig) -> None:
+    """Hypothesis tables for every point count a device-consensus frame can have."""
+    stages.ransac_prepare_range(device, cfg.ransac_model, max(cfg.effective_frame_skip, 3), cfg.n_kp_global,
+                                cfg.ransac_trials, cfg.seed)
+
+
+def _check_point_counts(cons: stages.Consensus, cfg: AlignConfig) -> None:
+    """skimage raises when a frame is not skipped but has N <= min_samples (fit.py:798-799);
+    only reachable when N_KP_FRAME_SKIP <= min_samples (the host then reads pt_off)."""
+    ms = {"euclidean": cfg.ransac_min_samples, "affine": 3, "projective": 4}[cfg.ransac_model]
+    skip = cfg.effective_frame_skip
+    if skip > ms:
+        return
+    ns = np.diff(cons.pt_off)
+    if ((ns >= skip) & (ns <= ms)).any():
+        raise ValueError("`min_samples` must be in range (0, <number-of-samples>)")
+
+
 def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.Consensus,
-                 cfg: AlignConfig, lists_dev: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
-                 ) -> stages.RansacResult:
+                 cfg: AlignConfig, lists_dev: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                 stream: Optional[int] = None, max_workgroups: int = 0) -> stages.RansacResult:
     """VA:137-142: RANSAC of every frame's consensus points (src = the frame's matched
     keypoints, dst = template keypoints).  params [F, 2, 3] for the euclidean and
     affine models (model.params[:2], like VA:319), [F, 3, 3] for the projective one.
-    ``lists_dev``: the consensus lists already on the device (consensus_to_device)."""
+    Device point lists (device_consensus / lookup_stage) run with the tables of every
+    count up to n_kp_global; host lists (consensus_stage) are uploaded first unless
+    ``lists_dev`` holds them already."""
     dev = kp_tpl.device
     F, n_tpl = match.kp_ordered.shape[:2]
-    pt_off, pt_idx = lists_dev if lists_dev is not None else consensus_to_device(cons, dev)
-    if cfg.ransac_model == "euclidean":
-        return stages.ransac_rigid(match.kp_ordered.view(F * n_tpl, 2), kp_tpl, pt_off, cons.pt_off, pt_idx=pt_idx,
-                                   src_frame_stride=n_tpl, trials=cfg.ransac_trials,
-                                   residual_threshold=cfg.ransac_threshold, spatial_rate=cfg.spatial_rate,
-                                   n_skip=cfg.n_kp_frame_skip, seed=cfg.seed, min_samples=cfg.ransac_min_samples)
-    rr = stages.ransac_model(match.kp_ordered.view(F * n_tpl, 2), kp_tpl, pt_off, cons.pt_off, model=cfg.ransac_model,
-                             pt_idx=pt_idx, src_frame_stride=n_tpl, trials=cfg.ransac_trials,
-                             residual_threshold=cfg.ransac_threshold, spatial_rate=cfg.spatial_rate,
-                             n_skip=cfg.effective_frame_skip, seed=cfg.seed)
+    src = match.kp_ordered.view(F * n_tpl, 2)
+    if lists_dev is None and cons.pt_off_dev is not None:
+        _check_point_counts(cons, cfg)
+        prepare_ransac(dev, cfg)
+        rr = stages.ransac_lists(cfg.ransac_model, src, kp_tpl, cons.pt_off_dev, cons.pt_idx_dev, n_tpl,
+                                 max_n=max(len(cons.order), 1), trials=cfg.ransac_trials,
+                                 residual_threshold=cfg.ransac_threshold, spatial_rate=cfg.spatial_rate,
+                                 n_skip=cfg.effective_frame_skip, stream=stream, max_workgroups=max_workgroups)
+    else:
+        pt_off, pt_idx = lists_dev if lists_dev is not None else consensus_to_device(cons, dev)
+        if cfg.ransac_model == "euclidean":
+            return stages.ransac_rigid(src, kp_tpl, pt_off, cons.pt_off, pt_idx=pt_idx,
+                                       src_frame_stride=n_tpl, trials=cfg.ransac_trials,
+                                       residual_threshold=cfg.ransac_threshold, spatial_rate=cfg.spatial_rate,
+                                       n_skip=cfg.n_kp_frame_skip, seed=cfg.seed, min_samples=cfg.ransac_min_samples)
+        rr = stages.ransac_model(src, kp_tpl, pt_off, cons.pt_off, model=cfg.ransac_model,
+                                 pt_idx=pt_idx, src_frame_stride=n_tpl, trials=cfg.ransac_trials,
+                                 residual_threshold=cfg.ransac_threshold, spatial_rate=cfg.spatial_rate,
+                                 n_skip=cfg.effective_frame_skip, seed=cfg.seed)
     if cfg.ransac_model == "affine":
         rr.params = rr.params[:, :2].contiguous()
     return rr
@@ -161,8 +237,13 @@ def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.C
 def postprocess_affines(params_host: np.ndarray, cfg: AlignConfig):
     """VA:143-145 on the host: NaN-pad, interpolate, Euclidean summary.  The
     reference's rotation-angle lerp (VA:409-437) assumes rigid matrices; the extension
-    models interpolate their gaps entry-wise linearly instead."""
-    affines, skipped = _aff.process_affines(np.asarray(params_host), cfg.frame_downsample_rate)
+    models interpolate their gaps entry-wise linearly instead.  Every frame with a model
+    and no temporal downsampling (the common case) is one copy."""
+    a = np.asarray(params_host)
+    if int(cfg.frame_downsample_rate) == 1 and not _aff._nan_rows(a).any():
+        affines = np.array(a, dtype=np.float64, copy=True)
+        return affines, [], [], _aff.euclidean_transforms(affines)
+    affines, skipped = _aff.process_affines(a, cfg.frame_downsample_rate)
     if cfg.ransac_model == "euclidean":
         affines, interpolated = _aff.interpolate_affines(affines)
     else:
@@ -170,11 +251,12 @@ def postprocess_affines(params_host: np.ndarray, cfg: AlignConfig):
     return affines, skipped, interpolated, _aff.euclidean_transforms(affines)
 
 
-def warp_frames(frames: torch.Tensor, maps: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def warp_frames(frames: torch.Tensor, maps: torch.Tensor, out: Optional[torch.Tensor] = None,
+                stream: Optional[int] = None) -> torch.Tensor:
     """VA:150 on the device: warpAffine for [F, 2, 3] maps, warpPerspective for [F, 3, 3]."""
     if maps.shape[1:] == (3, 3):
-        return stages.warp_perspective_u16(frames, maps, out=out)
-    return stages.warp_affine_u16(frames, maps, out=out)
+        return stages.warp_perspective_u16(frames, maps, out=out, stream=stream)
+    return stages.warp_affine_u16(frames, maps, out=out, stream=stream)
 
 
 def warp_stage(frames: torch.Tensor, affines: np.ndarray, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -193,8 +275,7 @@ def align_slab(inp: SlabInputs, cfg: AlignConfig, logger: Optional[logging.Logge
     counts = match.counts.cpu().numpy() if logger.isEnabledFor(logging.DEBUG) else None
     if counts is not None:
         log_frame_counts(logger, counts)
-    keep = match.keep_bits.cpu().numpy()
-    cons = consensus_stage(keep, n_tpl, n_sample, cfg, logger)
+    cons = device_consensus(match, n_tpl, n_sample, cfg, logger)
     rr = ransac_stage(match, inp.kp_tpl, cons, cfg)
     params = rr.params.cpu().numpy()
     affines, skipped, interpolated, eu = postprocess_affines(params, cfg)
@@ -236,24 +317,41 @@ def _h2d_async(arrays, dev, copy: torch.cuda.Stream):
     return outs
 
 
+class _Slot:
+    """Pinned host staging and transfer events of one slab in flight; slots are reused by
+    later slabs once their slab is finished (every transfer through them has completed)."""
+
+    def __init__(self):
+        self.bufs = {}
+        self.votes_ev = torch.cuda.Event()
+        self.pack_ev = torch.cuda.Event()
+        self.params_ev = torch.cuda.Event()
+
+    def buf(self, name: str, numel: int, dtype: torch.dtype) -> torch.Tensor:
+        b = self.bufs.get(name)
+        if b is None or b.numel() < numel or b.dtype != dtype:
+            b = torch.empty(max(numel, 1), dtype=dtype, pin_memory=True)
+            self.bufs[name] = b
+        return b[:numel]
+
+
 @dataclass
 class _SlabInFlight:
-    """A slab on its way through the pipeline: matched (survivor bitmasks on their way to
-    the host), then fitted (RANSAC queued, parameters on their way to the host)."""
+    """A slab on its way through the pipeline: matched (votes on their way to the host),
+    then fitted (consensus lookup + RANSAC queued, parameters on their way to the host)."""
 
     inp: SlabInputs
     out: Optional[torch.Tensor]
     f0: int
     match: stages.MatchResult
-    keep_host: torch.Tensor
-    keep_ready: torch.cuda.Event
+    slot: _Slot
+    n_votes: int                                   # elements of the (gathered) votes
+    matched: Optional[torch.cuda.Event] = None     # end of match(k) + vote on the kernel stream
     cons: Optional[stages.Consensus] = None
     rr: Optional[stages.RansacResult] = None
-    params_host: Optional[torch.Tensor] = None
-    params_ready: Optional[torch.cuda.Event] = None
     aligned: Optional[torch.Tensor] = None
-    matched: Optional[torch.cuda.Event] = None   # end of match(k) on the kernel stream (corun)
-    fitted_ev: Optional[torch.cuda.Event] = None  # end of RANSAC(k) on the analysis stream (corun)
+    fitted_ev: Optional[torch.cuda.Event] = None   # end of RANSAC(k) on the analysis stream (corun)
+    n_bound: int = 0                               # elements of the gathered boundaries (sharded)
 
 
 class OverlappedSlabs:
@@ -261,38 +359,38 @@ class OverlappedSlabs:
 
     submit(slab k) queues, in this device order (``depth=2``, the default),
 
-        kernel stream:    match(k) -> warp(k-1) -> [waits RANSAC(k)] -> warp(k) ...
-        analysis stream:              RANSAC(k)   (beside warp(k-1))
+        kernel stream:    match(k) -> vote(k) -> warp(k-1) -> [waits RANSAC(k)] -> warp(k) ...
+        analysis stream:                         lookup(k) -> RANSAC(k)   (beside warp(k-1))
 
-    with every transfer on a side stream: the host enqueues match(k) and the warp of the
-    slab fitted last time, then waits for slab k's survivor bitmasks (VA:224-286
-    consensus) while warp(k-1) keeps the device busy, and queues RANSAC(k) on the
-    analysis stream, where it shares the CUs with warp(k-1) (``corun``, the default).
-    The warp is bound by HBM at the speed of a plain copy, so the FP64 RANSAC work mostly
-    fits beside it (c2: the warp slows by ~0.18 ms and 0.23 ms of RANSAC leave the step);
-    the match stays on the kernel stream (its persistent large-LDS workgroups starve
-    beside the warp's tiles and delay the consensus).  ``corun=False`` queues RANSAC(k)
-    behind warp(k-1) on the one kernel stream, so a step costs the sum of its kernels.
-    ``depth=3`` queues match(k) -> warp(k-2) -> RANSAC(k-1) instead, so the consensus uses
-    bitmasks that were ready a whole step earlier; same-box A/B
-    found it no faster at c2 and slower at c3, so it is opt-in.  The warp of a slab reads
-    its RANSAC parameters where RANSAC left them: with frame_downsample_rate == 1 the
-    reference's post-processing (VA:143-145) hands a frame with a model its own
-    parameters, so only frames without a model need the host (NaN-gap interpolation); the
-    warp writes zeros for those and they are warped again, with the filled maps, once the
-    host has them.  With frame_downsample_rate > 1 every full-rate frame's map comes from
-    the host interpolation, and the warp of slab k waits for it.  Every slab runs every
-    stage and its results equal ``align_slab``'s.
+    with every transfer on a side stream.  The consensus (VA:224-286) runs in three parts:
+    the vote (per template count + first occurrence, VA:239) on the device right behind the
+    match, the merge (Counter.most_common, set(consensus), VA:240-248) on the host from the
+    O(n_tpl) votes, and the per-frame lookup (VA:274) on the device in front of RANSAC, so
+    only the votes, the consensus set and the parameters cross PCIe.  RANSAC(k) shares the
+    CUs with warp(k-1) (``corun``, the default: the warp is bound by HBM at the speed of a
+    plain copy and leaves VALU slots free); ``corun=False`` queues lookup/RANSAC(k) behind
+    warp(k-1) on the one kernel stream.  ``depth=3`` queues match(k) -> warp(k-2) ->
+    lookup/RANSAC(k-1) instead, so the host merge uses votes that were ready a whole step
+    earlier.  The warp of a slab reads its RANSAC parameters where RANSAC left them: with
+    frame_downsample_rate == 1 the reference's post-processing (VA:143-145) hands a frame
+    with a model its own parameters, so only frames without a model need the host (NaN-gap
+    interpolation); the warp writes zeros for those and they are warped again, with the
+    filled maps, once the host has them.  With frame_downsample_rate > 1 every full-rate
+    frame's map comes from the host interpolation, and the warp of slab k waits for it.
+    Every slab runs every stage and its results equal ``align_slab``'s.
 
     submit returns the SlabResult of the slab ``depth - 1`` submissions back (None
     before that); flush() finishes the slabs still in flight and returns their results
-    in order.
-    ``res.extras["done"]`` is an event after the slab's last warp; ``aligned`` is ready
-    once it has passed (or after synchronize()).
+    in order.  ``res.extras["done"]`` is an event after the slab's last warp; ``aligned`` is
+    ready once it has passed (or after synchronize()).
 
     With ``counts`` (frames per rank) the slabs are one rank's share of a frame-sharded
-    job: survivor bitmasks and RANSAC parameters are all-gathered over ``group``
-    (distributed.align_sharded's two exchanges) in the same stream order on every rank.
+    job (frame_downsample_rate 1): the votes [2, n_tpl] and each slab's parameter boundary
+    (first / last frame with a model, kcmc_params_boundary) are all-gathered over ``group``
+    in the same stream order on every rank, so a rank's host work per step is O(its own
+    frames + world * n_tpl).  A rank's result holds its own frames (``extras["f0"]`` = the
+    global index of the first): affines / euclidean of those frames, skipped and
+    interpolated as global indices inside them.
 
         ov = OverlappedSlabs(device, cfg)
         results = [r for r in (ov.submit(inp) for inp in slabs) if r is not None] + ov.flush()
@@ -316,17 +414,32 @@ class OverlappedSlabs:
         self.counts = counts
         self.group = group
         self.stream = torch.cuda.Stream(self.dev)
-        self.copy = torch.cuda.Stream(self.dev)  # bitmask / point-list / params / map transfers
-        # corun: RANSAC(k) on an analysis stream, beside warp(k-1) instead of behind it (the
-        # warp of slab k waits for it).  Same-box A/B: faster at c2, c3
-        # and c5; the match stays on the kernel stream (beside the warp it starves).
+        self.copy = torch.cuda.Stream(self.dev)  # vote / consensus / params / map transfers
+        # corun: lookup + RANSAC(k) on an analysis stream, beside warp(k-1) instead of behind
+        # it (the warp of slab k waits for it).  Same-box A/B: faster at
+        # c2, c3 and c5; the match stays on the kernel stream (beside the warp it starves).
         self.corun = bool(corun)
         self.ana = torch.cuda.Stream(self.dev) if self.corun else None
+        self._hs = self.stream.cuda_stream
+        self._hc = self.copy.cuda_stream
+        self._ha = self.ana.cuda_stream if self.corun else self._hs
         # RANSAC beside the warp on at most this many workgroups (each walks its share of
         # the frames; 0 / None = one per frame).  Same-box A/B at c2:
         # 128, 256 or 512 workgroups were no faster than one per frame, so the default
         # stays one per frame.
         self.ransac_grid = int(ransac_grid or 0) if self.corun else 0
+        self._rank = 0
+        self._world = 1
+        self._f0 = 0
+        self._nccl = False
+        if self._sharded():
+            import torch.distributed as dist
+
+            self._rank = dist.get_rank(group)
+            self._world = dist.get_world_size(group)
+            self._f0 = sum(counts[: self._rank])
+            self._nccl = dist.get_backend(group) == "nccl"
+        self._slots: List[_Slot] = []
         self._matched: Optional[_SlabInFlight] = None  # match queued, consensus pending
         self._fitted: Optional[_SlabInFlight] = None   # RANSAC queued, warp pending
         self._tail: Optional[torch.cuda.Event] = None   # an event at the kernel stream's tail
@@ -352,19 +465,31 @@ class OverlappedSlabs:
     def _device_maps(self) -> bool:
         return int(self.cfg.frame_downsample_rate) == 1
 
-    def _rank(self) -> int:
-        if not self._sharded():
-            return 0
+    def _gather(self, t: torch.Tensor) -> torch.Tensor:
+        """All-gather of an equally sized tensor over the ranks, on the current stream:
+        [world, *t.shape]."""
         import torch.distributed as dist
 
-        return dist.get_rank(self.group)
+        out = torch.empty((self._world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        if self._nccl:
+            dist.all_gather_into_tensor(out, t, group=self.group)
+        else:
+            dist.all_gather(list(out.unbind(0)), t, group=self.group)
+        return out
+
+    def _d2h(self, host: torch.Tensor, src: torch.Tensor, after: torch.cuda.Event, done: torch.cuda.Event) -> None:
+        """src (device) -> host (pinned) on the copy stream behind ``after``; ``done`` after it."""
+        self.copy.wait_event(after)
+        src.record_stream(self.copy)
+        stages.memcpy_async(host.data_ptr(), src.data_ptr(), src.numel() * src.element_size(), self._hc)
+        done.record(self.copy)
 
     def submit(self, inp: SlabInputs, out: Optional[torch.Tensor] = None,
                mark: Optional[Callable[[str, Optional[torch.cuda.Event]], None]] = None) -> Optional[SlabResult]:
-        """``mark(name, event)``: stage marks m0/m1 (match), w0/w1 (warp) with an event the
-        pipeline recorded on the kernel stream at that position, r0/r1 (RANSAC) with None
-        (record one on the current stream if needed)."""
-        mark = mark or (lambda name, ev=None: None)
+        """``mark(name, event)``: stage marks m0/m1 (match + vote), w0/w1 (warp) with an event
+        the pipeline recorded on the kernel stream at that position, r0/r1 (lookup + RANSAC)
+        with None (record one on the current stream if needed)."""
+        mark = mark or _nomark
         self._wait_current()
         with torch.cuda.stream(self.stream):
             for t in (inp.frames, out):
@@ -397,93 +522,105 @@ class OverlappedSlabs:
         self._queued()
 
     def _match(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
+        """match(k) and its vote on the kernel stream; the (gathered) votes to the host."""
         self._at_tail(mark, "m0")
-        match = match_stage(inp, self.cfg)
+        match = match_stage(inp, self.cfg, stream=self._hs)
+        n_tpl = inp.des_tpl.shape[0]
+        votes = stages.consensus_vote(match.keep_bits, n_tpl, self._f0, stream=self._hs)
         self._queued()
         matched = self._at_tail(mark, "m1")
         if self._sharded():
-            from .distributed import _all_gather_rows
-
-            rank = self._rank()
-            f0 = sum(self.counts[:rank])
-            keep = _all_gather_rows(match.keep_bits, self.counts, self.group)
-            self._queued()  # the kernel stream waits for the collective
-            keep_h, keep_ready = _d2h_async(keep, self.copy, self._at_tail(mark))
-        else:
-            f0 = 0
-            keep_h, keep_ready = _d2h_async(match.keep_bits, self.copy, matched)
-        p = _SlabInFlight(inp, out, f0, match, keep_h, keep_ready)
-        p.matched = matched
-        return p
+            votes = self._gather(votes)  # the kernel stream waits for the collective
+            self._queued()
+        ready = self._at_tail(mark)
+        slot = self._slots.pop() if self._slots else _Slot()
+        self._d2h(slot.buf("votes", votes.numel(), torch.int64), votes, ready, slot.votes_ev)
+        return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=matched)
 
     def _fit(self, p: _SlabInFlight, mark) -> _SlabInFlight:
-        """The consensus (host) and RANSAC (device) of a matched slab."""
+        """The consensus merge (host) and the lookup + RANSAC (device) of a matched slab."""
         cfg = self.cfg
         n_tpl = p.inp.des_tpl.shape[0]
         n_local = p.inp.q_off.numel() - 1
         n_all = sum(self.counts) if self._sharded() else n_local
-        p.keep_ready.synchronize()
-        # the global consensus; with counts, point lists of this rank's frames only
-        p.cons = consensus_stage(p.keep_host.numpy(), n_tpl, n_all, cfg, self.logger if self._rank() == 0 else None,
-                                 frames=(p.f0, p.f0 + n_local) if self._sharded() else None)
+        p.slot.votes_ev.synchronize()
+        votes = p.slot.buf("votes", p.n_votes, torch.int64).numpy().reshape(-1, 2, n_tpl)
+        words = (n_tpl + 31) // 32
+        pack_h = p.slot.buf("pack", cfg.n_kp_global + words, torch.int32)
+        choice = choose_consensus(votes, n_tpl, n_all, cfg, self.logger if self._rank == 0 else None,
+                                  pack_out=pack_h.numpy())
+        pack_dev = torch.empty(pack_h.numel(), dtype=torch.int32, device=self.dev)
+        stages.memcpy_async(pack_dev.data_ptr(), pack_h.data_ptr(), pack_h.numel() * 4, self._hc)
+        p.slot.pack_ev.record(self.copy)
         if self.corun:
             with torch.cuda.stream(self.ana):
                 self.ana.wait_event(p.matched)
-                for t in (p.match.kp_ordered, p.inp.kp_tpl):
+                self.ana.wait_event(p.slot.pack_ev)
+                for t in (p.match.kp_ordered, p.match.keep_bits, p.inp.kp_tpl, pack_dev):
                     t.record_stream(self.ana)
-                self._fit_device(p, mark)
-                for t in vars(p.rr).values():
-                    if isinstance(t, torch.Tensor):
-                        t.record_stream(self.stream)
+                self._fit_device(p, choice, pack_dev, mark, self._ha)
+                for t in (p.rr.params, p.rr.inliers, p.rr.n_inliers, p.rr.best_trial):
+                    t.record_stream(self.stream)
                 p.fitted_ev = torch.cuda.Event()
                 p.fitted_ev.record(self.ana)
         else:
-            self._fit_device(p, mark)
+            self.stream.wait_event(p.slot.pack_ev)
+            self._fit_device(p, choice, pack_dev, mark, self._hs)
+            self._queued()
         return p
 
-    def _fit_device(self, p: _SlabInFlight, mark) -> None:
-        """RANSAC of a slab whose consensus is known, on the current stream."""
-        pt_idx = p.cons.pt_idx if p.cons.pt_idx.size else np.zeros(1, np.int32)
-        lists = tuple(_h2d_async((p.cons.pt_off, pt_idx), self.dev, self.copy))
+    def _fit_device(self, p: _SlabInFlight, choice: stages.ConsensusChoice, pack_dev: torch.Tensor, mark,
+                    hs: int) -> None:
+        """Lookup + RANSAC of a slab whose consensus is known, on the current stream (hs)."""
+        n_tpl = p.inp.des_tpl.shape[0]
         mark("r0", None)
-        if self.ransac_grid:
-            with stages.ransac_grid(self.dev, self.ransac_grid):
-                p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, lists_dev=lists)
-        else:
-            p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, lists_dev=lists)
+        p.cons = lookup_stage(p.match, n_tpl, choice, pack_dev, stream=hs)
+        p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, stream=hs, max_workgroups=self.ransac_grid)
         mark("r1", None)
         params = p.rr.params
+        after = torch.cuda.Event()
         if self._sharded():
-            from .distributed import _all_gather_rows
-
-            params = _all_gather_rows(params, self.counts, self.group)
-        if self.corun:
-            produced = None  # _d2h_async records it on the analysis stream
-        else:  # RANSAC (and the gather) went onto the kernel stream: share its new tail event
-            self._queued()
-            produced = self._at_tail(mark)
-        p.params_host, p.params_ready = _d2h_async(params, self.copy, produced)
+            bound = self._gather(stages.params_boundary(params, stream=hs))
+            p.n_bound = bound.numel()
+            after.record()
+            self._d2h(p.slot.buf("bound", bound.numel(), torch.float64), bound, after, p.slot.params_ev)
+        else:
+            after.record()
+        self._d2h(p.slot.buf("params", params.numel(), torch.float64), params, after, p.slot.params_ev)
+        if logging_enabled(self.logger):
+            _log_low_counts(self.logger, np.diff(p.cons.pt_off), self.cfg, p.f0)
 
     def _warp_device_maps(self, p: _SlabInFlight, mark) -> None:
         if p.fitted_ev is not None:
             # RANSAC(k) ran beside warp(k-1) on the analysis stream: the host waits for it
-            # (it has nothing else to do before it blocks on this step's bitmasks) instead
-            # of queueing a cross-stream wait, which leaves the device idle for tens of
+            # (it has nothing else to do before it blocks on this step's votes) instead of
+            # queueing a cross-stream wait, which leaves the device idle for tens of
             # microseconds even when RANSAC finished long before
             p.fitted_ev.synchronize()
         self._at_tail(mark, "w0")
-        p.aligned = warp_frames(p.inp.frames, p.rr.params, out=p.out)
+        p.aligned = warp_frames(p.inp.frames, p.rr.params, out=p.out, stream=self._hs)
         self._queued()
         self._at_tail(mark, "w1")
 
     def _finish(self, p: _SlabInFlight, mark) -> SlabResult:
         """Host post-processing of slab p (VA:143-145) and the warps that need its maps."""
-        p.params_ready.synchronize()  # after RANSAC(k): its parameters are on the host
-        if p.fitted_ev is not None:
-            p.fitted_ev.synchronize()
-        affines, skipped, interpolated, eu = postprocess_affines(p.params_host.numpy(), self.cfg)
+        p.slot.params_ev.synchronize()  # after RANSAC(k): its parameters are on the host
         n = p.inp.frames.shape[0]
-        local = np.asarray(affines[p.f0:p.f0 + n], dtype=np.float64)
+        shape = tuple(p.rr.params.shape)
+        params = p.slot.buf("params", p.rr.params.numel(), torch.float64).numpy().reshape(shape)
+        if self._sharded():
+            from .distributed import neighbours
+
+            E = int(np.prod(shape[1:]))
+            bounds = p.slot.buf("bound", p.n_bound, torch.float64).numpy().reshape(self._world, 2 + 2 * E)
+            prev, nxt = neighbours(bounds, self.counts, self._rank)
+            local, skipped, interpolated = _aff.fill_gaps_slab(params, p.f0, prev, nxt,
+                                                               lerp=self.cfg.ransac_model == "euclidean")
+            affines, eu = local, _aff.euclidean_transforms(local)
+        else:
+            affines, skipped, interpolated, eu = postprocess_affines(params, self.cfg)
+            local = np.asarray(affines[:n], dtype=np.float64)
+        self._slots.append(p.slot)
         if self._device_maps():
             # frames without a model were warped to zeros: warp them with the filled maps
             redo = np.zeros(n, bool)
@@ -491,24 +628,25 @@ class OverlappedSlabs:
             redo[sk[(sk >= 0) & (sk < n)]] = True
             for a, b in _runs(redo):
                 (m,) = _h2d_async((local[a:b],), self.dev, self.copy)
-                warp_frames(p.inp.frames[a:b], m, out=p.aligned[a:b])
+                warp_frames(p.inp.frames[a:b], m, out=p.aligned[a:b], stream=self._hs)
                 self._queued()
             aligned = p.aligned
         else:
             (m,) = _h2d_async((local,), self.dev, self.copy)
             self._queued()
             self._at_tail(mark, "w0")
-            aligned = warp_frames(p.inp.frames, m, out=p.out)
+            aligned = warp_frames(p.inp.frames, m, out=p.out, stream=self._hs)
             self._queued()
             self._at_tail(mark, "w1")
         done = self._at_tail(mark)
         res = SlabResult(aligned, affines, eu, skipped, interpolated, match=p.match, consensus=p.cons, ransac=p.rr)
         res.extras["done"] = done
+        res.extras["f0"] = p.f0
         return res
 
     def flush(self, mark: Optional[Callable[[str, Optional[torch.cuda.Event]], None]] = None) -> List[SlabResult]:
         """Finish every slab still in flight; their results, oldest first."""
-        mark = mark or (lambda name, ev=None: None)
+        mark = mark or _nomark
         out: List[SlabResult] = []
         with torch.cuda.stream(self.stream):
             while self._fitted is not None or self._matched is not None:
@@ -527,6 +665,10 @@ class OverlappedSlabs:
         if self.ana is not None:
             self.ana.synchronize()
         self.copy.synchronize()
+
+
+def logging_enabled(logger: Optional[logging.Logger]) -> bool:
+    return logger is not None and logger.isEnabledFor(logging.INFO)
 
 
 def _runs(mask: np.ndarray):

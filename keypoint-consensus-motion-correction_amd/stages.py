@@ -56,8 +56,19 @@ def _device_of(t: torch.Tensor) -> torch.device:
     return t.device
 
 
-def _stream(device: torch.device):
+def _stream(device: torch.device, stream: Optional[int] = None):
+    """The HIP stream of a launch: ``stream`` (a raw hipStream_t handle, as pipelines pass
+    it) or torch's current stream on ``device``."""
+    if stream is not None:
+        return _P(stream)
     return _P(torch.cuda.current_stream(device).cuda_stream)
+
+
+def memcpy_async(dst: int, src: int, nbytes: int, stream: int) -> None:
+    """hipMemcpyAsync(dst, src, nbytes, hipMemcpyDefault, stream) on raw pointers (pinned host
+    <-> device transfers of the pipelines, without torch's per-copy dispatch)."""
+    if nbytes > 0:
+        _lib.check(_lib.load().kcmc_memcpy_async(_P(dst), _P(src), ctypes.c_size_t(nbytes), _P(stream)))
 
 
 def _ctx(device: torch.device) -> _lib.Context:
@@ -130,6 +141,7 @@ def match_frames(
     d_lo: float = 0.5,
     d_hi: float = 2.0,
     norm: str = "l2",
+    stream: Optional[int] = None,
 ) -> MatchResult:
     """VA:194-214 for every frame: knn k=2 + reorder + ratio + median filters.
     uint8 descriptors (the reference's) or float32 (SIFT-style extension; its distance is
@@ -170,17 +182,40 @@ def match_frames(
     _lib.check(fn(
         _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F,
         int(nq.max()) if F else 0, float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist),
-        _ptr(res.kp_ordered), _ptr(res.keep_bits), _ptr(res.counts), _stream(dev)))
+        _ptr(res.kp_ordered), _ptr(res.keep_bits), _ptr(res.counts), _stream(dev, stream)))
     return res
 
 
 # ------------------------------------------------------------------ consensus
-@dataclass
 class Consensus:
-    order: np.ndarray    # [n] i32 template indices in Counter.most_common order
-    votes: np.ndarray    # [n] i32 vote counts
-    pt_off: np.ndarray   # [F+1] i32 CSR offsets of per-frame RANSAC point lists
-    pt_idx: np.ndarray   # [P] i32 template indices in CPython set-iteration order (VA:274)
+    """The consensus of VA:224-286: ``order`` [n] i32 template indices in Counter.most_common
+    order, ``votes`` [n] their counts, and the per-frame RANSAC point lists (VA:274) as CSR
+    ``pt_off`` [F+1] / ``pt_idx`` [P] (template indices in CPython set-iteration order).
+    The lists live on the host, on the device (``pt_off_dev`` / ``pt_idx_dev``, from the
+    device lookup), or both; the host copies are made on first access."""
+
+    def __init__(self, order: np.ndarray, votes: np.ndarray, pt_off: Optional[np.ndarray] = None,
+                 pt_idx: Optional[np.ndarray] = None, pt_off_dev: Optional[torch.Tensor] = None,
+                 pt_idx_dev: Optional[torch.Tensor] = None):
+        self.order = order
+        self.votes = votes
+        self._pt_off = pt_off
+        self._pt_idx = pt_idx
+        self.pt_off_dev = pt_off_dev
+        self.pt_idx_dev = pt_idx_dev
+
+    @property
+    def pt_off(self) -> np.ndarray:
+        if self._pt_off is None:
+            self._pt_off = self.pt_off_dev.cpu().numpy()
+        return self._pt_off
+
+    @property
+    def pt_idx(self) -> np.ndarray:
+        if self._pt_idx is None:
+            n = int(self.pt_off[-1])
+            self._pt_idx = self.pt_idx_dev[:n].cpu().numpy()
+        return self._pt_idx
 
 
 def consensus(keep_bits: np.ndarray, n_tpl: int, n_kp_global: int, n_min: int,
@@ -209,6 +244,119 @@ def consensus(keep_bits: np.ndarray, n_tpl: int, n_kp_global: int, n_min: int,
     return Consensus(cons[:n].copy(), votes[:n].copy(), pt_off, pt_idx[: pt_off[-1]].copy())
 
 
+def consensus_vote(keep_bits: torch.Tensor, n_tpl: int, frame_base: int = 0, out: Optional[torch.Tensor] = None,
+                   stream: Optional[int] = None) -> torch.Tensor:
+    """The vote part of the consensus (VA:239) on the device: [2, n_tpl] i64, row 0 the
+    Counter count of every template over these frames, row 1 its first-occurrence key
+    (frame_base + frame) << 32 | slot in that frame's CPython set table (INT64_MAX: never).
+    Ranks' votes merge by summing counts and taking the min key (consensus_merge)."""
+    dev = _device_of(keep_bits)
+    _require(keep_bits, "keep_bits", torch.int32, dev, 2)
+    if keep_bits.shape[1] != (n_tpl + 31) // 32:
+        raise ValueError("keep_bits must be [F, ceil(n_tpl/32)]")
+    if out is None:
+        out = torch.empty((2, n_tpl), dtype=torch.int64, device=dev)
+    _lib.check(_lib.load().kcmc_consensus_vote(_ctx(dev).handle, _ptr(keep_bits), keep_bits.shape[0], int(n_tpl),
+                                               int(frame_base), _ptr(out), _stream(dev, stream)))
+    return out
+
+
+def consensus_vote_host(keep_bits: np.ndarray, n_tpl: int, frame_base: int = 0) -> np.ndarray:
+    """consensus_vote of host bitmasks (native host code, same definition)."""
+    kb = np.ascontiguousarray(keep_bits).view(np.uint32)
+    if kb.ndim != 2 or kb.shape[1] != (n_tpl + 31) // 32:
+        raise ValueError("keep_bits must be [F, ceil(n_tpl/32)]")
+    out = np.empty((2, n_tpl), np.int64)
+    _lib.check(_lib.load().kcmc_consensus_vote_host(_np_ptr(kb), kb.shape[0], int(n_tpl), int(frame_base),
+                                                    _np_ptr(out)))
+    return out
+
+
+@dataclass
+class ConsensusChoice:
+    order: np.ndarray    # [nc] i32 Counter.most_common(n_kp_global) order
+    votes: np.ndarray    # [nc] i32 counts
+    pack: np.ndarray     # [>= nc + words] i32: set(consensus) iteration order, then its bitmask
+
+    @property
+    def nc(self) -> int:
+        return len(self.order)
+
+    @property
+    def cons_iter(self) -> np.ndarray:
+        return self.pack[: self.nc]
+
+
+def consensus_merge(votes: np.ndarray, n_tpl: int, n_kp_global: int, n_min: int,
+                    pack_out: Optional[np.ndarray] = None) -> ConsensusChoice:
+    """Merge the votes of one or more ranks ([world, 2, n_tpl] or [2, n_tpl] i64):
+    Counter.most_common(n_kp_global) (VA:240) + set(consensus) order (VA:248).  Raises
+    VideoAligner.AlignmentError when fewer than n_min templates were voted (VA:241-244)."""
+    v = np.ascontiguousarray(votes, dtype=np.int64)
+    world = v.size // (2 * n_tpl) if n_tpl else 1
+    if n_tpl and v.size != world * 2 * n_tpl:
+        raise ValueError("votes must be [world, 2, n_tpl]")
+    n_kp_global = int(n_kp_global)
+    words = (n_tpl + 31) // 32
+    order = np.zeros(max(n_kp_global, 1), np.int32)
+    counts = np.zeros(max(n_kp_global, 1), np.int32)
+    if pack_out is None:
+        pack_out = np.zeros(n_kp_global + words, np.int32)
+    elif pack_out.dtype != np.int32 or pack_out.size < n_kp_global + words or not pack_out.flags.c_contiguous:
+        raise ValueError("pack_out must be a contiguous int32 array of >= n_kp_global + ceil(n_tpl/32) entries")
+    n_c = ctypes.c_int(0)
+    _lib.check(_lib.load().kcmc_consensus_merge(_np_ptr(v), int(world), int(n_tpl), n_kp_global, int(n_min),
+                                                _np_ptr(order), _np_ptr(counts), ctypes.byref(n_c), _np_ptr(pack_out)))
+    n = n_c.value
+    return ConsensusChoice(order[:n].copy(), counts[:n].copy(), pack_out)
+
+
+def consensus_lookup(keep_bits: torch.Tensor, n_tpl: int, pack_dev: torch.Tensor, nc: int,
+                     stream: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The lookup part of the consensus (VA:274) on the device: every frame's
+    list(consensus & frame_set) as CSR (pt_off [F+1], pt_idx [F*nc]) for RANSAC.
+    pack_dev = ConsensusChoice.pack on the device."""
+    dev = _device_of(keep_bits)
+    _require(keep_bits, "keep_bits", torch.int32, dev, 2)
+    _require(pack_dev, "pack_dev", torch.int32, dev, 1)
+    F = keep_bits.shape[0]
+    if keep_bits.shape[1] != (n_tpl + 31) // 32 or pack_dev.numel() < nc + keep_bits.shape[1] or not 0 <= nc <= n_tpl:
+        raise ValueError("consensus_lookup: inconsistent shapes")
+    L = _lib.load()
+    pt_off = torch.empty(F + 1, dtype=torch.int32, device=dev)
+    pt_idx = torch.empty(max(F * nc, 1), dtype=torch.int32, device=dev)
+    scratch = torch.empty(max(int(L.kcmc_consensus_lookup_scratch_bytes(F, nc)), 4), dtype=torch.uint8, device=dev)
+    _lib.check(L.kcmc_consensus_lookup(_ctx(dev).handle, _ptr(keep_bits), F, int(n_tpl), _ptr(pack_dev), int(nc),
+                                       _ptr(pt_off), _ptr(pt_idx), _ptr(scratch), _stream(dev, stream)))
+    return pt_off, pt_idx
+
+
+def consensus_lookup_host(keep_bits: np.ndarray, n_tpl: int, cons_iter: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """consensus_lookup of host bitmasks (native host code)."""
+    kb = np.ascontiguousarray(keep_bits).view(np.uint32)
+    ci = np.ascontiguousarray(cons_iter, dtype=np.int32)
+    F, nc = kb.shape[0], ci.size
+    pt_off = np.zeros(F + 1, np.int32)
+    pt_idx = np.zeros(max(F * nc, 1), np.int32)
+    _lib.check(_lib.load().kcmc_consensus_lookup_host(_np_ptr(kb), F, int(n_tpl), _np_ptr(ci), nc, _np_ptr(pt_off),
+                                                      _np_ptr(pt_idx)))
+    return pt_off, pt_idx[: pt_off[-1]].copy()
+
+
+def params_boundary(params: torch.Tensor, out: Optional[torch.Tensor] = None,
+                    stream: Optional[int] = None) -> torch.Tensor:
+    """[2 + 2E] f64: the first and last frame of params [F, ...] without NaN (-1: none) and
+    their parameters -- what the neighbouring ranks need for NaN-gap filling (VA:347-407)."""
+    dev = _device_of(params)
+    _require(params, "params", torch.float64, dev)
+    F = params.shape[0]
+    E = int(params[0].numel()) if F else int(np.prod(params.shape[1:]))
+    if out is None:
+        out = torch.empty(2 + 2 * E, dtype=torch.float64, device=dev)
+    _lib.check(_lib.load().kcmc_params_boundary(_ctx(dev).handle, _ptr(params), F, E, _ptr(out), _stream(dev, stream)))
+    return out
+
+
 def hypothesis_table(n: int, trials: int = 1000, seed: int = 42, min_samples: int = 2) -> np.ndarray:
     """The per-trial samples skimage 0.18.3's ransac draws (legacy MT19937)."""
     out = np.empty((trials, min_samples), np.int32)
@@ -231,14 +379,19 @@ def ransac_grid(device, max_workgroups: int):
     """RANSAC scoring launches on ``device`` inside the block use at most
     ``max_workgroups`` workgroups, each scoring frames g, g + max_workgroups, ... (C ABI
     kcmc_set_ransac_grid; 0 = one per frame, the default).  Results are identical; a narrow
-    grid keeps RANSAC on a few CU slots when it shares the device with the warp."""
+    grid keeps RANSAC on a few CU slots when it shares the device with the warp.  The value
+    in force before the block is restored after it.  The pipelines pass their grid per call
+    (ransac_lists(max_workgroups=...)), which other callers of the context cannot change."""
     ctx = _ctx(torch.device(device))
     L = _lib.load()
+    prev = ctx.ransac_grid
     _lib.check(L.kcmc_set_ransac_grid(ctx.handle, int(max_workgroups)))
+    ctx.ransac_grid = int(max_workgroups)
     try:
         yield
     finally:
-        _lib.check(L.kcmc_set_ransac_grid(ctx.handle, 0))
+        _lib.check(L.kcmc_set_ransac_grid(ctx.handle, prev))
+        ctx.ransac_grid = prev
 
 
 def ransac_rigid(
@@ -356,9 +509,67 @@ def ransac_model(
     return res
 
 
+_PREPARED_RANGES = set()
+
+
+def ransac_prepare_range(device, model: str, n_lo: int, n_hi: int, trials: int = 1000, seed: int = 42) -> None:
+    """Upload the hypothesis tables of every point count in [n_lo, n_hi] once (the device
+    lookup's point counts are not seen by the host; every count a frame can have is ready)."""
+    dev = torch.device(device)
+    ctx = _ctx(dev)
+    ms = _lib.MODEL_MIN_SAMPLES[model]
+    n_lo = max(int(n_lo), ms + 1, 3)
+    key = (id(ctx), ms, n_lo, int(n_hi), int(trials), int(seed) & 0xFFFFFFFF)
+    if key in _PREPARED_RANGES or n_hi < n_lo:
+        return
+    n_run = np.arange(n_lo, int(n_hi) + 1, dtype=np.int32)
+    L = _lib.load()
+    if ms == 2:
+        _lib.check(L.kcmc_ransac_prepare(ctx.handle, _np_ptr(n_run), int(n_run.size), int(trials), key[-1]))
+    else:
+        _lib.check(L.kcmc_ransac_prepare_samples(ctx.handle, ms, _np_ptr(n_run), int(n_run.size), int(trials), key[-1]))
+    _PREPARED_RANGES.add(key)
+
+
+def ransac_lists(model: str, src: torch.Tensor, dst: torch.Tensor, pt_off: torch.Tensor, pt_idx: torch.Tensor,
+                 src_frame_stride: int, max_n: int, trials: int = 1000, residual_threshold: float = 2.0,
+                 spatial_rate: float = 1.0, n_skip: int = 3, stream: Optional[int] = None,
+                 max_workgroups: int = 0) -> RansacResult:
+    """RANSAC of every frame on device point lists whose sizes the host does not know
+    (the device consensus lookup): max_n bounds every frame's point count (n_kp_global) and
+    the tables of every count in [n_skip, max_n] must be ready (ransac_prepare_range).
+    params [F, 2, 3] (euclidean) or [F, 3, 3] (affine / projective), as ransac_rigid /
+    ransac_model."""
+    dev = _device_of(src)
+    F = pt_off.numel() - 1
+    P = pt_idx.numel()
+    res = RansacResult(
+        params=torch.empty((F, 2, 3) if model == "euclidean" else (F, 3, 3), dtype=torch.float64, device=dev),
+        inliers=torch.empty((max(P, 1),), dtype=torch.uint8, device=dev),
+        n_inliers=torch.empty((F,), dtype=torch.int32, device=dev),
+        best_trial=torch.empty((F,), dtype=torch.int32, device=dev),
+    )
+    if F == 0:
+        return res
+    L = _lib.load()
+    ctx = _ctx(dev).handle
+    st = _stream(dev, stream)
+    if model == "euclidean":
+        _lib.check(L.kcmc_ransac_rigid_grid(
+            ctx, _ptr(src), _ptr(dst), _ptr(pt_idx), _ptr(pt_off), int(src_frame_stride), F, int(max_n), int(trials),
+            float(residual_threshold), float(spatial_rate), int(n_skip), _ptr(res.params), _ptr(res.inliers),
+            _ptr(res.n_inliers), _ptr(res.best_trial), int(max_workgroups), st))
+    else:
+        _lib.check(L.kcmc_ransac_model_grid(
+            ctx, _lib.MODEL_IDS[model], _ptr(src), _ptr(dst), _ptr(pt_idx), _ptr(pt_off), int(src_frame_stride), F,
+            int(max_n), int(trials), float(residual_threshold), float(spatial_rate), int(n_skip), _ptr(res.params),
+            _ptr(res.inliers), _ptr(res.n_inliers), _ptr(res.best_trial), int(max_workgroups), st))
+    return res
+
+
 # ----------------------------------------------------------------------- K3
 def warp_affine_u16(frames: torch.Tensor, affines: torch.Tensor, out: Optional[torch.Tensor] = None,
-                    inverse_map: bool = False) -> torch.Tensor:
+                    inverse_map: bool = False, stream: Optional[int] = None) -> torch.Tensor:
     """cv2.warpAffine(frame, M, (W, H), INTER_LINEAR) for every frame (VA:458).
 
     frames [F, H, W] or [F, H, W, C] uint16 on the device; affines [F, 2, 3] f64.
@@ -382,12 +593,12 @@ def warp_affine_u16(frames: torch.Tensor, affines: torch.Tensor, out: Optional[t
             raise ValueError("out must have the shape of frames")
     L = _lib.load()
     _lib.check(L.kcmc_warp_affine_u16(_ctx(dev).handle, _ptr(frames), _ptr(out), _ptr(affines), F, H, W, C,
-                                      int(bool(inverse_map)), _stream(dev)))
+                                      int(bool(inverse_map)), _stream(dev, stream)))
     return out
 
 
 def warp_perspective_u16(frames: torch.Tensor, homographies: torch.Tensor, out: Optional[torch.Tensor] = None,
-                         inverse_map: bool = False) -> torch.Tensor:
+                         inverse_map: bool = False, stream: Optional[int] = None) -> torch.Tensor:
     """cv2.warpPerspective(frame, H, (W, H), INTER_LINEAR) for every frame (the warp of
     the homography extension).  frames [F, H, W] or [F, H, W, C] uint16; homographies
     [F, 3, 3] f64 (forward maps, frame -> template, as RANSAC returns them)."""
@@ -410,7 +621,7 @@ def warp_perspective_u16(frames: torch.Tensor, homographies: torch.Tensor, out: 
             raise ValueError("out must have the shape of frames")
     L = _lib.load()
     _lib.check(L.kcmc_warp_perspective_u16(_ctx(dev).handle, _ptr(frames), _ptr(out), _ptr(homographies), F, H, W, C,
-                                           int(bool(inverse_map)), _stream(dev)))
+                                           int(bool(inverse_map)), _stream(dev, stream)))
     return out
 
 

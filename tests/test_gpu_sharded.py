@@ -3,8 +3,10 @@ as fresh child processes) run `distributed.align_sharded` with the HIP stages an
 pipelined `OverlappedSlabs(counts=...)` on uneven slabs, with the template broadcast
 from rank 0 (VA:117-123 / VA:460-465 pickle it to every worker).  The concatenated
 per-rank results must be bit-identical to one single-device `align_slab` over all
-frames: the survivor-bitmask and affine all-gathers and the per-rank consensus slice
-(VA:224-286) may not change a single pixel.
+frames: the vote all-gather + per-rank device lookup (VA:224-286) and the slab-boundary
+all-gather + per-rank gap filling (VA:347-407) may not change a single pixel.  In the
+"blind" case rank 1's frames carry random descriptors, so none of them gets a model and
+the NaN gap spans rank 1's whole slab (filled from rank 0's last and rank 2's first model).
 
 The ranks are separate interpreters (this file run as a script), launched before this
 process touches the GPU in the test body."""
@@ -23,14 +25,16 @@ if REPO not in sys.path:
 
 from kcmc_amd import pipeline, synthetic  # noqa: E402
 
-WORLD = 2
-COUNTS = (9, 14)            # uneven slabs (frames per rank)
+COUNTS = {2: (9, 14), 3: (9, 7, 11)}  # uneven slabs (frames per rank)
 N_TPL, D, HW = 160, 32, (120, 200)
 N_KP_GLOBAL = 40
 
 
-def _keypoints(rank: int, slab: int, model: str):
-    return synthetic.make_keypoints(COUNTS[rank], N_TPL, D, HW, seed=17, frame_seed=100 * slab + rank, model=model)
+def _keypoints(rank: int, slab: int, model: str, world: int = 2, blind: bool = False):
+    ks = synthetic.make_keypoints(COUNTS[world][rank], N_TPL, D, HW, seed=17, frame_seed=100 * slab + rank, model=model)
+    if blind and rank == 1:  # descriptors unrelated to the template: no frame of this rank gets a model
+        ks.des_q[:] = np.random.default_rng(99 + slab).integers(0, 256, ks.des_q.shape, dtype=np.uint8)
+    return ks
 
 
 def _frames(n: int):
@@ -52,17 +56,17 @@ def _inputs(ks_list, dev):
                                t(q_off), q_off)
 
 
-def _rank_main(rank: int, port: int, out_dir: str, model: str, depth: int) -> None:
+def _rank_main(rank: int, port: int, out_dir: str, model: str, depth: int, world: int, blind: bool) -> None:
     import torch.distributed as dist
 
     from kcmc_amd import distributed as kdist
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     cfg = pipeline.AlignConfig(n_kp_global=N_KP_GLOBAL, ransac_model=model)
-    slabs = [_inputs([_keypoints(rank, s, model)], dev) for s in range(3)]
+    slabs = [_inputs([_keypoints(rank, s, model, world, blind)], dev) for s in range(3)]
     for inp in slabs:
         if rank != 0:  # only rank 0 holds the template; the others receive it
             inp.des_tpl.zero_()
@@ -75,8 +79,9 @@ def _rank_main(rank: int, port: int, out_dir: str, model: str, depth: int) -> No
     out["sharded_aligned"] = res.aligned.cpu().numpy()
     out["sharded_affines"] = res.affines
     out["sharded_skipped"] = np.asarray(res.skipped, np.int64)
+    out["sharded_interpolated"] = np.asarray(res.interpolated, np.int64)
     # 2. the pipelined schedule with the two exchanges, `depth` slabs in flight
-    ov = pipeline.OverlappedSlabs(dev, cfg, counts=list(COUNTS), depth=depth)
+    ov = pipeline.OverlappedSlabs(dev, cfg, counts=list(COUNTS[world]), depth=depth)
     r = [ov.submit(s) for s in slabs]
     rest = ov.flush()
     ov.synchronize()
@@ -84,6 +89,7 @@ def _rank_main(rank: int, port: int, out_dir: str, model: str, depth: int) -> No
     for k, r in enumerate(r[depth - 1:] + rest):
         out[f"ov{k}_aligned"] = r.aligned.cpu().numpy()
         out[f"ov{k}_affines"] = r.affines
+        out[f"ov{k}_skipped"] = np.asarray(r.skipped, np.int64)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out)
     dist.destroy_process_group()
 
@@ -100,33 +106,44 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("model,depth", [("euclidean", 2), ("affine", 3)])
-def test_sharded_hip_path_equals_single_device(tmp_path, model, depth):
+@pytest.mark.parametrize("model,depth,world,blind", [("euclidean", 2, 2, False), ("affine", 3, 2, False),
+                                                     ("euclidean", 2, 3, True)])
+def test_sharded_hip_path_equals_single_device(tmp_path, model, depth, world, blind):
     port = _free_port()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), str(r), str(port), str(tmp_path), model, str(depth)],
-                              env=env, cwd=REPO) for r in range(WORLD)]
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), str(r), str(port), str(tmp_path), model,
+                               str(depth), str(world), str(int(blind))], env=env, cwd=REPO) for r in range(world)]
     try:
         rcs = [p.wait(timeout=200) for p in procs]
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    assert rcs == [0] * WORLD, rcs
-    got = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(WORLD)]
+    assert rcs == [0] * world, rcs
+    got = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(world)]
+    counts = COUNTS[world]
+    starts = np.concatenate(([0], np.cumsum(counts)))
 
     dev = torch.device("cuda", 0)
     cfg = pipeline.AlignConfig(n_kp_global=N_KP_GLOBAL, ransac_model=model)
     for s, tag in ((0, "sharded"), (0, "ov0"), (1, "ov1"), (2, "ov2")):
-        ref = pipeline.align_slab(_inputs([_keypoints(r, s, model) for r in range(WORLD)], dev), cfg)
-        assert len(ref.skipped) < sum(COUNTS) // 2
+        ref = pipeline.align_slab(_inputs([_keypoints(r, s, model, world, blind) for r in range(world)], dev), cfg)
+        if blind:  # the premise: rank 1's whole slab has no model, the gap crosses both boundaries
+            assert set(range(starts[1], starts[2])) <= set(ref.skipped)
+            assert set(range(starts[1], starts[2])) <= set(ref.interpolated)
+        else:
+            assert len(ref.skipped) < sum(counts) // 2
         aligned = ref.aligned.cpu().numpy()
-        for r in range(WORLD):
-            np.testing.assert_array_equal(got[r][f"{tag}_affines"], ref.affines)
-        np.testing.assert_array_equal(np.concatenate([got[r][f"{tag}_aligned"] for r in range(WORLD)]), aligned)
+        for r in range(world):
+            np.testing.assert_array_equal(got[r][f"{tag}_affines"], ref.affines[starts[r]:starts[r + 1]])
+        np.testing.assert_array_equal(np.concatenate([got[r][f"{tag}_aligned"] for r in range(world)]), aligned)
         if tag == "sharded":
-            assert got[0]["sharded_skipped"].tolist() == ref.skipped
+            assert np.concatenate([got[r]["sharded_skipped"] for r in range(world)]).tolist() == ref.skipped
+            assert np.concatenate([got[r]["sharded_interpolated"] for r in range(world)]).tolist() == ref.interpolated
+        else:
+            assert np.concatenate([got[r][f"{tag}_skipped"] for r in range(world)]).tolist() == ref.skipped
 
 
 if __name__ == "__main__":
-    _rank_main(int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5]))
+    _rank_main(int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5]), int(sys.argv[6]),
+               bool(int(sys.argv[7])))

@@ -249,3 +249,113 @@ def test_max_scale_lut_matches_reference_expression():
     for k in range(int(g["n_cases"])):
         imgs, b = g[f"p{k}_images"], float(g[f"p{k}_brightest"])
         assert np.array_equal(max_scale_lut(b)[imgs], g[f"p{k}_u8"])
+
+
+# ------------------------------------------------------------ consensus in three parts
+def _split_consensus(kb, n_tpl, n_kp_global, n_min, cuts):
+    """vote per frame range ("rank"), merge, lookup per range: the sharded consensus."""
+    votes = np.stack([stages.consensus_vote_host(kb[a:b], n_tpl, a) for a, b in zip(cuts, cuts[1:])])
+    rng = np.random.default_rng(len(cuts))
+    choice = stages.consensus_merge(votes[rng.permutation(len(votes))], n_tpl, n_kp_global, n_min)
+    offs, idxs = [0], []
+    for a, b in zip(cuts, cuts[1:]):
+        po, pi = stages.consensus_lookup_host(kb[a:b], n_tpl, choice.cons_iter)
+        offs.extend((offs[-1] + po[1:]).tolist())
+        idxs.append(pi)
+    return choice, np.asarray(offs, np.int32), np.concatenate(idxs) if idxs else np.zeros(0, np.int32)
+
+
+def test_three_part_consensus_equals_cpython_and_full():
+    """vote (per frame range) -> merge (ranks in any order) -> lookup (per frame range) gives
+    CPython's Counter.most_common order, counts and every frame's set-order point list --
+    the same as the one-shot native consensus."""
+    rng = np.random.default_rng(21)
+    for case in range(40):
+        n_tpl = int(rng.choice([8, 33, 100, 500, 1000, 4096]))
+        F = int(rng.integers(1, 40))
+        p = rng.uniform(0.0, 0.9, n_tpl) * rng.uniform(0.05, 1.0)
+        sets = [set(np.flatnonzero(rng.random(n_tpl) < p).tolist()) for _ in range(F)]
+        n_kp_global = int(rng.choice([1, 5, 10, 50, 100, 500]))
+        kb = _bits(sets, n_tpl)
+        cuts = sorted({0, F, *rng.integers(0, F + 1, int(rng.integers(0, 4))).tolist()})
+        try:
+            cons_set, order, votes = oracle.consensus(sets, n_kp_global, 1)
+        except RuntimeError:
+            continue
+        choice, po, pi = _split_consensus(kb, n_tpl, n_kp_global, 1, cuts)
+        assert choice.order.tolist() == list(order) and choice.votes.tolist() == list(votes)
+        assert choice.cons_iter.tolist() == list(cons_set)
+        lists = oracle.lookup(cons_set, sets)
+        for f, L in enumerate(lists):
+            assert pi[po[f]:po[f + 1]].tolist() == L
+        full = stages.consensus(kb, n_tpl, n_kp_global, 1)
+        assert np.array_equal(full.pt_off, po) and np.array_equal(full.pt_idx, pi)
+
+
+def test_consensus_vote_first_occurrence_keys():
+    """The vote's key row: (frame << 32) | slot of the template in the first frame's set
+    table (iteration position), INT64_MAX for templates no frame holds."""
+    sets = [set(), {5, 3, 900}, {3, 7}, {1000 % 1001}]
+    kb = _bits(sets, 1001)
+    v = stages.consensus_vote_host(kb, 1001, frame_base=10)
+    assert v[0, 3] == 2 and v[0, 7] == 1 and v[0, 999] == 0
+    assert v[1, 999] == np.iinfo(np.int64).max
+    assert v[1, 3] >> 32 == 11 and v[1, 7] >> 32 == 12 and v[1, 1000] >> 32 == 13
+    it = list({5, 3, 900})  # CPython's iteration order of frame 1's set
+    slots = sorted((v[1, k] & 0xFFFFFFFF, k) for k in (3, 5, 900))
+    assert [k for _, k in slots] == it
+
+
+def test_consensus_merge_too_few_raises_and_bad_votes():
+    v = stages.consensus_vote_host(_bits([{1, 2}, {2, 3}], 10), 10)
+    with pytest.raises(VideoAligner.AlignmentError):
+        stages.consensus_merge(v, 10, 10, 5)
+    bad = v.copy()
+    bad[1, 2] = np.iinfo(np.int64).max  # a voted template without a first occurrence
+    with pytest.raises(ValueError):
+        stages.consensus_merge(bad, 10, 10, 1)
+
+
+# ------------------------------------------------------------ sharded gap filling
+@pytest.mark.parametrize("lerp", [True, False])
+def test_fill_gaps_slab_equals_global_interpolation(lerp):
+    """affines.fill_gaps_slab on every rank's slab with only its two neighbouring models ==
+    the rows of the global interpolate_affines / interpolate_linear, incl. gaps that span
+    whole ranks and leading / trailing gaps."""
+    from kcmc_amd import distributed as kdist
+
+    rng = np.random.default_rng(4 if lerp else 5)
+    for case in range(60):
+        n = int(rng.integers(2, 40))
+        t = rng.normal(0, 0.05, n)
+        a = np.stack([np.array([[np.cos(x), -np.sin(x), rng.normal()], [np.sin(x), np.cos(x), rng.normal()]]) for x in t])
+        miss = rng.random(n) < rng.choice([0.1, 0.5, 0.9])
+        if case % 7 == 0:
+            miss[: n // 2] = True
+        if miss.all():
+            miss[int(rng.integers(0, n))] = False
+        a[miss] = np.nan
+        ref, ref_it = (affines.interpolate_affines if lerp else affines.interpolate_linear)(a)
+        ref_sk = np.flatnonzero(miss).tolist()
+        cuts = sorted({0, n, *rng.integers(0, n + 1, int(rng.integers(0, 5))).tolist()})
+        counts = [b - c for c, b in zip(cuts, cuts[1:])]
+        bounds = []
+        for c, b in zip(cuts, cuts[1:]):
+            ok = np.flatnonzero(~miss[c:b])
+            row = np.full(14, np.nan)
+            row[:2] = (ok[0], ok[-1]) if ok.size else (-1, -1)
+            if ok.size:
+                row[2:8], row[8:] = a[c + ok[0]].ravel(), a[c + ok[-1]].ravel()
+            bounds.append(row)
+        bounds = np.stack(bounds)
+        got, sk, it = [], [], []
+        for r, (c, b) in enumerate(zip(cuts, cuts[1:])):
+            prev, nxt = kdist.neighbours(bounds, counts, r)
+            m, s, i = affines.fill_gaps_slab(a[c:b], c, prev, nxt, lerp)
+            got.append(m)
+            sk += s
+            it += i
+        np.testing.assert_array_equal(np.concatenate(got), ref)
+        assert sk == ref_sk and it == ref_it
+    with pytest.raises(VideoAligner.AlignmentError):
+        affines.fill_gaps_slab(np.full((3, 2, 3), np.nan), 4, None, None, True)
