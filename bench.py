@@ -265,6 +265,17 @@ def cpu_baseline(bc: BenchConfig, ks, n_sample: int, procs: int):
             pool.close()
             pool.join()
     total = t3 - t0
+    calib = ""
+    try:  # the port against the reference's own code, measured in the build container
+        with open(os.path.join(REPO, "profiles", "r03_cpu_reference_calibration.json")) as f:
+            c = json.load(f)
+        calib = (f"; calibration (profiles/r03_cpu_reference_calibration.json, {c['host']}): the port's RANSAC "
+                 f"runs at {c['port_speed_over_reference']}x the speed of the reference's own "
+                 f"_parallelize(_compute_euclidean_affine) with scikit-image 0.18.3 on the same {c['procs']} cores "
+                 f"({c['port']['ms_per_frame_per_core']} vs {c['reference']['ms_per_frame_per_core']} ms/frame/core, "
+                 f"N = 90, identical parameters)")
+    except (OSError, ValueError, KeyError):
+        pass
     return {
         "value": n_sample / total,
         "unit": "aligned frames/s",
@@ -275,7 +286,7 @@ def cpu_baseline(bc: BenchConfig, ks, n_sample: int, procs: int):
                    f"like the reference's joblib pool: match {1e3 * (t1 - t0):.0f} ms "
                    f"(C oracle knnMatch + reference numpy filters), consensus {1e3 * (t2 - t1):.1f} ms "
                    f"(CPython set/Counter, parent), RANSAC + warp {1e3 * (t3 - t2):.0f} ms "
-                   f"(numpy/LAPACK restatement of skimage 0.18.3 with 1000 trials; C warp)"),
+                   f"(numpy/LAPACK restatement of skimage 0.18.3 with 1000 trials; C warp)" + calib),
         "seconds": total,
     }
 

@@ -136,6 +136,11 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         if _lib is not None:
             return _lib
         path = lib_path()
+        if os.environ.get("KCMC_LIB_PATH"):
+            import warnings
+
+            warnings.warn(f"KCMC_LIB_PATH set: loading {path} (an A/B build; no auto-build, entry points it lacks "
+                          "stay unbound and fail when called)", RuntimeWarning, stacklevel=2)
         if auto_build and os.environ.get("KCMC_NO_BUILD", "0") != "1" and not os.environ.get("KCMC_LIB_PATH"):
             try:
                 if not _build.up_to_date():

@@ -114,10 +114,9 @@ struct DevPySet {
 
 constexpr int kVoteChunk = 64;    // frames per vote_count_kernel thread
 constexpr int kVoteThreads = 256;
-constexpr int kKeyThreads = 1024;
+constexpr int kKeyThreads = 256;
 constexpr int kEmuLanes = 64;     // vote_key_kernel replays of non-ascending first frames
-constexpr int kScanThreads = 1024;
-constexpr int kCountThreads = 256;
+constexpr int kCountThreads = 64;
 constexpr uint32_t kOrderLdsCap = 2048;  // lookup_order_kernel keeps result tables up to this size in LDS
 
 // cnt[t] += frames of the chunk holding t; first_enc[t] = max(0x7fffffff - first frame):
@@ -228,31 +227,23 @@ __global__ __launch_bounds__(kCountThreads) void lookup_count_kernel(const uint3
   pt_off[f + 1] = m;
 }
 
-// In-place inclusive scan of pt_off[1..F] (one workgroup), pt_off[0] = 0: CSR offsets.
-__global__ __launch_bounds__(kScanThreads) void lookup_scan_kernel(int F, int32_t* __restrict__ pt_off) {
-  __shared__ int32_t wsum[kScanThreads / 64];
-  __shared__ int32_t carry;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (threadIdx.x == 0) {
-    carry = 0;
-    pt_off[0] = 0;
-  }
-  __syncthreads();
-  for (int base = 0; base < F; base += kScanThreads) {
-    const int f = base + threadIdx.x;
+// In-place inclusive scan of pt_off[1..F], pt_off[0] = 0: CSR offsets.  ONE wave: the
+// lookup runs beside the warp, whose tiles fill every CU; a single-wave workgroup gets a
+// slot as soon as one tile retires, a 1024-thread one waited ~0.43 ms for 16 free slots on
+// one CU (c3 trace).
+__global__ __launch_bounds__(64) void lookup_scan_kernel(int F, int32_t* __restrict__ pt_off) {
+  const int lane = threadIdx.x;
+  if (lane == 0) pt_off[0] = 0;
+  int carry = 0;
+  for (int base = 0; base < F; base += 64) {
+    const int f = base + lane;
     int x = f < F ? pt_off[f + 1] : 0;
     for (int d = 1; d < 64; d <<= 1) {
       const int y = __shfl_up(x, d, 64);
       if (lane >= d) x += y;
     }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    int before = carry;
-    for (int v = 0; v < wave; ++v) before += wsum[v];
-    if (f < F) pt_off[f + 1] = before + x;
-    __syncthreads();
-    if (threadIdx.x == kScanThreads - 1) carry = before + x;
-    __syncthreads();
+    if (f < F) pt_off[f + 1] = carry + x;
+    carry += __shfl(x, 63, 64);
   }
 }
 
@@ -448,7 +439,7 @@ extern "C" int kcmc_consensus_lookup(kcmc_ctx* ctx, const uint32_t* keep_bits, i
   hipLaunchKernelGGL(lookup_count_kernel, dim3(ceil_div(n_frames, kCountThreads)), dim3(kCountThreads), 0, s, keep_bits,
                      n_frames, W, cons_bits, out_pt_off);
   KCMC_TRY(launch_check("lookup_count_kernel"));
-  hipLaunchKernelGGL(lookup_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, n_frames, out_pt_off);
+  hipLaunchKernelGGL(lookup_scan_kernel, dim3(1), dim3(64), 0, s, n_frames, out_pt_off);
   KCMC_TRY(launch_check("lookup_scan_kernel"));
   const uint32_t cap = pyset_table_size((uint32_t)nc);
   const size_t lds = cap <= kOrderLdsCap ? (size_t)2 * cap * sizeof(int32_t) : 0;

@@ -66,6 +66,9 @@ int launch_check(const char* what);
 
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
+// CU count of the calling thread's current HIP device (cached per device id; match.hip).
+int device_cus();
+
 // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (speed only, never
 // relied on for correctness), so give each XCD a contiguous run of ids (bijective also
 // when n % 8 != 0): neighbouring tiles that share input then share one XCD's L2.

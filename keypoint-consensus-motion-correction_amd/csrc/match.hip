@@ -34,9 +34,26 @@
 #include <cfloat>
 #include <climits>
 
+#include <atomic>
+
 #include "kcmc_internal.h"
 
 namespace kcmc {
+
+// CU count of the calling thread's current device, cached per device id.
+int device_cus() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  int cus = cache[dev].load(std::memory_order_relaxed);
+  if (cus <= 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cache[dev].store(cus, std::memory_order_relaxed);
+  }
+  return cus;
+}
+
 namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -51,7 +68,12 @@ struct KnnShape {
 constexpr int kQChunk = 256;                              // frame descriptors per LDS chunk (8-bit local index)
 constexpr uint32_t kNoKey = 0xffffffffu;                  // chunk keys of real rows are < 2^31
 constexpr uint32_t kPad = 0xc0000000u;                    // key of the padding rows of a tile (acc = 0)
-constexpr int kBias = 1 << 20;                            // B > max T = 16129 * 64
+// Bias of the frame-row term: B = 2^20 = max T (T = sum (x + 1)^2 over D <= 64 bytes with
+// x = a - 128 in [-128, 127]: 64 * 128^2).  The biased keys stay >= 0 only because the SSD
+// they encode is >= 0; the asserts keep every real key below the padding key.
+constexpr int kBias = 1 << 20;
+static_assert(64 * 128 * 128 <= kBias, "kBias must cover the largest template term T");
+static_assert(((64ull * 255 * 255) << 8 | 0xffull) < kPad, "real keys (SSD << 8 | row) must stay below kPad");
 constexpr unsigned long long kNoKey64 = ~0ull;
 
 __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
@@ -437,15 +459,7 @@ __global__ __launch_bounds__(kFilterThreads) void match_filter_kernel(
 
 // Workgroups that fill the device once (2 per CU at 8 waves, 4 at 4 waves: the kernels'
 // ~100 VGPRs allow 4 waves per SIMD), split evenly over the template groups.
-int device_cus() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
-  return cus;
-}
+
 
 // persistent grid: n_tg template groups x G frame strides, G = the resident workgroups
 // per template group (workgroups never wait on each other, so a wrong residency count

@@ -166,12 +166,7 @@ int check_hamming_args(const void* des_tpl, int n_tpl, int D, const void* des_q,
 int launch_knn_hamming(const uint8_t* des_tpl, int n_tpl, int D, const uint8_t* des_q, const int32_t* q_off,
                        int n_frames, int32_t* out_idx, float* out_dist, hipStream_t s) {
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
+  const int cus = device_cus();
   const int n_tg = ceil_div(n_tpl, kThreads);
   // workgroups per CU: LDS-bound (2 x 256 rows x 32 / 64 B per workgroup)
   const int G = std::max(1, std::min(n_frames, (D <= 32 ? 8 : 4) * cus / n_tg));

@@ -10,6 +10,7 @@ PCIe.
 from __future__ import annotations
 
 import logging
+import time
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Tuple
 
@@ -440,6 +441,9 @@ class OverlappedSlabs:
             self._f0 = sum(counts[: self._rank])
             self._nccl = dist.get_backend(group) == "nccl"
         self._slots: List[_Slot] = []
+        # host seconds spent blocked in event waits / inside the all-gathers (the rest of a
+        # submit is the host's own work; tools/host_scaling.py)
+        self.stats = {"wait_s": 0.0, "gather_s": 0.0, "merge_s": 0.0, "post_s": 0.0}
         self._matched: Optional[_SlabInFlight] = None  # match queued, consensus pending
         self._fitted: Optional[_SlabInFlight] = None   # RANSAC queued, warp pending
         self._tail: Optional[torch.cuda.Event] = None   # an event at the kernel stream's tail
@@ -470,12 +474,19 @@ class OverlappedSlabs:
         [world, *t.shape]."""
         import torch.distributed as dist
 
+        t0 = time.perf_counter()
         out = torch.empty((self._world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         if self._nccl:
             dist.all_gather_into_tensor(out, t, group=self.group)
         else:
             dist.all_gather(list(out.unbind(0)), t, group=self.group)
+        self.stats["gather_s"] += time.perf_counter() - t0
         return out
+
+    def _wait(self, ev: torch.cuda.Event) -> None:
+        t0 = time.perf_counter()
+        ev.synchronize()
+        self.stats["wait_s"] += time.perf_counter() - t0
 
     def _d2h(self, host: torch.Tensor, src: torch.Tensor, after: torch.cuda.Event, done: torch.cuda.Event) -> None:
         """src (device) -> host (pinned) on the copy stream behind ``after``; ``done`` after it."""
@@ -543,12 +554,14 @@ class OverlappedSlabs:
         n_tpl = p.inp.des_tpl.shape[0]
         n_local = p.inp.q_off.numel() - 1
         n_all = sum(self.counts) if self._sharded() else n_local
-        p.slot.votes_ev.synchronize()
+        self._wait(p.slot.votes_ev)
         votes = p.slot.buf("votes", p.n_votes, torch.int64).numpy().reshape(-1, 2, n_tpl)
         words = (n_tpl + 31) // 32
         pack_h = p.slot.buf("pack", cfg.n_kp_global + words, torch.int32)
+        t0 = time.perf_counter()
         choice = choose_consensus(votes, n_tpl, n_all, cfg, self.logger if self._rank == 0 else None,
                                   pack_out=pack_h.numpy())
+        self.stats["merge_s"] += time.perf_counter() - t0
         pack_dev = torch.empty(pack_h.numel(), dtype=torch.int32, device=self.dev)
         stages.memcpy_async(pack_dev.data_ptr(), pack_h.data_ptr(), pack_h.numel() * 4, self._hc)
         p.slot.pack_ev.record(self.copy)
@@ -596,7 +609,7 @@ class OverlappedSlabs:
             # (it has nothing else to do before it blocks on this step's votes) instead of
             # queueing a cross-stream wait, which leaves the device idle for tens of
             # microseconds even when RANSAC finished long before
-            p.fitted_ev.synchronize()
+            self._wait(p.fitted_ev)
         self._at_tail(mark, "w0")
         p.aligned = warp_frames(p.inp.frames, p.rr.params, out=p.out, stream=self._hs)
         self._queued()
@@ -604,10 +617,11 @@ class OverlappedSlabs:
 
     def _finish(self, p: _SlabInFlight, mark) -> SlabResult:
         """Host post-processing of slab p (VA:143-145) and the warps that need its maps."""
-        p.slot.params_ev.synchronize()  # after RANSAC(k): its parameters are on the host
+        self._wait(p.slot.params_ev)  # after RANSAC(k): its parameters are on the host
         n = p.inp.frames.shape[0]
         shape = tuple(p.rr.params.shape)
         params = p.slot.buf("params", p.rr.params.numel(), torch.float64).numpy().reshape(shape)
+        t0 = time.perf_counter()
         if self._sharded():
             from .distributed import neighbours
 
@@ -620,6 +634,7 @@ class OverlappedSlabs:
         else:
             affines, skipped, interpolated, eu = postprocess_affines(params, self.cfg)
             local = np.asarray(affines[:n], dtype=np.float64)
+        self.stats["post_s"] += time.perf_counter() - t0
         self._slots.append(p.slot)
         if self._device_maps():
             # frames without a model were warped to zeros: warp them with the filled maps

@@ -30,6 +30,13 @@ def test_library_exports_every_declared_symbol():
         assert re.search(rf"\bT {name}\b", out), name
 
 
+def test_library_has_no_unresolved_internal_symbols():
+    """Every kcmc:: symbol one translation unit uses is defined in the library (a helper
+    left with internal linkage links into a .so silently and fails only at load time)."""
+    out = os.popen(f"nm -D --undefined-only {_lib.lib_path()}").read()
+    assert not re.findall(r"\S*kcmc\S*", out), out
+
+
 def test_abi_version_and_error_reporting():
     L = _lib.load()
     assert L.kcmc_abi_version() == _lib.ABI_VERSION
@@ -55,4 +62,11 @@ def test_launch_entry_points_validate_before_touching_the_gpu():
                                None, None) == _lib.KCMC_EINVAL
     assert L.kcmc_ransac_prepare_samples(None, 3, None, 1, 1000, 42) == _lib.KCMC_EINVAL
     assert L.kcmc_warp_perspective_u16(None, None, None, None, 1, 4, 4, 1, 0, None) == _lib.KCMC_EINVAL
+    assert L.kcmc_consensus_vote(None, None, 1, 8, 0, None, None) == _lib.KCMC_EINVAL
+    assert L.kcmc_consensus_lookup(None, None, 1, 8, None, 1, None, None, None, None) == _lib.KCMC_EINVAL
+    assert L.kcmc_params_boundary(None, None, 1, 6, None, None) == _lib.KCMC_EINVAL
+    assert L.kcmc_ransac_rigid_grid(None, None, None, None, None, 0, 1, 10, 1000, 2.0, 1.0, 3, None, None, None, None,
+                                    0, None) == _lib.KCMC_EINVAL
+    assert L.kcmc_consensus_merge(None, 0, 8, 1, 1, None, None, None, None) == _lib.KCMC_EINVAL
+    assert L.kcmc_memcpy_async(None, None, 8, None) == _lib.KCMC_EINVAL
     del P

@@ -166,6 +166,44 @@ def test_overlapped_slabs_equal_align_slab(dev, depth, corun, grid):
         assert torch.equal(r.aligned, g.aligned)
 
 
+@pytest.mark.parametrize("model,rate,depth,corun", [("euclidean", 2, 2, True), ("euclidean", 2, 3, False),
+                                                    ("euclidean", 3, 3, True), ("projective", 1, 2, True),
+                                                    ("projective", 1, 3, True), ("projective", 1, 2, False)])
+def test_overlapped_slabs_host_maps_and_projective(dev, model, rate, depth, corun):
+    """The OverlappedSlabs paths test_overlapped_slabs_equal_align_slab does not reach:
+    frame_downsample_rate > 1 (every full-rate frame's map comes from the host NaN-padding
+    + interpolation, so the warp waits for the host; with corun the host waits for RANSAC
+    on the analysis stream), and the projective model on device maps (warpPerspective of
+    RANSAC's own [F, 3, 3] output, then the re-warp of model-less frames with the
+    gap-filled homographies).  Equal to align_slab, gaps included."""
+    S, H, W = 12, 180, 240
+    cfg = pipeline.AlignConfig(n_kp_global=40, ransac_model=model, frame_downsample_rate=rate)
+    slabs = []
+    for k, seed in enumerate((41, 42, 43)):
+        ks = synthetic.make_keypoints(S, 200, 32, (H, W), seed=seed, model=model)
+        rng = np.random.default_rng(seed)
+        for f in ((0, 5), (4, 5, S - 1), ())[k]:  # model-less sample frames (see above)
+            a, b = ks.q_off[f], ks.q_off[f + 1]
+            ks.des_q[a:b] = rng.integers(0, 256, (1, 32), dtype=np.uint8)
+        base = synthetic.make_texture((H, W), seed=seed)
+        frames = torch.from_numpy(np.broadcast_to(base, (S * rate, H, W)).copy()).to(dev)
+        slabs.append(pipeline.SlabInputs(frames, torch.from_numpy(ks.des_tpl).to(dev),
+                                         torch.from_numpy(ks.kp_tpl).to(dev), torch.from_numpy(ks.des_q).to(dev),
+                                         torch.from_numpy(ks.kp_q).to(dev), torch.from_numpy(ks.q_off).to(dev),
+                                         ks.q_off))
+    ref = [pipeline.align_slab(s, cfg) for s in slabs]
+    assert [len(r.skipped) for r in ref] == [2, 3, 0]
+    ov = pipeline.OverlappedSlabs(dev, cfg, depth=depth, corun=corun)
+    got = [ov.submit(s) for s in slabs]
+    got = got[depth - 1:] + ov.flush()
+    ov.synchronize()
+    for r, g in zip(ref, got):
+        assert r.affines.shape[0] == S * rate
+        assert np.array_equal(r.affines, g.affines, equal_nan=True)
+        assert r.skipped == g.skipped and r.interpolated == g.interpolated
+        assert torch.equal(r.aligned, g.aligned)
+
+
 def test_align_streamed_equals_device_resident(dev):
     """Host-resident frames streamed through the warp in slabs (3 streams, double
     buffering) give exactly the device-resident slab result."""
