@@ -52,6 +52,14 @@ struct WarpCfg {
   static constexpr int kRowPasses = ROW_PASSES;  // staging passes of 8 rows x 32 chunks
 };
 using BlockCfg = WarpCfg<56, 10240, 9>;  // 20 KB box, box rows <= 72 (7 workgroups per CU)
+// Frame heights that are a multiple of 64 but not of 56 (512: config 3) lose 9 % of their
+// tiles to a partial last tile row at 56 rows; 64-row tiles with the same 20 KB box budget
+// cover them exactly (the fast path's 71 staged rows still hold a 64-row tile rotated by up
+// to ~2.5 deg; larger rotations take the general staged path or the direct gather).
+using Block64Cfg = WarpCfg<64, 10240, 9>;
+
+// one-channel tile height for a frame height (round 3)
+inline bool use_tile64(int H) { return H % 64 == 0 && H % 56 != 0; }
 // Multi-channel frames (RGB / RGBA, config 4): 3-4x the bytes per box pixel, so shorter
 // tiles keep the interleaved box in a 32 KB LDS budget (box rows <= 32).
 using ChanCfg = WarpCfg<24, 16384, 4>;
@@ -765,26 +773,6 @@ __device__ __forceinline__ void invert_perspective(const double* S, double* M) {
   M[8] = (S[0] * S[4] - S[1] * S[3]) * d;
 }
 
-// WarpPerspectiveInvoker's fixed-point source coordinate of output pixel (x, y), where
-// xo is the first column of x's bw0-wide block and x1 = x - xo.  IN_RANGE: the tile's
-// plan has bounded every source coordinate of the tile within +-30000 px (a staged box),
-// so OpenCV's clamp to [INT_MIN, INT_MAX] is the identity and is left out.
-template <bool IN_RANGE = false>
-__device__ __forceinline__ void persp_coord(const double* M, int xo, int x1, int y, int& X, int& Y) {
-  const double X0 = M[0] * xo + M[1] * y + M[2];
-  const double Y0 = M[3] * xo + M[4] * y + M[5];
-  const double W0 = M[6] * xo + M[7] * y + M[8];
-  double w = W0 + M[6] * x1;
-  w = w != 0.0 ? 32.0 / w : 0.0;
-  double fX = (X0 + M[0] * x1) * w, fY = (Y0 + M[3] * x1) * w;
-  if (!IN_RANGE) {
-    fX = fmax((double)INT_MIN, fmin((double)INT_MAX, fX));
-    fY = fmax((double)INT_MIN, fmin((double)INT_MAX, fY));
-  }
-  X = (int)__builtin_rint(fX);
-  Y = (int)__builtin_rint(fY);
-}
-
 // Source box of a tile: when the projective denominator has one sign over the tile,
 // the tile's image is the convex hull of its corner images; one pixel of margin on each
 // side absorbs the 1/32-px rounding and the second tap.  Otherwise: direct gather.
@@ -862,6 +850,27 @@ __device__ __forceinline__ uint16_t blend_exact(uint32_t v00, uint32_t v01, uint
   return r;
 }
 
+// WarpPerspectiveInvoker's fixed-point source coordinate of an output pixel from its
+// per-(block, row) values X0, Y0, W0 (xo = the first column of the pixel's bw0-wide block)
+// and the column's products M0 x1, M3 x1, M6 x1 (x1 = x - xo) -- the same values OpenCV
+// computes, so the result is unchanged: W = W0 + M6 x1, W = W ? 32/W : 0,
+// X = cvRound(clamp((X0 + M0 x1) W)), Y likewise.  IN_RANGE: the tile's plan has bounded
+// every source coordinate of the tile within +-30000 px (a staged box), so OpenCV's clamp
+// to [INT_MIN, INT_MAX] is the identity and is left out.
+template <bool IN_RANGE>
+__device__ __forceinline__ void persp_px(double X0, double Y0, double W0, double m0x1, double m3x1, double m6x1,
+                                         int& X, int& Y) {
+  double w = W0 + m6x1;
+  w = w != 0.0 ? 32.0 / w : 0.0;
+  double fX = (X0 + m0x1) * w, fY = (Y0 + m3x1) * w;
+  if (!IN_RANGE) {
+    fX = fmax((double)INT_MIN, fmin((double)INT_MAX, fX));
+    fY = fmax((double)INT_MIN, fmin((double)INT_MAX, fY));
+  }
+  X = (int)__builtin_rint(fX);
+  Y = (int)__builtin_rint(fY);
+}
+
 template <class Cfg, int C, int MODE>
 __device__ __forceinline__ void persp_rows(const uint16_t* stile, const Box& box, const uint16_t* __restrict__ S,
                                            uint16_t* __restrict__ Dst, const double* M, int H, int W, int xb, int yb,
@@ -869,21 +878,43 @@ __device__ __forceinline__ void persp_rows(const uint16_t* stile, const Box& box
   const int x = xb + 2 * lane;
   const bool pair_store = C == 1 && (W & 1) == 0 && x + 2 <= W;
   int xo[2], x1[2];
+  double m0x1[2], m3x1[2], m6x1[2], dxo[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int xc = min(x + q, W - 1);  // columns past the edge reuse the last column's taps
     xo[q] = xc - xc % bw0;
     x1[q] = xc - xo[q];
+    // row-invariant: the column products and the block origin (round 3: hoisted out of
+    // the row loop, and X0 / Y0 / W0 evaluated once per row for the lane's pixel pair)
+    m0x1[q] = M[0] * x1[q];
+    m3x1[q] = M[3] * x1[q];
+    m6x1[q] = M[6] * x1[q];
+    dxo[q] = (double)xo[q];
   }
+  const bool one_block = xo[0] == xo[1];  // the pair straddles a block edge only for odd bw0
+  const double mx0 = M[0] * dxo[0], mx3 = M[3] * dxo[0], mx6 = M[6] * dxo[0];
 #pragma unroll
   for (int i = 0; i < Cfg::kTileH / 4; ++i) {
     const int y = yb + wave + 4 * i;  // wave-uniform
     if (y >= H) break;
     uint16_t o[2 * C];
+    const double dy = (double)y;
+    double X0[2], Y0[2], W0[2];
+    X0[0] = mx0 + M[1] * dy + M[2];
+    Y0[0] = mx3 + M[4] * dy + M[5];
+    W0[0] = mx6 + M[7] * dy + M[8];
+    X0[1] = X0[0];
+    Y0[1] = Y0[0];
+    W0[1] = W0[0];
+    if (!one_block) {
+      X0[1] = M[0] * dxo[1] + M[1] * dy + M[2];
+      Y0[1] = M[3] * dxo[1] + M[4] * dy + M[5];
+      W0[1] = M[6] * dxo[1] + M[7] * dy + M[8];
+    }
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       int X, Y;
-      persp_coord<MODE == 0>(M, xo[p], x1[p], y, X, Y);
+      persp_px<MODE == 0>(X0[p], Y0[p], W0[p], m0x1[p], m3x1[p], m6x1[p], X, Y);
       if (MODE == 0) {
         const int fx = X & 31, fy = Y & 31;
         const int li = ((Y >> 5) - box.sy0) * box.pitch + ((X >> 5) - box.ax0);
@@ -1035,11 +1066,17 @@ extern "C" int kcmc_warp_affine_u16(kcmc_ctx* ctx, const uint16_t* src, uint16_t
     return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: too many tiles in one call");
   hipStream_t s = (hipStream_t)stream;
   void* ws = nullptr;
-  const size_t wsb = C == 1 ? warp_workspace_bytes<BlockCfg>(n_frames, H, W) : warp_workspace_bytes<ChanCfg>(n_frames, H, W);
+  const bool t64 = C == 1 && use_tile64(H);
+  const size_t wsb = C == 1 ? (t64 ? warp_workspace_bytes<Block64Cfg>(n_frames, H, W)
+                                   : warp_workspace_bytes<BlockCfg>(n_frames, H, W))
+                            : warp_workspace_bytes<ChanCfg>(n_frames, H, W);
   KCMC_TRY(workspace_alloc(ctx, &ws, wsb, s));
   switch (C) {
     case 1:
-      launch_warp<1>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
+      if (t64)
+        launch_warp<1, Block64Cfg>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
+      else
+        launch_warp<1>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
       break;
     case 3:
       launch_warp<3>(src, dst, M, n_frames, H, W, inverse_map, ws, s);

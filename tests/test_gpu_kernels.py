@@ -447,6 +447,31 @@ def test_warp_all_tile_paths_at_1080p(dev):
         assert np.array_equal(out[f], oracle.warp_affine_u16(img, M)), f
 
 
+@pytest.mark.parametrize("values", ["full", "14bit", "hot"])
+def test_warp_64_row_tiles(dev, values):
+    """Frame heights that are multiples of 64 but not of 56 (512 x 512: BASELINE config 3)
+    take 64-row tiles: the fixed-pitch fast path for small rotations, the general staged
+    path / direct gather / zeros for larger rotations, zooms and shifts off the frame."""
+    rng = np.random.default_rng(64)
+    H, W = 512, 512
+    if values == "full":
+        img = rng.integers(0, 65536, (H, W))
+    elif values == "14bit":
+        img = rng.integers(0, 16384, (H, W))
+    else:
+        img = rng.integers(0, 16384, (H, W))
+        img[rng.random((H, W)) < 3e-4] = 65535
+    img = img.astype(np.uint16)
+    Ms = [synthetic.rigid(np.deg2rad(0.5), 3.25, -2.5), synthetic.rigid(np.deg2rad(2.4), -4.0, 1.75),
+          synthetic.rigid(np.deg2rad(6.0), 10.5, -7.25), synthetic.rigid(np.deg2rad(-30.0), 100, 50),
+          np.array([[0.6, 0.01, 5.0], [-0.01, 0.6, 3.0]]), np.array([[1.02, 0.0, -3.0], [0.0, 0.98, 2.0]]),
+          synthetic.rigid(0.0, 900.0, 0.0), synthetic.rigid(0.0, 0.0, 0.0)]
+    imgs = np.broadcast_to(img, (len(Ms), H, W)).copy()
+    out = stages.warp_affine_u16(_t(imgs, dev), _t(np.stack(Ms), dev)).cpu().numpy()
+    for f, M in enumerate(Ms):
+        assert np.array_equal(out[f], oracle.warp_affine_u16(img, M)), f
+
+
 def test_warp_nan_map_gives_zeros(dev):
     """A frame without a RANSAC model (NaN map) warps to zeros (coordinates outside the
     image under BORDER_CONSTANT); the pipeline re-warps it with the gap-filled map."""
