@@ -7,37 +7,34 @@
 //   S = sum_k ((double)a_k - (double)b_k)^2 (sequential, fp64), dist = sqrtf((float)S),
 // top-2 by (dist, frame index) like OpenCV's K-insertion.
 //
-// tpl_norm_max_kernel -- once per call: K = max over template rows of |a|^2 (fp32).
+// Phase 1 finds, per template row, a short candidate list on the fp16 matrix cores with a
+// certified error bound; phase 2 ranks the candidates with the exact definition.
 //
-// split_tiles_kernel -- once per call: every frame's rows, 32 at a time, written as the
-//   exact LDS image the matcher copies (18 KiB per tile: bf16 hi rows | bf16 lo rows, each
-//   row padded to 272 B, then C = (|b|^2 + K) / 2 per row; v = hi + lo + e with
-//   |e| <= 2^-18 |v|; hi = RNE(v), v - hi exact, lo = RNE(v - hi)), and each tile's
-//   max |b|^2.  Rows past the frame's last get C = +inf.
+// tpl_stats_kernel / tpl_err_kernel -- once per call: K = max |a|^2 over the template
+//   rows, the largest |a_k| (its power-of-2 scale s_T maps it into (2^14, 2^15]) and the
+//   largest norm of a row's fp16 rounding error.
+//
+// frame_images_kernel -- one workgroup per 64-row tile: the exact LDS image the matcher
+//   copies (18 KiB: fp16(s_f b) rows padded to 272 B, s_f = s_T / 2^8, then per row
+//   C' = s_T s_f ((|b|^2 + K) / 2 + beta_j)); rows past the frame's last: zeros and
+//   C' = +inf; and the frame's max |b|^2 and max beta_j.
 //
 // knn2_l2f32_kernel -- one workgroup = 256 template rows x one frame (8 waves x one block
-//   of 32 rows).  Tiles reach LDS by LDS-DMA (global_load_lds_dwordx4, three buffers:
-//   two tiles in flight ahead of the one in use, one barrier per tile; no staging
-//   registers).  On the bf16 matrix cores, with the template
-//   operand negated and the accumulator started at the row's C,
-//     v = (|b|^2 + K) / 2 - a.b,  a.b ~ hi.hi + hi.lo + lo.hi
-//   (v_mfma_f32_32x32x16_bf16, 3 MFMAs per k-step of 16: 5.3x fewer cycles than
-//   v_mfma_f32_32x32x2_f32 for the same contraction).  v orders a lane's frame rows
-//   exactly like |a - b|^2 = 2 v + |a|^2 - K (K >= |a|^2 keeps it non-negative), so a
-//   distance costs 7 VALU: clamp, key (v's float bits with the low mantissa bits
-//   replaced by the row within a group of kFoldTiles tiles), and the sorted top-4
-//   insertion; each group's top-4 is folded into a running approximate top-4.  The
-//   error of a listed value is bounded by
-//     eps = (5 (D + 2) 2^-24 + 0.6 (3 2^-18 + t)) (sqrt(K) + max|b|)^2 * 1.02
-//   with t = the keys' relative truncation (derivation at its use below).
-//   (derivation at its use below).
-//   A frame row can be among the exact top-2 only if v <= v(2) + 2 eps, so when the
-//   approximate 4th value exceeds that bound the exact top-2 lies within the top-3
-//   candidates: phase 2 re-evaluates them with the exact fp64 definition and orders
-//   them by (dist, index).  Rows that cannot be certified (near-ties of 4+ frame
-//   descriptors) are appended to their frame's list, which knn2_l2f32_fallback_kernel
-//   finishes by exact brute force, reading each frame row once per batch of up to 4
-//   listed rows.
+//   of 32 rows, the template operand fp16(-s_T a) in registers).  Tiles reach LDS by
+//   LDS-DMA (three buffers: two tiles in flight ahead of the one in use, one barrier per
+//   tile).  One v_mfma_f32_32x32x16_f16 per 16-wide k-step and 32-row half tile, the
+//   accumulator started at C':
+//     v~ = s_T s_f ((|b|^2 + K) / 2 + beta_j - a.b + e_j),  |e_j| <= beta_j
+//   (fp16 products are exact in fp32; e_j = the fp16 roundings of a and b, the fp32
+//   accumulation and the norms, bounded below at its use), so v~ orders a lane's frame
+//   rows like |a - b|^2 = 2 v + |a|^2 - K up to 2 beta, and v~ >= 0.  A distance costs 8
+//   VALU: the key (v~'s bits with the low bits replaced by the frame row: 2 ops) and a
+//   sorted top-6 insertion (v_med3_u32 x 5 + v_min_u32).  After the frame, the top-6 of
+//   the two lane halves are merged; when the 6th value exceeds v(2) (1 + 2T) + 2B the
+//   exact top-2 lies among the listed rows below that bound (usually 2-3), which phase 2
+//   re-evaluates with the exact fp64 definition and orders by (dist, index).  Rows that
+//   cannot be certified (6+ rows within 2B of the second) are appended to their frame's
+//   list, which knn2_l2f32_fallback_kernel finishes by exact brute force.
 #include <cfloat>
 
 #include "kcmc_internal.h"
@@ -46,27 +43,22 @@ namespace kcmc {
 namespace {
 
 typedef float v16f __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
-constexpr int kNBuf = 3;                           // tile buffers: two tiles in flight ahead of the one in use
-constexpr int kBlocks = 1;                         // 32-row template blocks per wave (2: 1 wave per SIMD)
-constexpr int kTplPerWG = kWaves * kBlocks * 32;  // 256
-constexpr int kDP = 128;                           // padded descriptor length
-constexpr int kKSteps = kDP / 16;                  // k-steps of v_mfma_f32_32x32x16_bf16
-constexpr int kTile = 32;                          // frame rows per tile image (one MFMA tile)
-constexpr int kFoldTiles = 2;                      // tiles per top-4 fold (the row within them is in the key)
-constexpr uint32_t kRowMask = kFoldTiles * kTile - 1;
-// relative truncation of a key (its low log2(kFoldTiles * kTile) mantissa bits)
-constexpr float kKeyTrunc = (float)(kFoldTiles * kTile) * 1.1920929e-7f;
-constexpr int kRowB = kDP + 8;                     // padded LDS row (bf16 elements, 272 B)
-constexpr int kImgLo = kTile * kRowB * 2;          // byte offset of the lo rows in a tile image
-constexpr int kImgC = 2 * kImgLo;                  // byte offset of the per-row C values
-constexpr int kImgBytes = 18 * 1024;               // tile image, whole 1 KiB LDS-DMA pieces
+constexpr int kNBuf = 3;                  // tile buffers: two tiles in flight ahead of the one in use
+constexpr int kTplPerWG = kWaves * 32;    // 256 template rows per workgroup
+constexpr int kDP = 128;                  // padded descriptor length
+constexpr int kKSteps = kDP / 16;         // k-steps of v_mfma_f32_32x32x16_f16
+constexpr int kTile = 64;                 // frame rows per tile image (two MFMA row blocks)
+constexpr int kRowB = kDP + 8;            // padded LDS row (fp16 elements, 272 B)
+constexpr int kImgC = kTile * kRowB * 2;  // byte offset of the per-row C' values
+constexpr int kImgBytes = 18 * 1024;      // tile image, whole 1 KiB LDS-DMA pieces
 constexpr int kPieces = kImgBytes / 1024;
 static_assert(kImgC + kTile * 4 <= kImgBytes, "tile image layout");
-constexpr uint32_t kNoKey = 0xffffffffu;
+constexpr int kTop = 6;                   // approximate top-K per lane
+constexpr int kImgThreads = 1024;         // frame_images_kernel
 
 // The build's exact distance (identical operation order in the oracle).
 __device__ __forceinline__ float exact_dist(const float* __restrict__ a, const float* __restrict__ b, int D) {
@@ -78,8 +70,7 @@ __device__ __forceinline__ float exact_dist(const float* __restrict__ a, const f
   return sqrtf((float)S);
 }
 
-// The same sum for 16-byte aligned rows with D % 4 == 0, read four floats per load (the
-// fallback's lanes each walk a different frame row: a quarter of the load instructions).
+// The same sum for 16-byte aligned rows with D % 4 == 0, read four floats per load.
 __device__ __forceinline__ float exact_dist4(const float* __restrict__ a, const float* __restrict__ b, int D) {
   double S = 0.0;
   for (int k = 0; k < D; k += 4) {
@@ -116,23 +107,6 @@ __device__ __forceinline__ void top2_insert_exact(float& d0, int& j0, float& d1,
   }
 }
 
-// Approximate top-4 values (v0 <= v1 <= v2 <= v3) with the indices of the first three.
-struct Top4 {
-  float v[4];
-  int j[3];
-};
-
-__device__ __forceinline__ void top4_insert(Top4& t, float x, int j) {
-  const bool c0 = x < t.v[0], c1 = x < t.v[1], c2 = x < t.v[2], c3 = x < t.v[3];
-  t.v[3] = c2 ? t.v[2] : (c3 ? x : t.v[3]);
-  t.v[2] = c1 ? t.v[1] : (c2 ? x : t.v[2]);
-  t.j[2] = c1 ? t.j[1] : (c2 ? j : t.j[2]);
-  t.v[1] = c0 ? t.v[0] : (c1 ? x : t.v[1]);
-  t.j[1] = c0 ? t.j[0] : (c1 ? j : t.j[1]);
-  t.v[0] = c0 ? x : t.v[0];
-  t.j[0] = c0 ? j : t.j[0];
-}
-
 // Workgroups are dealt round-robin over the 8 XCDs: give each XCD a contiguous run of
 // ids (bijective also when n % 8 != 0).
 __device__ __forceinline__ int xcd_remap(int bid, int n) {
@@ -146,100 +120,226 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
   return r;
 }
 
-// Sorted top-4 of 32-bit keys (k0 <= k1 <= k2 <= k3): 4 VALU per insertion.
-__device__ __forceinline__ void top4_key(uint32_t (&k)[4], uint32_t x) {
-  k[3] = med3_u32(k[2], k[3], x);
-  k[2] = med3_u32(k[1], k[2], x);
-  k[1] = med3_u32(k[0], k[1], x);
+// Sorted top-kTop of 32-bit keys (k0 <= k1 <= ...): kTop VALU per insertion.
+__device__ __forceinline__ void topk_key(uint32_t (&k)[kTop], uint32_t x) {
+#pragma unroll
+  for (int i = kTop - 1; i > 0; --i) k[i] = med3_u32(k[i - 1], k[i], x);
   k[0] = min(k[0], x);
 }
 
-// bf16 split of an fp32 value: v = hi + lo + e with |e| <= 2^-18 |v| (hi = RNE(v), the
-// difference v - hi is exact in fp32, lo = RNE(v - hi)).
-__device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
-  hi = (__bf16)v;
-  lo = (__bf16)(v - (float)hi);
+// Sorted approximate top-kTop values with the frame rows of the first kTop - 1.
+struct TopK {
+  float v[kTop];
+  int j[kTop - 1];
+};
+
+__device__ __forceinline__ void topk_insert(TopK& t, float x, int j) {
+  bool c[kTop];
+#pragma unroll
+  for (int i = 0; i < kTop; ++i) c[i] = x < t.v[i];
+  t.v[kTop - 1] = c[kTop - 2] ? t.v[kTop - 2] : (c[kTop - 1] ? x : t.v[kTop - 1]);
+#pragma unroll
+  for (int i = kTop - 2; i > 0; --i) {
+    t.v[i] = c[i - 1] ? t.v[i - 1] : (c[i] ? x : t.v[i]);
+    t.j[i] = c[i - 1] ? t.j[i - 1] : (c[i] ? j : t.j[i]);
+  }
+  t.v[0] = c[0] ? x : t.v[0];
+  t.j[0] = c[0] ? j : t.j[0];
 }
 
-// K = max_i |a_i|^2 over the template rows (positive float bits order as integers; *Kbits
-// zeroed before the launch).  32 lanes per row, 4 floats each.
-__global__ __launch_bounds__(256) void tpl_norm_max_kernel(const float* __restrict__ des_tpl, int n_tpl, int D,
-                                                           unsigned* __restrict__ Kbits) {
-  const int i = blockIdx.x * 8 + (threadIdx.x >> 5);
-  if (i >= n_tpl) return;  // whole 32-lane groups exit together
-  const int col = (threadIdx.x & 31) * 4;
-  const float* src = des_tpl + (size_t)i * D;
-  float ss = 0.f;
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (col + k < D) ss = fmaf(src[col + k], src[col + k], ss);
-#pragma unroll
-  for (int off = 16; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
-  if ((threadIdx.x & 31) == 0) atomicMax(Kbits, __float_as_uint(ss));
+// Power-of-2 scale that maps a largest magnitude m into (2^14, 2^15]: fp16 then holds every
+// scaled value (max 65504) with 11 significant bits; 1 for m == 0 / non-finite m, clamped
+// to [2^-60, 2^60] (a frame outside that range is certified nowhere and falls back).
+__device__ __forceinline__ float pow2_scale(float m) {
+  if (!(m > 0.f) || !(m < INFINITY)) return 1.f;
+  int e;
+  (void)frexpf(m, &e);  // m < 2^e
+  return ldexpf(1.f, max(-60, min(60, 15 - e)));
 }
 
-// Frame f's tile t (rows 32 t .. 32 t + 31) -> img[(f * tpf + t) * kImgBytes]: the LDS
-// image the matcher copies (hi rows, lo rows, C = (|b|^2 + K) / 2 per row; rows past the
-// frame's last: zero descriptors, C = +inf), and the tile's max |b|^2 -> tile_max[f * tpf
-// + t].  One workgroup per tile, 8 rows per pass (32 lanes per row, 4 floats each).
-__global__ __launch_bounds__(256) void split_tiles_kernel(const float* __restrict__ des_q, int D,
-                                                          const int32_t* __restrict__ q_off, int tpf,
-                                                          const unsigned* __restrict__ Kbits,
-                                                          uint8_t* __restrict__ img,
-                                                          float* __restrict__ tile_max) {
-  __shared__ float s_max[4];
-  const int f = blockIdx.y, t = blockIdx.x;
-  const int n_q = q_off[f + 1] - q_off[f];
-  const int n_rows = min(n_q, tpf * kTile);
-  if (t * kTile >= n_rows) return;  // the whole workgroup
-  const int col = (threadIdx.x & 31) * 4;
-  const bool v4 = (D & 3) == 0 && (reinterpret_cast<uintptr_t>(des_q) & 15) == 0;
-  const float K = __uint_as_float(*Kbits);
-  uint8_t* tile = img + ((size_t)f * tpf + t) * kImgBytes;
-  float tmax = 0.f;
+// Bias of row j's accumulator start (unscaled units): beta_j >= |e_j| for every template
+// row, e_j the phase-1 error of v~_j.  With a'' = fp16(s_T a) / s_T = a - da and b'' = b -
+// db the values the matrix cores multiply (fp16 products are exact in fp32):
+// |a.b - a''.b''| <= |da||b| + |a||db| + |da||db|, where |da| <= dA (the template's
+// largest rounding-error norm, tpl_err_kernel) and |db_j| is the row's own (both computed
+// from the actual roundings, subnormals included); the fp32 accumulation of C' and D
+// products (rounding or truncating) <= (D + 1) 2u 1.01 S_j with S_j <= U_j / 2 + beta_j,
+// U_j = (sqrt(K) + |b_j|)^2, u = 2^-24; the norm, K, halving, bias and scaling roundings
+// <= (D + 4) u U_j / 2; K below an exact |a|^2 by <= D u K / 2.  Sum <= dA |b_j| +
+// sqrt(K) |db_j| (1 + 2^-10) + (3.6 D + 6) u U_j; taken as 1.1 (dA |b| + sqrt(K) |db| +
+// (4 D + 8) u U).  (|a| <= sqrt(K) (1 + D u / 2), |b_j| <= sqrt(ss_j) (1 + D u) and the
+// fp32 evaluation of the norms are inside the 1.1.)
+__device__ __forceinline__ float beta_of(float sK, float nb, float dA, float db, int D) {
+  const float U = (sK + nb) * (sK + nb);
+  return 1.1f * (dA * nb + sK * db + (float)(4 * D + 8) * 5.9604645e-8f * U) + 1e-30f;
+}
+
+constexpr int kTplRowsPerWG = 64;  // tpl_stats_kernel / tpl_err_kernel: 8 row groups x 8 rows
+
+// Workgroup max of a non-negative float (bits) -> one atomicMax.
+__device__ __forceinline__ void wg_atomic_max(float v, unsigned* dst) {
+  __shared__ float s_w[4];
 #pragma unroll
-  for (int pass = 0; pass < kTile / 8; ++pass) {
-    const int rr = pass * 8 + (threadIdx.x >> 5);
-    const int r = t * kTile + rr;
-    const bool real = r < n_rows;
-    const float* src = des_q + (size_t)(q_off[f] + r) * D;
-    float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (real) {
-      if (v4) {
-        if (col < D) w = *reinterpret_cast<const float4*>(src + col);
-      } else {
-        w.x = col < D ? src[col] : 0.f;
-        w.y = col + 1 < D ? src[col + 1] : 0.f;
-        w.z = col + 2 < D ? src[col + 2] : 0.f;
-        w.w = col + 3 < D ? src[col + 3] : 0.f;
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(dst, __float_as_uint(fmaxf(fmaxf(s_w[0], s_w[1]), fmaxf(s_w[2], s_w[3]))));
+}
+
+// Kst[0] = K = max_i |a_i|^2, Kst[1] = max |a_ik| (non-negative float bits, zeroed before
+// the launch).  32 lanes per row, 4 floats each; 8 rows per 32-lane group.
+__global__ __launch_bounds__(256) void tpl_stats_kernel(const float* __restrict__ des_tpl, int n_tpl, int D,
+                                                        unsigned* __restrict__ Kst) {
+  const int col = (threadIdx.x & 31) * 4;
+  float K = 0.f, mx = 0.f;
+  for (int rr = 0; rr < 8; ++rr) {
+    const int i = blockIdx.x * kTplRowsPerWG + (threadIdx.x >> 5) * 8 + rr;
+    if (i >= n_tpl) break;  // whole 32-lane groups together
+    const float* src = des_tpl + (size_t)i * D;
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (col + k < D) {
+        ss = fmaf(src[col + k], src[col + k], ss);
+        mx = fmaxf(mx, fabsf(src[col + k]));
       }
-    }
-    float ss = fmaf(w.w, w.w, fmaf(w.z, w.z, fmaf(w.y, w.y, w.x * w.x)));
 #pragma unroll
     for (int off = 16; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
-    tmax = fmaxf(tmax, ss);
-    if ((threadIdx.x & 31) == 0) *reinterpret_cast<float*>(tile + kImgC + 4 * rr) = real ? 0.5f * (ss + K) : INFINITY;
-    __bf16 hv[4], lv[4];
-    split_bf16(w.x, hv[0], lv[0]);
-    split_bf16(w.y, hv[1], lv[1]);
-    split_bf16(w.z, hv[2], lv[2]);
-    split_bf16(w.w, hv[3], lv[3]);
-    *reinterpret_cast<uint2*>(tile + (rr * kRowB + col) * 2) = *reinterpret_cast<const uint2*>(hv);
-    *reinterpret_cast<uint2*>(tile + kImgLo + (rr * kRowB + col) * 2) = *reinterpret_cast<const uint2*>(lv);
-    // the rows' padding columns too: every cache line of the image is written whole
-    if (col == kDP - 4) {
-      *reinterpret_cast<uint4*>(tile + (rr * kRowB + kDP) * 2) = make_uint4(0u, 0u, 0u, 0u);
-      *reinterpret_cast<uint4*>(tile + kImgLo + (rr * kRowB + kDP) * 2) = make_uint4(0u, 0u, 0u, 0u);
+    K = fmaxf(K, ss);
+  }
+  wg_atomic_max(K, &Kst[0]);
+  wg_atomic_max(mx, &Kst[1]);
+}
+
+// Kst[2] = dA >= max_i |a_i - fp16(s_T a_i) / s_T| (fp64 sums, rounded up): the
+// template's largest rounding-error norm on the matrix cores.
+__global__ __launch_bounds__(256) void tpl_err_kernel(const float* __restrict__ des_tpl, int n_tpl, int D,
+                                                      unsigned* __restrict__ Kst) {
+  const float sT = pow2_scale(__uint_as_float(Kst[1]));
+  const int col = (threadIdx.x & 31) * 4;
+  float dA = 0.f;
+  for (int rr = 0; rr < 8; ++rr) {
+    const int i = blockIdx.x * kTplRowsPerWG + (threadIdx.x >> 5) * 8 + rr;
+    if (i >= n_tpl) break;  // whole 32-lane groups together
+    const float* src = des_tpl + (size_t)i * D;
+    double e2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (col + k < D) {
+        const double d = (double)src[col + k] - (double)(float)(_Float16)(src[col + k] * sT) / (double)sT;
+        e2 += d * d;
+      }
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) e2 += __shfl_xor(e2, off);
+    dA = fmaxf(dA, (float)(sqrt(e2) * 1.000001) + 1e-38f);
+  }
+  wg_atomic_max(dA, &Kst[2]);
+}
+
+// Tile t of frame f -> img[(f * tpf + t) * kImgBytes]: fp16(s_f b) rows with s_f = s_T /
+// 2^8 (frame values up to 2^8 x the template's largest element are in range; smaller ones
+// keep 11 bits down to 2^-14 and the subnormal rest is in |db|), per row C'; and the
+// frame's max |b|^2 / max beta_j (fmax / fbeta, zeroed before the launch).  A value
+// beyond fp16's range flags the frame (fbad), whose rows are then all certified nowhere
+// (exact fallback).  One workgroup per tile: 16 lanes per row, 8 elements each.
+__device__ __forceinline__ float frame_scale(const unsigned* __restrict__ Kst) {
+  return pow2_scale(__uint_as_float(Kst[1])) * 0.00390625f;
+}
+
+__global__ __launch_bounds__(kImgThreads) void frame_images_kernel(const float* __restrict__ des_q, int D,
+                                                                   const int32_t* __restrict__ q_off, int tpf,
+                                                                   const unsigned* __restrict__ Kst,
+                                                                   uint8_t* __restrict__ img,
+                                                                   unsigned* __restrict__ fmax,
+                                                                   unsigned* __restrict__ fbeta,
+                                                                   int32_t* __restrict__ fbad) {
+  const int t = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+  const int q_begin = q_off[f];
+  const int n_q = min(q_off[f + 1] - q_begin, tpf * kTile);
+  if (t * kTile >= n_q) return;  // the whole workgroup
+  const float* base = des_q + (size_t)q_begin * D;
+  const bool v4 = (D & 3) == 0 && (reinterpret_cast<uintptr_t>(base) & 15) == 0;
+  const float K = __uint_as_float(Kst[0]);
+  const float sK = sqrtf(K);
+  const float sT = pow2_scale(__uint_as_float(Kst[1]));
+  const float sf = frame_scale(Kst);
+  const float sc = sT * sf;
+  const float dA = __uint_as_float(Kst[2]);
+  const int rr = tid >> 4, col = (tid & 15) * 8;
+  uint8_t* tile = img + ((size_t)f * tpf + t) * kImgBytes;
+  const int r = t * kTile + rr;
+  const bool real = r < n_q;
+  float x[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = 0.f;
+  if (real) {
+    const float* src = base + (size_t)r * D;
+    if (v4) {
+      if (col < D) {
+        const float4 p = *reinterpret_cast<const float4*>(src + col);
+        x[0] = p.x; x[1] = p.y; x[2] = p.z; x[3] = p.w;
+      }
+      if (col + 4 < D) {
+        const float4 p = *reinterpret_cast<const float4*>(src + col + 4);
+        x[4] = p.x; x[5] = p.y; x[6] = p.z; x[7] = p.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = col + k < D ? src[col + k] : 0.f;
     }
   }
-  // and the image's tail after the C values
-  for (int e = kImgC + kTile * 4 + 16 * (int)threadIdx.x; e < kImgBytes; e += 16 * 256)
-    *reinterpret_cast<uint4*>(tile + e) = make_uint4(0u, 0u, 0u, 0u);
-  tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
-  if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = tmax;
+  float ss = 0.f, e2 = 0.f;
+  bool big = false;
+  f16x8 h;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    ss = fmaf(x[k], x[k], ss);
+    const float y = x[k] * sf;
+    big |= !(fabsf(y) <= 65504.f);  // also NaN
+    h[k] = (_Float16)y;
+    const float d = x[k] - (float)h[k] / sf;  // the rounding error, exact
+    e2 = fmaf(d, d, e2);
+  }
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) {
+    ss += __shfl_xor(ss, off);
+    e2 += __shfl_xor(e2, off);
+  }
+  *reinterpret_cast<f16x8*>(tile + (rr * kRowB + col) * 2) = h;
+  if ((tid & 15) == 15)  // the row's 16 bytes of padding: every image line is written whole
+    *reinterpret_cast<uint4*>(tile + (rr * kRowB + kDP) * 2) = make_uint4(0u, 0u, 0u, 0u);
+  float nmax = 0.f, bmax = 0.f;
+  if ((tid & 15) == 0) {
+    const float beta = beta_of(sK, sqrtf(ss), dA, sqrtf(e2), D);
+    *reinterpret_cast<float*>(tile + kImgC + 4 * rr) = real ? (0.5f * (ss + K) + beta) * sc : INFINITY;
+    if (real) {
+      nmax = ss;
+      bmax = beta;
+    }
+  }
+  if (tid < (kImgBytes - kImgC - kTile * 4) / 16)  // the image's tail after the C' values
+    *reinterpret_cast<uint4*>(tile + kImgC + kTile * 4 + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
+  if (__any(big) && (tid & 63) == 0) atomicOr(&fbad[f], 1);
+  __shared__ float s_n[kImgThreads / 64], s_b[kImgThreads / 64];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    nmax = fmaxf(nmax, __shfl_xor(nmax, off));
+    bmax = fmaxf(bmax, __shfl_xor(bmax, off));
+  }
+  if ((tid & 63) == 0) {
+    s_n[tid >> 6] = nmax;
+    s_b[tid >> 6] = bmax;
+  }
   __syncthreads();
-  if (threadIdx.x == 0)
-    tile_max[(size_t)f * tpf + t] = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
+  if (tid == 0) {
+    for (int w = 1; w < kImgThreads / 64; ++w) {
+      nmax = fmaxf(nmax, s_n[w]);
+      bmax = fmaxf(bmax, s_b[w]);
+    }
+    atomicMax(&fmax[f], __float_as_uint(nmax));
+    atomicMax(&fbeta[f], __float_as_uint(bmax));
+  }
 }
 
 // One tile image (18 x 1 KiB) global -> LDS: wave w copies pieces w, w + kWaves, ...
@@ -270,13 +370,13 @@ __device__ __forceinline__ void dma_tile(const uint8_t* __restrict__ src, uint8_
   }
 }
 
-// 4 waves per SIMD (<= 128 VGPRs): without the cap the compiler hoists every fragment
-// read of a tile (239 VGPRs, 2 waves per SIMD)
+// 4 waves per SIMD (<= 128 VGPRs)
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void knn2_l2f32_kernel(
     const float* __restrict__ des_tpl, int n_tpl, int D, const float* __restrict__ des_q,
     const int32_t* __restrict__ q_off, const uint8_t* __restrict__ img, int tpf,
-    const unsigned* __restrict__ Kbits, const float* __restrict__ tile_max, int32_t* __restrict__ out_idx,
-    float* __restrict__ out_dist, int32_t* __restrict__ fallback, int32_t* __restrict__ fb_cnt) {
+    const unsigned* __restrict__ Kst, const float* __restrict__ fmax, const float* __restrict__ fbeta,
+    const int32_t* __restrict__ fbad, int key_bits, int32_t* __restrict__ out_idx, float* __restrict__ out_dist, int32_t* __restrict__ fallback,
+    int32_t* __restrict__ fb_cnt) {
   __shared__ __attribute__((aligned(16))) uint8_t tbuf[kNBuf][kImgBytes];
 
   // XCD-aware order: the workgroups of one frame get consecutive ids of one XCD's run
@@ -287,7 +387,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
   const int f = wg / ntb, tb = wg - f * ntb;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int c = lane & 31;  // MFMA column = template row within a block
+  const int c = lane & 31;  // MFMA column = template row within the wave's block
   const int h = lane >> 5;  // k-half of the fragments / row group of the output
   const int q_begin = q_off[f];
   const int n_q = q_off[f + 1] - q_begin;
@@ -300,36 +400,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
   const bool many = wave < kPieces % kWaves;
   static_assert(kPieces / kWaves == 2 && kPieces % kWaves != 0, "vmcnt counts below assume 2 or 3 pieces per wave");
 
-  // ---- template fragments (B operand, bf16 hi/lo split of -a) kept in registers: lane
-  // (c, h) holds row i's elements k = 16 s + 8 h + j of k-step s
-  bf16x8 bhi[kBlocks][kKSteps], blo[kBlocks][kKSteps];
-  int tpl_row[kBlocks];
+  // ---- template fragment (B operand, fp16(-s_T a)) kept in registers: lane (c, h) holds
+  // row i's elements k = 16 s + 8 h + j of k-step s
+  const float sT = pow2_scale(__uint_as_float(Kst[1]));
+  const int i = tb * kTplPerWG + wave * 32 + c;
+  f16x8 btpl[kKSteps];
 #pragma unroll
-  for (int b = 0; b < kBlocks; ++b) {
-    const int i = tb * kTplPerWG + (wave * kBlocks + b) * 32 + c;
-    tpl_row[b] = i;
+  for (int st = 0; st < kKSteps; ++st)
 #pragma unroll
-    for (int st = 0; st < kKSteps; ++st)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 16 * st + 8 * h + j;
-        const float v = (i < n_tpl && k < D) ? des_tpl[(size_t)i * D + k] : 0.f;
-        __bf16 hv, lv;
-        split_bf16(-v, hv, lv);
-        bhi[b][st][j] = hv;
-        blo[b][st][j] = lv;
-      }
-  }
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * st + 8 * h + j;
+      const float v = (i < n_tpl && k < D) ? des_tpl[(size_t)i * D + k] : 0.f;
+      btpl[st][j] = (_Float16)(-v * sT);
+    }
 
-  Top4 best[kBlocks];
+  // keys: v~'s bits with the low key_bits bits replaced by (tile << 5 | half << 4 | r)
+  const uint32_t kmask = ~((1u << key_bits) - 1u);
+  uint32_t ck[kTop];
 #pragma unroll
-  for (int b = 0; b < kBlocks; ++b) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) best[b].v[k] = INFINITY;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) best[b].j[k] = -1;
-  }
-  uint32_t ck[kBlocks][4];
+  for (int k = 0; k < kTop; ++k) ck[k] = 0xffffffffu;
   int cur = 0;  // t % kNBuf
   for (int t = 0; t < n_tiles; ++t) {
     // tile t has landed (this wave's pieces: vmcnt, leaving tile t + 1's in flight; the
@@ -350,135 +439,109 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     }
     const uint8_t* tbp = tbuf[cur];
     cur = cur + 1 == kNBuf ? 0 : cur + 1;
-    if ((t & (kFoldTiles - 1)) == 0) {
-#pragma unroll
-      for (int b = 0; b < kBlocks; ++b)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ck[b][k] = kNoKey;
-    }
-    // accumulators start at the rows' C: lane's 16 rows (r & 3) + 8 (r >> 2) + 4h
+    // accumulators start at the rows' C': half hh, lane's 16 rows 32 hh + (r & 3) + 8 (r >> 2) + 4h
     const float* cq = reinterpret_cast<const float*>(tbp + kImgC);
-    v16f acc0;
+    v16f acc[2];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 q4 = *reinterpret_cast<const float4*>(cq + 8 * g + 4 * h);
-      acc0[4 * g] = q4.x;
-      acc0[4 * g + 1] = q4.y;
-      acc0[4 * g + 2] = q4.z;
-      acc0[4 * g + 3] = q4.w;
-    }
-    v16f acc[kBlocks];
+    for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
-    for (int b = 0; b < kBlocks; ++b) acc[b] = acc0;
-    const __bf16* ah = reinterpret_cast<const __bf16*>(tbp) + c * kRowB + 8 * h;
-    const __bf16* al = reinterpret_cast<const __bf16*>(tbp + kImgLo) + c * kRowB + 8 * h;
-#pragma unroll
-    for (int st = 0; st < kKSteps; ++st) {
-      const bf16x8 a_h = *reinterpret_cast<const bf16x8*>(ah + 16 * st);
-      const bf16x8 a_l = *reinterpret_cast<const bf16x8*>(al + 16 * st);
-#pragma unroll
-      for (int b = 0; b < kBlocks; ++b) {
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_h, bhi[b][st], acc[b], 0, 0, 0);
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_h, blo[b][st], acc[b], 0, 0, 0);
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_l, bhi[b][st], acc[b], 0, 0, 0);
+      for (int g = 0; g < 4; ++g) {
+        const float4 q4 = *reinterpret_cast<const float4*>(cq + 32 * hh + 8 * g + 4 * h);
+        acc[hh][4 * g] = q4.x;
+        acc[hh][4 * g + 1] = q4.y;
+        acc[hh][4 * g + 2] = q4.z;
+        acc[hh][4 * g + 3] = q4.w;
       }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const _Float16* ap = reinterpret_cast<const _Float16*>(tbp) + (32 * hh + c) * kRowB + 8 * h;
+#pragma unroll
+      for (int st = 0; st < kKSteps; ++st)
+        acc[hh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*reinterpret_cast<const f16x8*>(ap + 16 * st), btpl[st],
+                                                         acc[hh], 0, 0, 0);
     }
-    // keys: v's bits (negative v -> +0 by a signed max; +inf / NaN sort after every
-    // finite key) with the row within the group of kFoldTiles tiles in the low bits
-    const uint32_t pair_row = (uint32_t)(t & (kFoldTiles - 1)) * kTile + 4 * h;
+    const uint32_t tbase = (uint32_t)t << 5;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const uint32_t row = pair_row + (uint32_t)((r & 3) + 8 * (r >> 2));
+    for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
-      for (int b = 0; b < kBlocks; ++b)
-        top4_key(ck[b], ((uint32_t)max(__float_as_int(acc[b][r]), 0) & ~kRowMask) | row);
-    }
-    // ---- fold the group's top-4 into the running top-4 (the group's 4th key bounds
-    // every row of the group it did not report, and so does the running 4th value)
-    if ((t & (kFoldTiles - 1)) == kFoldTiles - 1 || t + 1 == n_tiles) {
-      const int base = (t & ~(kFoldTiles - 1)) * kTile;
+      for (int r = 0; r < 16; ++r)
+        topk_key(ck, ((__float_as_uint(acc[hh][r]) & kmask) | (uint32_t)(hh * 16 + r)) | tbase);
+  }
+
+  // ---- decode (value truncated to the key, frame row) and merge the two row halves
+  // (lanes c and c + 32 own the same template row)
+  TopK best;
 #pragma unroll
-      for (int b = 0; b < kBlocks; ++b)
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (ck[b][k] != kNoKey)
-            top4_insert(best[b], __uint_as_float(ck[b][k] & ~kRowMask), base + (int)(ck[b][k] & kRowMask));
+  for (int k = 0; k < kTop; ++k) {
+    const uint32_t low = ck[k] & ~kmask;
+    best.v[k] = ck[k] == 0xffffffffu ? INFINITY : __uint_as_float(ck[k] & kmask);
+    if (k < kTop - 1) {
+      const int r = (int)(low & 15);
+      best.j[k] = (int)(low >> 5) * kTile + (int)((low >> 4) & 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
     }
   }
-  // the frame's max |b|^2, from its tiles'
-  float maxqn = 0.f;
-  for (int t = lane; t < n_tiles; t += 64) maxqn = fmaxf(maxqn, tile_max[(size_t)f * tpf + t]);
+  {
+    float ov[kTop];
+    int oj[kTop - 1];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) maxqn = fmaxf(maxqn, __shfl_xor(maxqn, off));
-  const float maxb = sqrtf(maxqn);
-  const float sK = sqrtf(__uint_as_float(*Kbits));
-
-  // ---- merge the two row halves (lanes c and c + 32 own the same template row)
+    for (int k = 0; k < kTop; ++k) ov[k] = __shfl_xor(best.v[k], 32);
 #pragma unroll
-  for (int b = 0; b < kBlocks; ++b) {
-    float ov[4];
-    int oj[3];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ov[k] = __shfl_xor(best[b].v[k], 32);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) oj[k] = __shfl_xor(best[b].j[k], 32);
+    for (int k = 0; k < kTop - 1; ++k) oj[k] = __shfl_xor(best.j[k], 32);
     if (h == 0) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) top4_insert(best[b], ov[k], oj[k]);
-      // the partner's 4th value bounds every index it did not report
-      best[b].v[3] = fminf(best[b].v[3], ov[3]);
+      for (int k = 0; k < kTop - 1; ++k) topk_insert(best, ov[k], oj[k]);
+      // the partner's last value bounds every row it did not report
+      best.v[kTop - 1] = fminf(best.v[kTop - 1], ov[kTop - 1]);
     }
   }
-  if (h != 0) return;
+  if (h != 0 || i >= n_tpl) return;
 
-  // ---- certify and re-rank with the exact distance
-  const float* base = des_q + (size_t)q_begin * D;
+  // ---- certify and re-rank with the exact distance.  In scaled units (sc = s_T s_f):
+  // v~_j is in [sc v_j, sc (v_j + 2B)] with B = max_j beta_j (fbeta), and a listed
+  // value tv_j (a key: low key_bits bits cleared, relative truncation T <= 2^(key_bits - 23))
+  // is in [v~_j (1 - T), v~_j].  An unlisted row has sc v_j >= tv_j - 2 sc B >= tv(6) -
+  // 2 sc B, a listed one sc v_j <= tv_j / (1 - T): rows whose tv exceeds thr = tv(2) (1 + 2T)
+  // + 2 sc B cannot reach the exact top-2 (the fp64 distance keeps the order of v up to
+  // its rounding, far inside T).  A frame whose scaled values could overflow is not
+  // certified (fallback).
+  const float K = __uint_as_float(Kst[0]);
+  const float sK = sqrtf(K);
+  const float sc = sT * frame_scale(Kst);
+  const float maxb = sqrtf(fmax[f]);
+  const float Bs = fbeta[f] * sc;
+  const float T = ldexpf(1.f, key_bits - 23);
+  const float thr = best.v[1] * (1.f + 2.f * T) + 2.f * Bs;
+  const bool sane = fbad[f] == 0 && sc * (K + maxb * maxb) < 1e36f && Bs < 1e36f;
+  int ncand;
+  if (!(best.v[1] < INFINITY)) {
+    ncand = best.v[0] < INFINITY ? 1 : 0;  // fewer than two frame rows: all are listed
+  } else if (!sane || !(best.v[kTop - 1] > thr)) {
+    ncand = -1;
+  } else {
+    ncand = 2;
 #pragma unroll
-  for (int b = 0; b < kBlocks; ++b) {
-    const int i = tpl_row[b];
-    if (i >= n_tpl) continue;
-    const Top4& t = best[b];
-    // |v~ - v| for every listed value, with v = (|b|^2 + K)/2 - a.b exact and
-    // S = (|b|^2 + K)/2 + |a||b| <= U/2, U = (sqrt(K) + max|b|)^2, u = 2^-24: the norm and
-    // C roundings (D + 1) u S; the bf16x3 residual 3 2^-18 S; the fp32 accumulation of
-    // C and 3D exact bf16 products (rounding or truncating) (3D + 1) 2u 1.01 S; the key
-    // truncation kKeyTrunc S.  Sum <= (4 (D + 1) u + (3 2^-18 + kKeyTrunc) / 2) U, taken
-    // with margin as (5 (D + 2) u + 0.6 (3 2^-18 + kKeyTrunc)) U 1.02.
-    const float U = (sK + maxb) * (sK + maxb);
-    const float eps =
-        (5.f * (float)(D + 2) * 5.9604645e-8f + 0.6f * (1.1444092e-5f + kKeyTrunc)) * U * 1.02f + 1e-30f;
-    const float thr = t.v[1] + 2.f * eps;
-    int ncand;
-    if (!(t.v[1] < INFINITY)) {
-      ncand = t.v[0] < INFINITY ? 1 : 0;  // fewer than two frame rows: all are listed
-    } else if (t.v[2] > thr) {
-      ncand = 2;
-    } else if (t.v[3] > thr) {
-      ncand = 3;
-    } else {
-      ncand = -1;
-    }
-    const size_t o = ((size_t)f * n_tpl + i) * 2;
-    if (ncand < 0) {  // frame f's list (room for every template row)
-      const int slot = atomicAdd(&fb_cnt[f], 1);
-      fallback[(size_t)f * n_tpl + slot] = i;
-      continue;
-    }
-    float d0 = FLT_MAX, d1 = FLT_MAX;
-    int j0 = -1, j1 = -1;
-    const float* a = des_tpl + (size_t)i * D;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      if (k < ncand) {
-        const int j = t.j[k];
-        top2_insert_exact(d0, j0, d1, j1, exact_dist_any(a, base + (size_t)j * D, D), j);
-      }
-    }
-    out_idx[o] = j0;
-    out_idx[o + 1] = j1;
-    out_dist[o] = d0;
-    out_dist[o + 1] = d1;
+    for (int k = 2; k < kTop - 1; ++k) ncand += best.v[k] <= thr ? 1 : 0;
   }
+  const size_t o = ((size_t)f * n_tpl + i) * 2;
+  if (ncand < 0) {  // frame f's list (room for every template row)
+    const int slot = atomicAdd(&fb_cnt[f], 1);
+    fallback[(size_t)f * n_tpl + slot] = i;
+    return;
+  }
+  float d0 = FLT_MAX, d1 = FLT_MAX;
+  int j0 = -1, j1 = -1;
+  const float* a = des_tpl + (size_t)i * D;
+  const float* fb = des_q + (size_t)q_begin * D;
+#pragma unroll
+  for (int k = 0; k < kTop - 1; ++k) {
+    const int j = best.j[k];
+    if (k < ncand && (unsigned)j < (unsigned)n_q)  // (always in range; the guard keeps reads inside the frame)
+      top2_insert_exact(d0, j0, d1, j1, exact_dist_any(a, fb + (size_t)j * D, D), j);
+  }
+  out_idx[o] = j0;
+  out_idx[o + 1] = j1;
+  out_dist[o] = d0;
+  out_dist[o + 1] = d1;
 }
 
 // Exact brute force for the rows phase 1 could not certify: frame f's listed template
@@ -657,36 +720,45 @@ int check_f32_args(const void* des_tpl, int n_tpl, int D, const void* des_q, con
 int launch_knn_f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const float* des_q, const int32_t* q_off,
                    int n_frames, int max_nq, int32_t* out_idx, float* out_dist, hipStream_t s) {
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
-  // workspace: per-frame fallback counters and lists (room for every template row), K,
-  // the tiles' max |b|^2, then the tile images (tpf = ceil(max_nq / 32) per frame; the
-  // CSR total is a device value)
+  // workspace: per-frame fallback counters and lists (room for every template row), the
+  // template stats, the frames' scales and max |b|^2, then the tile images (tpf =
+  // ceil(max_nq / 64) per frame; the CSR total is a device value) and the fallback keys
   const size_t rows = (size_t)n_frames * n_tpl;
   const int tpf = ceil_div(max(max_nq, 0), kTile);
+  int tbits = 0;
+  while ((1 << tbits) < tpf) ++tbits;
+  const int key_bits = 5 + tbits;  // (tile << 5 | half << 4 | register)
+  if (key_bits > 20) return fail(KCMC_EUNSUPPORTED, "match_f32: more than 2^21 descriptors in one frame");
   const size_t cnt_bytes = ((size_t)n_frames * sizeof(int32_t) + 255) & ~(size_t)255;
   const size_t fb_bytes = (rows * sizeof(int32_t) + 255) & ~(size_t)255;
-  const size_t norm_bytes = (256 + (size_t)n_frames * tpf * sizeof(float) + 255) & ~(size_t)255;
+  const size_t stat_bytes = (256 + 3 * (size_t)n_frames * sizeof(float) + 255) & ~(size_t)255;
   const size_t img_bytes = (size_t)n_frames * tpf * kImgBytes;
   const size_t key_bytes = rows * 2 * sizeof(unsigned long long);  // the fallback's merged top-2 keys
   void* ws = nullptr;
-  KCMC_TRY(workspace_alloc(ctx, &ws, cnt_bytes + fb_bytes + norm_bytes + img_bytes + key_bytes, s));
+  KCMC_TRY(workspace_alloc(ctx, &ws, cnt_bytes + fb_bytes + stat_bytes + img_bytes + key_bytes, s));
   char* w = static_cast<char*>(ws);
   int32_t* fb_cnt = reinterpret_cast<int32_t*>(w);
   int32_t* fb = reinterpret_cast<int32_t*>(w + cnt_bytes);
-  unsigned* Kbits = reinterpret_cast<unsigned*>(w + cnt_bytes + fb_bytes);
-  float* tile_max = reinterpret_cast<float*>(w + cnt_bytes + fb_bytes + 256);
-  uint8_t* img = reinterpret_cast<uint8_t*>(w + cnt_bytes + fb_bytes + norm_bytes);
-  unsigned long long* fb_keys = reinterpret_cast<unsigned long long*>(w + cnt_bytes + fb_bytes + norm_bytes + img_bytes);
+  unsigned* Kst = reinterpret_cast<unsigned*>(w + cnt_bytes + fb_bytes);
+  unsigned* fmax = reinterpret_cast<unsigned*>(w + cnt_bytes + fb_bytes + 256);  // max |b|^2, max beta, bad flag
+  unsigned* fbeta = fmax + n_frames;
+  int32_t* fbad = reinterpret_cast<int32_t*>(fbeta + n_frames);
+  uint8_t* img = reinterpret_cast<uint8_t*>(w + cnt_bytes + fb_bytes + stat_bytes);
+  unsigned long long* fb_keys = reinterpret_cast<unsigned long long*>(w + cnt_bytes + fb_bytes + stat_bytes + img_bytes);
   KCMC_TRY(hip_check(hipMemsetAsync(fb_cnt, 0, (size_t)n_frames * sizeof(int32_t), s), "hipMemsetAsync"));
-  KCMC_TRY(hip_check(hipMemsetAsync(Kbits, 0, sizeof(unsigned), s), "hipMemsetAsync"));
-  hipLaunchKernelGGL(tpl_norm_max_kernel, dim3(ceil_div(n_tpl, 8)), dim3(256), 0, s, des_tpl, n_tpl, D, Kbits);
-  KCMC_TRY(launch_check("tpl_norm_max_kernel"));
+  KCMC_TRY(hip_check(hipMemsetAsync(Kst, 0, stat_bytes, s), "hipMemsetAsync"));
+  hipLaunchKernelGGL(tpl_stats_kernel, dim3(ceil_div(n_tpl, kTplRowsPerWG)), dim3(256), 0, s, des_tpl, n_tpl, D, Kst);
+  KCMC_TRY(launch_check("tpl_stats_kernel"));
+  hipLaunchKernelGGL(tpl_err_kernel, dim3(ceil_div(n_tpl, kTplRowsPerWG)), dim3(256), 0, s, des_tpl, n_tpl, D, Kst);
+  KCMC_TRY(launch_check("tpl_err_kernel"));
   if (tpf > 0) {
-    hipLaunchKernelGGL(split_tiles_kernel, dim3(tpf, n_frames), dim3(256), 0, s, des_q, D, q_off, tpf, Kbits, img,
-                       tile_max);
-    KCMC_TRY(launch_check("split_tiles_kernel"));
+    hipLaunchKernelGGL(frame_images_kernel, dim3(tpf, n_frames), dim3(kImgThreads), 0, s, des_q, D, q_off, tpf, Kst,
+                       img, fmax, fbeta, fbad);
+    KCMC_TRY(launch_check("frame_images_kernel"));
   }
   hipLaunchKernelGGL(knn2_l2f32_kernel, dim3(ceil_div(n_tpl, kTplPerWG), n_frames), dim3(kThreads), 0, s, des_tpl,
-                     n_tpl, D, des_q, q_off, img, tpf, Kbits, tile_max, out_idx, out_dist, fb, fb_cnt);
+                     n_tpl, D, des_q, q_off, img, tpf, Kst, reinterpret_cast<const float*>(fmax),
+                     reinterpret_cast<const float*>(fbeta), fbad, key_bits, out_idx, out_dist, fb, fb_cnt);
   KCMC_TRY(launch_check("knn2_l2f32_kernel"));
   KCMC_TRY(hip_check(hipMemsetAsync(fb_keys, 0xff, key_bytes, s), "hipMemsetAsync"));
   hipLaunchKernelGGL(knn2_l2f32_fallback_kernel, dim3(n_frames, kFbSplit, kFbLanes), dim3(kFbThreads), 0, s, des_tpl, n_tpl, D,

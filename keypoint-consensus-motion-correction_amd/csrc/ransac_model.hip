@@ -294,117 +294,6 @@ __device__ __forceinline__ float score_fast(const double (&h)[9], const Pts& P, 
   return S;
 }
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-// Phase A of the affine scoring in fp32 with a certified fallback (round 3).  With the
-// frame's coordinate maxima (ax, ay, adx, ady) and the trial's model h, every residual
-// component computed in fp32 from the fp32-rounded coordinates and model differs from the
-// fp64 one (resid2's operation order) by at most D = 10 u (max(|h0| ax + |h1| ay + |h2|,
-// |h3| ax + |h4| ay + |h5|) + max(adx, ady)), u = 2^-24 (input roundings, three roundings
-// per component, the final subtraction; x2 margin).  For q_f <= 2 tq each component is
-// <= sqrt(2 tq), so |q_f - q| <= 4 D sqrt(tq) + 2 D^2 + 8 u (tq + 1) =: B (x1.25 margin):
-//   q_f < tq - B  ->  an inlier;   q_f >= tq + B  ->  not one (for q_f > 2 tq this needs
-//   D <= 0.1 sqrt(tq), checked per trial);   otherwise the point is recomputed in fp64.
-// The counts are exact.  S32 = sum q_f: |S - S32| <= 2 D sqrt(2 N S32') + 2 N D^2 +
-// (N + 8) u S32' (Cauchy-Schwarz over the components, the fp32 sum, numpy's pairwise sum and
-// the squared correctly rounded roots), returned as the interval [lo, hi].  false: the
-// bounds do not hold (non-finite values, huge D) and the frame is scored exactly.
-// the next float towards -inf / +inf (finite x)
-__device__ __forceinline__ float next_down(float x) {
-  const int b = __float_as_int(x);
-  return x > 0.f ? __int_as_float(b - 1) : (x == 0.f ? -0x1p-149f : __int_as_float(b + 1));
-}
-__device__ __forceinline__ float next_up(float x) { return -next_down(-x); }
-
-struct AffineBounds {
-  float tq_lo, tq_hi;
-  double D;
-  bool ok;
-};
-
-__device__ __forceinline__ AffineBounds affine_bounds(const double (&h)[9], double ax, double ay, double adx,
-                                                      double ady, double tq) {
-  constexpr double u = 0x1p-24;
-  const double mx = fabs(h[0]) * ax + fabs(h[1]) * ay + fabs(h[2]);
-  const double my = fabs(h[3]) * ax + fabs(h[4]) * ay + fabs(h[5]);
-  const double D = 10.0 * u * (fmax(mx, my) + fmax(adx, ady)) + 0x1p-120;
-  const double st = sqrt(tq);
-  const double B = 1.25 * (4.0 * D * st + 2.0 * D * D + 8.0 * u * (tq + 1.0));
-  AffineBounds b;
-  b.D = D;
-  b.ok = D <= 0.1 * st && B < 0.5 * tq && mx < 1e30 && my < 1e30;
-  // directed conversions: tq_lo <= tq - B, tq_hi >= tq + B
-  float lo = (float)(tq - B), hi = (float)(tq + B);
-  if ((double)lo > tq - B) lo = next_down(lo);
-  if ((double)hi < tq + B) hi = next_up(hi);
-  b.tq_lo = lo;
-  b.tq_hi = hi;
-  return b;
-}
-
-struct AffineF32 {
-  f2v h03, h14, h25;
-};
-
-__device__ __forceinline__ float q_f32(const AffineF32& m, const float4 c) {
-  const f2v xx = {c.x, c.x}, yy = {c.y, c.y}, dd = {c.z, c.w};
-  f2v v = xx * m.h03;
-  v = __builtin_elementwise_fma(yy, m.h14, v);
-  v = v + m.h25;
-  const f2v e = v - dd;
-  const f2v e2 = e * e;
-  return e2.x + e2.y;
-}
-
-// Branch-free pass (counts of the certain inliers, sum of q_f, whether any point fell in
-// the band); only trials with a point in the band take the second pass, which decides those
-// points with the fp64 residual.
-__device__ __forceinline__ float score_fast_affine_f32(const double (&h)[9], const Pts& P, const float4* pf, int N,
-                                                       double tq, const AffineBounds& b, int& cnt) {
-  AffineF32 m;
-  m.h03 = f2v{(float)h[0], (float)h[3]};
-  m.h14 = f2v{(float)h[1], (float)h[4]};
-  m.h25 = f2v{(float)h[2], (float)h[5]};
-  const float lo = b.tq_lo, hi = b.tq_hi;
-  float S = 0.f;
-  int c = 0;
-  bool band = false;
-  int k = 0;
-  for (; k + 4 <= N; k += 4) {
-    const float4 p0 = pf[k], p1 = pf[k + 1], p2 = pf[k + 2], p3 = pf[k + 3];
-    const float q0 = q_f32(m, p0), q1 = q_f32(m, p1), q2 = q_f32(m, p2), q3 = q_f32(m, p3);
-    S += q0;
-    S += q1;
-    S += q2;
-    S += q3;
-    c += (int)(q0 < lo) + (int)(q1 < lo) + (int)(q2 < lo) + (int)(q3 < lo);
-    band |= (q0 >= lo && q0 < hi) | (q1 >= lo && q1 < hi) | (q2 >= lo && q2 < hi) | (q3 >= lo && q3 < hi);
-  }
-  for (; k < N; ++k) {
-    const float q = q_f32(m, pf[k]);
-    S += q;
-    c += (int)(q < lo);
-    band |= q >= lo && q < hi;
-  }
-  if (band) {
-    c = 0;
-    for (k = 0; k < N; ++k) {
-      const float q = q_f32(m, pf[k]);
-      if (q < lo) {
-        ++c;
-      } else if (q < hi) {
-        const double x = P.sx[k], y = P.sy[k];
-        const double X = fma(y, h[1], x * h[0]) + h[2];
-        const double Y = fma(y, h[4], x * h[3]) + h[5];
-        const double ex = X - P.dx[k], ey = Y - P.dy[k];
-        c += (ex * ex + ey * ey < tq) ? 1 : 0;
-      }
-    }
-  }
-  cnt += c;
-  return S;
-}
-
 template <int MODEL>
 __device__ __forceinline__ HModel fit_trial(const Pts& P, uint64_t pr) {
   if constexpr (MODEL == KCMC_MODEL_AFFINE) {
@@ -474,45 +363,24 @@ __device__ __forceinline__ void ransac_model_score_frame(
     return;
   }
 
-  // LDS: sx, sy, dx, dy [N] f64 | (x, y, dx, dy) [N] f32x4 | trial S (exact, or the lower
-  //      bound of phase A's interval) [T] f64 | phase A's upper bound [T] f64
-  //      | [LARGE: stack [kMaxStack][256] f64] | per-wave leaf values [4][128] f64 | trial count [T] i32
+  // LDS: sx, sy, dx, dy [N] f64 | trial S [T] f64 | [LARGE: stack [kMaxStack][256] f64]
+  //      | per-wave leaf values [4][128] f64 | trial count [T] i32
   double* sx = smem;
   double* sy = sx + N;
   double* dxs = sy + N;
   double* dys = dxs + N;
-  float4* pf = reinterpret_cast<float4*>(dys + N);
-  double* tS = reinterpret_cast<double*>(pf + N);
-  double* tSh = tS + T;
-  double* stk = tSh + T;
+  double* tS = dys + N;
+  double* stk = tS + T;
   double* wvals = stk + (LARGE ? kMaxStack * kThreads : 0);
   int* tC = reinterpret_cast<int*>(wvals + kThreads / 64 * 128);
-  __shared__ unsigned long long s_amax[4];  // max |x|, |y|, |dx|, |dy| (bit patterns of non-negative doubles)
   if (LARGE && tid == 0) {
     s_plan.n = 0;
     plan_gen<kPwDepth>(s_plan, 0, N);
   }
-  if (tid < 4) s_amax[tid] = 0ull;
-  __syncthreads();
-  double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;
-  for (int k = tid; k < N; k += kThreads) {
+  for (int k = tid; k < N; k += kThreads)
     gather_point(src, dst, pt_idx, src_stride, f, p0 + k, sx[k], sy[k], dxs[k], dys[k]);
-    pf[k] = make_float4((float)sx[k], (float)sy[k], (float)dxs[k], (float)dys[k]);
-    m0 = fmax(m0, fabs(sx[k]));
-    m1 = fmax(m1, fabs(sy[k]));
-    m2 = fmax(m2, fabs(dxs[k]));
-    m3 = fmax(m3, fabs(dys[k]));
-  }
-  if (MODEL == KCMC_MODEL_AFFINE) {
-    atomicMax(&s_amax[0], (unsigned long long)__double_as_longlong(m0));
-    atomicMax(&s_amax[1], (unsigned long long)__double_as_longlong(m1));
-    atomicMax(&s_amax[2], (unsigned long long)__double_as_longlong(m2));
-    atomicMax(&s_amax[3], (unsigned long long)__double_as_longlong(m3));
-  }
   if (tid == 0) s_any_zero = 0;
   __syncthreads();
-  const double ax = __longlong_as_double((long long)s_amax[0]), ay = __longlong_as_double((long long)s_amax[1]);
-  const double adx = __longlong_as_double((long long)s_amax[2]), ady = __longlong_as_double((long long)s_amax[3]);
 
   const Pts P{sx, sy, dxs, dys};
   const uint64_t* H = hyp + hoff;
@@ -524,37 +392,17 @@ __device__ __forceinline__ void ransac_model_score_frame(
   const bool fast = tq == tq;
   int mcount = -1, flag = fast ? 0 : 1;
   if (fast) {
-    const double eps = s32_eps(N);
     for (int t = tid; t < T; t += kThreads) {
       const HModel m = fit_trial<MODEL>(P, H[t]);
       int cnt = -1;
-      double lo = NAN, hi = NAN;
+      float S32 = NAN;
       if (m.ok) {
         cnt = 0;
-        if constexpr (MODEL == KCMC_MODEL_AFFINE) {
-          const AffineBounds b = affine_bounds(m.h, ax, ay, adx, ady, tq);
-          if (!b.ok) {
-            flag = 1;
-          } else {
-            const double S32 = (double)score_fast_affine_f32(m.h, P, pf, N, tq, b, cnt);
-            constexpr double u = 0x1p-24;
-            const double Sp = S32 * (1.0 + (N + 8) * u) + 1e-300;
-            const double e = 2.0 * b.D * sqrt(2.0 * N * Sp) * 1.01 + 2.0 * N * b.D * b.D + (N + 8) * u * Sp;
-            lo = S32 - e;
-            hi = S32 + e;
-            // S == 0 (skimage's early exit) and overflow need the exact path
-            if (!(lo > 0.0) || !(hi < 1e300)) flag = 1;
-          }
-        } else {
-          const float S32 = score_fast<MODEL>(m.h, P, N, tq, cnt);
-          if (!s32_certain(S32)) flag = 1;
-          lo = (double)S32 * (1.0 - eps);
-          hi = (double)S32 * (1.0 + eps);
-        }
+        S32 = score_fast<MODEL>(m.h, P, N, tq, cnt);
+        if (!s32_certain(S32)) flag = 1;
       }
       tC[t] = cnt;
-      tS[t] = lo;
-      tSh[t] = hi;
+      tS[t] = (double)S32;
       mcount = max(mcount, cnt);
     }
   }
@@ -611,9 +459,10 @@ __device__ __forceinline__ void ransac_model_score_frame(
       }
     }
   } else {
+    const double eps = s32_eps(N);
     double lm = INFINITY;
     for (int t = tid; t < T; t += kThreads)
-      if (tC[t] == mcount) lm = fmin(lm, tSh[t]);
+      if (tC[t] == mcount) lm = fmin(lm, tS[t] * (1.0 + eps));
     for (int o = 32; o > 0; o >>= 1) lm = fmin(lm, __shfl_xor(lm, o));
     if (lane == 0) s_min[wave] = lm;
     __syncthreads();
@@ -622,7 +471,7 @@ __device__ __forceinline__ void ransac_model_score_frame(
     double* wstk = stk + wave * kMaxStack;  // LARGE: the wave's combine stack
     for (int t0 = wave * 64; t0 < T; t0 += kThreads) {
       const int t = t0 + lane;
-      uint64_t cand = __ballot(t < T && tC[t] == mcount && tS[t] <= minhi);
+      uint64_t cand = __ballot(t < T && tC[t] == mcount && tS[t] * (1.0 - eps) <= minhi);
       while (cand) {
         const int tc = t0 + __builtin_ctzll(cand);
         cand &= cand - 1;
@@ -985,10 +834,9 @@ static int ransac_model_impl(kcmc_ctx* ctx, int model, const double* src, const 
   const int need = max_n < ms + 1 ? ms + 1 : max_n;
   const int n_small = need < 128 ? need : 128;
   const size_t wvals = (size_t)kThreads / 64 * 128 * sizeof(double);
-  const size_t per_pt = 4 * sizeof(double) + 4 * sizeof(float);
-  const size_t per_trial = 2 * sizeof(double) + sizeof(int);
-  const size_t lds_small = (size_t)n_small * per_pt + (size_t)trials * per_trial + wvals + 16;
-  const size_t lds_large = (size_t)need * per_pt + (size_t)trials * per_trial + wvals +
+  const size_t lds_small =
+      (size_t)n_small * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) + wvals + 16;
+  const size_t lds_large = (size_t)need * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) + wvals +
                            (size_t)kMaxStack * kThreads * sizeof(double) + 16;
   if ((max_n > 128 ? lds_large : lds_small) > 150 * 1024)
     return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_model: max_n/trials exceed the LDS budget");
