@@ -40,8 +40,12 @@ from kcmc_amd import pipeline, stages, synthetic  # noqa: E402
 
 METRIC = "aligned frames/sec (whole node) at 1080p; RANSAC hypotheses scored/sec/GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 / fp16 MFMA (MI355X_MICROARCH.md: the F16 forms take the same cycles)
 I8_PEAK_TOPS = 5000.0  # dense i8 MFMA: 2x the bf16 rate per clock (MI355X_MICROARCH.md)
+# wave64 VALU instructions per second per GPU: 256 CUs x 4 SIMDs x one per 4 cycles (the
+# integer ops of the matcher epilogues issue at this rate: SQ_ACTIVE_INST_VALU = 4 cycles
+# per instruction in the r03 PMC passes) x 2.4 GHz
+VALU_INSTR_PER_S_PER_GPU = 1024 * 0.25 * 2.4e9
 TRIALS = 1000
 ISOLATED_HEAD_START_CYCLES = 2_000_000  # spin ahead of the isolated match / RANSAC reps
 
@@ -373,6 +377,9 @@ def main():
                     help="RANSAC behind the warp on the one kernel stream (OverlappedSlabs corun=False)")
     ap.add_argument("--ransac-grid", type=int, default=None,
                     help="workgroups of the RANSAC launches beside the warp (default 0: one per frame)")
+    ap.add_argument("--match-beside", action="store_true",
+                    help="the match + vote also on the analysis stream, beside the warp (depth 3; "
+                         "OverlappedSlabs match_beside=True); default: the config's")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
@@ -410,7 +417,8 @@ def main():
 
     ov = None if args.serial else pipeline.OverlappedSlabs(dev, cfg, counts=counts if world > 1 else None,
                                                             depth=args.pipeline_depth, corun=not args.no_corun,
-                                                            ransac_grid=args.ransac_grid)
+                                                            ransac_grid=args.ransac_grid,
+                                                            match_beside=args.match_beside)
 
     def step(timer):
         if ov is None:
@@ -432,6 +440,8 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     timer = StageTimer()
+    if ov is not None:
+        ov.stats = {k: 0.0 for k in ov.stats}
     t0 = time.perf_counter()
     # K steps = K passes of match -> consensus -> RANSAC -> post-processing -> warp; the
     # pipelined schedule starts empty and is drained inside the timed region
@@ -469,11 +479,18 @@ def main():
     if ov is None:
         stage_ms["host_and_transfers"] = round(ms_step - match_ms - ransac_ms - warp_ms, 3)
     else:  # step k+1's match/consensus/RANSAC/post-processing overlap step k's warp
-        stage_ms["schedule"] = ("pipelined: match+vote(k) -> warp(k-1) -> lookup+RANSAC(k)" if args.pipeline_depth == 2 else
-                                "pipelined: match+vote(k) -> warp(k-2) -> lookup+RANSAC(k-1)") + (
-                                    " on one stream" if args.no_corun else ", RANSAC on a second stream beside the warp"
-                                ) + ", host consensus merge under the warp"
+        if args.match_beside:
+            stage_ms["schedule"] = ("pipelined: kernel stream warp(k-2); analysis stream lookup+RANSAC(k-1) -> "
+                                    "match+vote(k) beside it; host consensus merge under the warp")
+        else:
+            stage_ms["schedule"] = ("pipelined: match+vote(k) -> warp(k-1) -> lookup+RANSAC(k)" if args.pipeline_depth == 2
+                                    else "pipelined: match+vote(k) -> warp(k-2) -> lookup+RANSAC(k-1)") + (
+                                        " on one stream" if args.no_corun else ", RANSAC on a second stream beside the warp"
+                                    ) + ", host consensus merge under the warp"
         stage_ms["step_minus_warp"] = round(ms_step - warp_ms, 3)
+        # rank 0's host seconds per step blocked in event waits / inside the all-gathers, and
+        # its consensus merge / post-processing (OverlappedSlabs.stats)
+        stage_ms["host_ms_per_step_rank0"] = {k: round(1e3 * v / args.steps, 4) for k, v in ov.stats.items()}
     result = {
         "metric": METRIC,
         "value": round(fps, 1),
@@ -485,7 +502,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("u16 frames; " + ("f32 descriptors: bf16x3 MFMA candidate search + exact f64 re-rank"
+        "dtype": ("u16 frames; " + ("f32 descriptors: fp16 MFMA candidate search (certified bound) + exact f64 re-rank"
                                     if bc.descriptor == "f32" else "u8 descriptors: i8 MFMA exact integer distances")
                   + ", f64 RANSAC, f32 warp weights"),
         "data": "synthetic (seeded jittered 1080p texture + ORB-shaped keypoints; no detector in image)",
@@ -524,26 +541,45 @@ def main():
             "avg_launch_ms": round(warp_ms, 4),
         },
     }
-    # the matcher against its MFMA roofline (the dominant kernel of c5): algorithmic work
-    # 2 * n_tpl * n_q * D per frame; the float matcher issues three bf16 products per
-    # fp32 product, so its issued MFMA work is 3x that and is priced against bf16 dense
+    # the matcher against its rooflines (the dominant kernel of c5): algorithmic work
+    # 2 * n_tpl * n_q * D per frame.  The float matcher issues one fp16 product per fp32
+    # product (a certified candidate search; exact fp64 re-rank of 2-3 candidates), priced
+    # against fp16 dense (= bf16 dense); its bound is the top-6 selection on VALU (8 integer
+    # VALU per distance), reported beside it
     n_q_total = float(inp.q_off_host[-1])
     match_ops = 2.0 * bc.n_tpl * n_q_total * bc.D
     iso_match_s = iso["match"] * 1e-3
     if bc.descriptor == "f32":
-        issued = 3.0 * match_ops / iso_match_s / 1e12
+        issued = match_ops / iso_match_s / 1e12
+        dists = match_ops / (2.0 * bc.D) / iso_match_s / 1e12
+        valu_peak = VALU_INSTR_PER_S_PER_GPU * 64 / 8.0 / 1e12
         result["roofline_match"] = {
-            "kernel": "split_rows_kernel + knn2_l2f32_kernel + rerank + match_filter_kernel (whole match stage)",
-            "bound": "mfma", "achieved": round(issued, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "kernel": "tpl_stats + frame_images + knn2_l2f32_kernel (fp16 MFMA, top-6, exact re-rank) + fallback "
+                      "+ match_filter (whole match stage)",
+            "bound": "valu", "achieved": round(issued, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(issued / BF16_PEAK_TFLOPS, 4), "traffic": None,
-            "algorithmic_tflops_fp32_equiv": round(match_ops / iso_match_s / 1e12, 1),
-            "avg_launch_ms": iso["match"], "note": "achieved = issued bf16 MFMA work (3 x algorithmic) / isolated stage time"}
+            "algorithmic_tflops_fp32_equiv": round(issued, 1),
+            "avg_launch_ms": iso["match"],
+            "valu_bound": {"distances_per_s_T": round(dists, 3), "peak_distances_per_s_T": round(valu_peak, 3),
+                           "frac": round(dists / valu_peak, 4),
+                           "note": "peak = 1024 SIMDs x 0.25 wave64 VALU instr/cycle x 2.4 GHz x 64 lanes / 8 VALU "
+                                   "per distance (key + top-6 insertion)"},
+            "note": "achieved = issued fp16 MFMA work (= algorithmic) / isolated stage time; frac against dense fp16"}
     else:
         tops = match_ops / iso_match_s / 1e12
+        # knn2_l2u8 is bound by its integer VALU top-2 epilogue (~2.5 VALU per distance), not
+        # by the i8 MFMA: the MFMA fraction is reported beside the VALU-issue one
+        valu_per_dist = 2.5
+        valu_peak = VALU_INSTR_PER_S_PER_GPU * 64 / valu_per_dist / 1e12  # distances/s (T)
+        dists = match_ops / (2.0 * bc.D) / iso_match_s / 1e12
         result["roofline_match"] = {
-            "kernel": "knn2_l2u8_kernel + match_filter_kernel (whole match stage)", "bound": "mfma",
+            "kernel": "knn2_l2u8_kernel + match_filter_kernel (whole match stage)", "bound": "valu",
             "achieved": round(tops, 1), "peak": I8_PEAK_TOPS, "unit": "TOP/s", "frac": round(tops / I8_PEAK_TOPS, 4),
-            "traffic": None, "avg_launch_ms": iso["match"]}
+            "traffic": None, "avg_launch_ms": iso["match"],
+            "valu_bound": {"distances_per_s_T": round(dists, 3), "peak_distances_per_s_T": round(valu_peak, 3),
+                           "frac": round(dists / valu_peak, 4),
+                           "note": "peak = 1024 SIMDs x 0.25 wave64 VALU instr/cycle x 2.4 GHz x 64 lanes / "
+                                   "2.5 VALU per distance (the top-2 epilogue); frac/peak above = i8 MFMA"}}
     if args.e2e:
         result["end_to_end"] = end_to_end(bc, inp, cfg, dev, world)
     if args.detect and bc.C == 1:

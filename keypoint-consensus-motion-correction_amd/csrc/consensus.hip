@@ -232,17 +232,29 @@ __global__ __launch_bounds__(kCountThreads) void lookup_count_kernel(const uint3
 // slot as soon as one tile retires, a 1024-thread one waited ~0.43 ms for 16 free slots on
 // one CU (c3 trace).
 __global__ __launch_bounds__(64) void lookup_scan_kernel(int F, int32_t* __restrict__ pt_off) {
+  // 1024 frames per pass, 16 consecutive ones per lane: the 16 loads of a lane are in
+  // flight together (a pass per 64 frames waited on one load at a time: ~40 us at F = 2500)
+  constexpr int kPer = 16;
   const int lane = threadIdx.x;
   if (lane == 0) pt_off[0] = 0;
+  int32_t* c = pt_off + 1;
   int carry = 0;
-  for (int base = 0; base < F; base += 64) {
-    const int f = base + lane;
-    int x = f < F ? pt_off[f + 1] : 0;
+  for (int base = 0; base < F; base += 64 * kPer) {
+    const int f0 = base + lane * kPer;
+    int v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) v[k] = f0 + k < F ? c[f0 + k] : 0;
+#pragma unroll
+    for (int k = 1; k < kPer; ++k) v[k] += v[k - 1];
+    int x = v[kPer - 1];  // inclusive prefix of the lane totals
     for (int d = 1; d < 64; d <<= 1) {
       const int y = __shfl_up(x, d, 64);
       if (lane >= d) x += y;
     }
-    if (f < F) pt_off[f + 1] = carry + x;
+    const int before = carry + x - v[kPer - 1];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      if (f0 + k < F) c[f0 + k] = before + v[k];
     carry += __shfl(x, 63, 64);
   }
 }

@@ -11,7 +11,7 @@
 //   row and Q = sum(y^2 + 2y) per frame row.  One v_mfma_i32_32x32x32_i8 pass per
 //   32-deep k-step gives x.y (accumulator from zero).  T is constant along a template
 //   column, so a column's frame rows are ordered by SSD - T + B = Q + 2 x.y + B, with
-//   B = 2^20 > max T making it non-negative (< 2^23).  A operand = 32 frame
+//   B = 2^20 = max T; the key is non-negative because SSD >= 0 (and < 2^23).  A operand = 32 frame
 //   descriptors (rows j), B operand = 32 template descriptors (columns i): each lane
 //   owns one template column and 16 frame rows of the 32x32 tile and keeps a running
 //   top-2 in registers.
@@ -457,6 +457,121 @@ __global__ __launch_bounds__(kFilterThreads) void match_filter_kernel(
   }
 }
 
+// The same filters for n_tpl <= 512 with ONE wave per frame and no barrier: template i =
+// 64 k + lane sits in the lane's register k (k < 8), and the median of the ratio survivors
+// comes from a bitonic sort of all 512 register slots (non-survivors +inf) across the wave
+// (stride < 8: within a lane; >= 8: shuffles with lane ^ stride / 8), so the survivors need
+// no compaction: the sorted slots 0 .. nr - 1 are their sorted displacements.  The
+// barrier-per-stage sort of the workgroup kernel waited ~40 us per launch at c2 / c3.
+constexpr int kFilterWaveFrames = 4;  // frames (waves) per 256-thread workgroup
+
+__device__ __forceinline__ void cmpx(double& a, double& b, bool asc) {
+  const double lo = fmin(a, b), hi = fmax(a, b);
+  a = asc ? lo : hi;
+  b = asc ? hi : lo;
+}
+
+__global__ __launch_bounds__(64 * kFilterWaveFrames) void match_filter_wave_kernel(
+    const int32_t* __restrict__ idx, const float* __restrict__ dist, const double* __restrict__ kp_tpl,
+    const double* __restrict__ kp_q, const int32_t* __restrict__ q_off, int n_frames, int n_tpl, double ratio,
+    double d_lo, double d_hi, double* __restrict__ kp_ordered, uint32_t* __restrict__ keep_bits,
+    int32_t* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * kFilterWaveFrames + (threadIdx.x >> 6);
+  if (f >= n_frames) return;  // the whole wave
+  const int q_begin = q_off[f];
+  const int words = (n_tpl + 31) >> 5;
+  // pass 1: reorder (VA:197-200), ratio filter (VA:202-203), displacement of survivors (VA:208)
+  double dv[8];
+  uint64_t okm[8];
+  int nr = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int i = 64 * k + lane;
+    bool ok = false;
+    double d = INFINITY;
+    if (i < n_tpl) {
+      const size_t o = ((size_t)f * n_tpl + i) * 2;
+      const int j0 = idx[o];
+      double qx = 0.0, qy = 0.0;
+      if (j0 >= 0) {
+        qx = kp_q[2 * (size_t)(q_begin + j0)];
+        qy = kp_q[2 * (size_t)(q_begin + j0) + 1];
+      }
+      kp_ordered[((size_t)f * n_tpl + i) * 2] = qx;
+      kp_ordered[((size_t)f * n_tpl + i) * 2 + 1] = qy;
+      ok = (double)dist[o] < ratio * (double)dist[o + 1];
+      if (ok) {
+        const double dx = kp_tpl[2 * i] - qx, dy = kp_tpl[2 * i + 1] - qy;
+        d = sqrt(dx * dx + dy * dy);
+      }
+    }
+    dv[k] = d;
+    okm[k] = __ballot(ok);
+    nr += __popcll(okm[k]);
+  }
+  // bitonic sort (ascending) of the 512 slots e = 8 lane + k
+  double v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = dv[k];
+#pragma unroll
+  for (int size = 2; size <= 512; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= 8) {
+        const int ls = stride >> 3;
+        const bool lower = (lane & ls) == 0;
+        const bool asc = size >= 16 ? (lane & (size >> 3)) == 0 : true;  // (e & size) == 0
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const double o = __shfl_xor(v[k], ls, 64);
+          v[k] = (lower == asc) ? fmin(v[k], o) : fmax(v[k], o);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if ((k & stride) == 0) {
+            const bool asc = size >= 8 ? (lane & (size >> 3)) == 0 : (k & size) == 0;  // (e & size) == 0
+            cmpx(v[k], v[k | stride], asc);
+          }
+        }
+      }
+    }
+  }
+  // the median of the nr survivors: sorted slots (nr - 1) / 2 and nr / 2 (np.median, VA:210)
+  double med = 0.0;
+  if (nr > 0) {
+    auto slot = [&](int e) -> double {
+      double x = v[0];
+#pragma unroll
+      for (int k = 1; k < 8; ++k)
+        if ((e & 7) == k) x = v[k];  // wave-uniform
+      return __shfl(x, e >> 3, 64);
+    };
+    const double b = slot(nr >> 1);
+    med = (nr & 1) ? b : (slot((nr >> 1) - 1) + b) / 2.0;
+  }
+  const double lo = d_lo * med, hi = d_hi * med;
+  // pass 2: keep = ratio survivor and lo <= d <= hi (VA:210); bitmask + counts
+  int nk = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool keep = nr > 0 && ((okm[k] >> lane) & 1ull) && lo <= dv[k] && dv[k] <= hi;
+    const uint64_t m = __ballot(keep);
+    nk += __popcll(m);
+    if (lane == 0) {
+      if (2 * k < words) keep_bits[(size_t)f * words + 2 * k] = (uint32_t)m;
+      if (2 * k + 1 < words) keep_bits[(size_t)f * words + 2 * k + 1] = (uint32_t)(m >> 32);
+    }
+  }
+  if (lane == 0) {
+    counts[4 * (size_t)f + 0] = n_tpl;  // len(kp_query) after the reorder at VA:200
+    counts[4 * (size_t)f + 1] = n_tpl;  // len(matches)
+    counts[4 * (size_t)f + 2] = nr;
+    counts[4 * (size_t)f + 3] = nk;
+  }
+}
+
 // Workgroups that fill the device once (2 per CU at 8 waves, 4 at 4 waves: the kernels'
 // ~100 VGPRs allow 4 waves per SIMD), split evenly over the template groups.
 
@@ -516,6 +631,12 @@ int check_match_args(const void* des_tpl, int n_tpl, int D, const void* des_q, c
 int launch_match_filter(const int32_t* idx, const float* dist, const double* kp_tpl, const double* kp_q,
                         const int32_t* q_off, int n_frames, int n_tpl, double ratio, double d_lo, double d_hi,
                         double* kp_ordered, uint32_t* keep_bits, int32_t* counts, hipStream_t s) {
+  if (n_tpl <= 512) {
+    hipLaunchKernelGGL(match_filter_wave_kernel, dim3(ceil_div(n_frames, kFilterWaveFrames)),
+                       dim3(64 * kFilterWaveFrames), 0, s, idx, dist, kp_tpl, kp_q, q_off, n_frames, n_tpl, ratio,
+                       d_lo, d_hi, kp_ordered, keep_bits, counts);
+    return launch_check("match_filter_wave_kernel");
+  }
   int P = 1;
   while (P < n_tpl) P <<= 1;
   hipLaunchKernelGGL(match_filter_kernel, dim3(n_frames), dim3(kFilterThreads), (size_t)P * sizeof(double), s, idx,

@@ -375,8 +375,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     const float* __restrict__ des_tpl, int n_tpl, int D, const float* __restrict__ des_q,
     const int32_t* __restrict__ q_off, const uint8_t* __restrict__ img, int tpf,
     const unsigned* __restrict__ Kst, const float* __restrict__ fmax, const float* __restrict__ fbeta,
-    const int32_t* __restrict__ fbad, int key_bits, int32_t* __restrict__ out_idx, float* __restrict__ out_dist, int32_t* __restrict__ fallback,
-    int32_t* __restrict__ fb_cnt) {
+    const int32_t* __restrict__ fbad, int key_bits, int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
+    int32_t* __restrict__ fallback, int32_t* __restrict__ fb_cnt, int32_t* __restrict__ fb_frames,
+    unsigned long long* __restrict__ fb_keys) {
   __shared__ __attribute__((aligned(16))) uint8_t tbuf[kNBuf][kImgBytes];
 
   // XCD-aware order: the workgroups of one frame get consecutive ids of one XCD's run
@@ -526,6 +527,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
   if (ncand < 0) {  // frame f's list (room for every template row)
     const int slot = atomicAdd(&fb_cnt[f], 1);
     fallback[(size_t)f * n_tpl + slot] = i;
+    fb_keys[2 * ((size_t)f * n_tpl + slot)] = ~0ull;  // the merge keys of the entry start empty
+    fb_keys[2 * ((size_t)f * n_tpl + slot) + 1] = ~0ull;
+    if (slot == 0) fb_frames[1 + atomicAdd(&fb_frames[0], 1)] = f;  // the frame's first entry lists it
     return;
   }
   float d0 = FLT_MAX, d1 = FLT_MAX;
@@ -612,19 +616,24 @@ __global__ __launch_bounds__(kFbThreads) void knn2_l2f32_fallback_kernel(const f
                                                                          const int32_t* __restrict__ q_off,
                                                                          const int32_t* __restrict__ fb,
                                                                          const int32_t* __restrict__ fb_cnt,
+                                                                         const int32_t* __restrict__ fb_frames,
                                                                          unsigned long long* __restrict__ fb_keys) {
   __shared__ __attribute__((aligned(16))) float sa[kFbBatch][kDP];
   __shared__ float sd[kFbThreads / 64][kFbBatch][2];
   __shared__ int sj[kFbThreads / 64][kFbBatch][2];
-  const int f = blockIdx.x;
-  const int cnt = fb_cnt[f];
-  if (cnt <= (int)blockIdx.z * kFbBatch) return;  // the whole workgroup: no batch for it
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int q_begin = q_off[f], n_q = q_off[f + 1] - q_begin;
-  const int j_lo = (int)((long long)n_q * blockIdx.y / kFbSplit);
-  const int j_hi = (int)((long long)n_q * (blockIdx.y + 1) / kFbSplit);
   const bool v4 = (D & 3) == 0 && (reinterpret_cast<uintptr_t>(des_q) & 15) == 0;
-  for (int k0 = blockIdx.z * kFbBatch; k0 < cnt; k0 += kFbLanes * kFbBatch) {
+  // work items (listed frame, slice y, batch lane z), grid-stride: only the frames with
+  // listed rows are visited (a grid over every frame launched ~32k mostly idle workgroups)
+  const int n_items = fb_frames[0] * kFbSplit * kFbLanes;
+  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+  const int f = fb_frames[1 + item / (kFbSplit * kFbLanes)];
+  const int y = (item / kFbLanes) % kFbSplit, z = item % kFbLanes;
+  const int cnt = fb_cnt[f];
+  const int q_begin = q_off[f], n_q = q_off[f + 1] - q_begin;
+  const int j_lo = (int)((long long)n_q * y / kFbSplit);
+  const int j_hi = (int)((long long)n_q * (y + 1) / kFbSplit);
+  for (int k0 = z * kFbBatch; k0 < cnt; k0 += kFbLanes * kFbBatch) {
     const int nb = min(kFbBatch, cnt - k0);
     __syncthreads();  // the previous batch's merge is done with sa / sd / sj
     for (int e = tid; e < kFbBatch * kDP; e += kFbThreads) {
@@ -682,25 +691,30 @@ __global__ __launch_bounds__(kFbThreads) void knn2_l2f32_fallback_kernel(const f
       }
     }
   }
+  }
 }
 
-// The listed rows' merged keys -> out_idx / out_dist (no key: index -1, FLT_MAX).
+// The listed rows' merged keys -> out_idx / out_dist (no key: index -1, FLT_MAX); one
+// workgroup per listed frame, grid-stride.
 __global__ __launch_bounds__(256) void knn2_l2f32_fallback_out_kernel(int n_tpl, const int32_t* __restrict__ fb,
                                                                       const int32_t* __restrict__ fb_cnt,
+                                                                      const int32_t* __restrict__ fb_frames,
                                                                       const unsigned long long* __restrict__ fb_keys,
                                                                       int32_t* __restrict__ out_idx,
                                                                       float* __restrict__ out_dist) {
-  const int f = blockIdx.x;
-  const int cnt = fb_cnt[f];
-  for (int k = threadIdx.x; k < cnt; k += 256) {
-    const size_t slot = (size_t)f * n_tpl + k;
-    const size_t o = ((size_t)f * n_tpl + fb[slot]) * 2;
+  for (int q = blockIdx.x; q < fb_frames[0]; q += gridDim.x) {
+    const int f = fb_frames[1 + q];
+    const int cnt = fb_cnt[f];
+    for (int k = threadIdx.x; k < cnt; k += 256) {
+      const size_t slot = (size_t)f * n_tpl + k;
+      const size_t o = ((size_t)f * n_tpl + fb[slot]) * 2;
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const unsigned long long key = fb_keys[2 * slot + r];
-      const bool ok = key != ~0ull;
-      out_idx[o + r] = ok ? (int32_t)(uint32_t)key : -1;
-      out_dist[o + r] = ok ? __uint_as_float((uint32_t)(key >> 32)) : FLT_MAX;
+      for (int r = 0; r < 2; ++r) {
+        const unsigned long long key = fb_keys[2 * slot + r];
+        const bool ok = key != ~0ull;
+        out_idx[o + r] = ok ? (int32_t)(uint32_t)key : -1;
+        out_dist[o + r] = ok ? __uint_as_float((uint32_t)(key >> 32)) : FLT_MAX;
+      }
     }
   }
 }
@@ -720,16 +734,17 @@ int check_f32_args(const void* des_tpl, int n_tpl, int D, const void* des_q, con
 int launch_knn_f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const float* des_q, const int32_t* q_off,
                    int n_frames, int max_nq, int32_t* out_idx, float* out_dist, hipStream_t s) {
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
-  // workspace: per-frame fallback counters and lists (room for every template row), the
-  // template stats, the frames' scales and max |b|^2, then the tile images (tpf =
-  // ceil(max_nq / 64) per frame; the CSR total is a device value) and the fallback keys
+  // workspace: per-frame fallback counters, the listed frames (count + ids) and the lists
+  // (room for every template row), the template stats, the frames' max |b|^2 / max beta /
+  // bad flags, then the tile images (tpf = ceil(max_nq / 64) per frame; the CSR total is a
+  // device value) and the fallback merge keys (set by the matcher when it lists a row)
   const size_t rows = (size_t)n_frames * n_tpl;
   const int tpf = ceil_div(max(max_nq, 0), kTile);
   int tbits = 0;
   while ((1 << tbits) < tpf) ++tbits;
   const int key_bits = 5 + tbits;  // (tile << 5 | half << 4 | register)
   if (key_bits > 20) return fail(KCMC_EUNSUPPORTED, "match_f32: more than 2^21 descriptors in one frame");
-  const size_t cnt_bytes = ((size_t)n_frames * sizeof(int32_t) + 255) & ~(size_t)255;
+  const size_t cnt_bytes = ((2 * (size_t)n_frames + 1) * sizeof(int32_t) + 255) & ~(size_t)255;
   const size_t fb_bytes = (rows * sizeof(int32_t) + 255) & ~(size_t)255;
   const size_t stat_bytes = (256 + 3 * (size_t)n_frames * sizeof(float) + 255) & ~(size_t)255;
   const size_t img_bytes = (size_t)n_frames * tpf * kImgBytes;
@@ -745,7 +760,8 @@ int launch_knn_f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const 
   int32_t* fbad = reinterpret_cast<int32_t*>(fbeta + n_frames);
   uint8_t* img = reinterpret_cast<uint8_t*>(w + cnt_bytes + fb_bytes + stat_bytes);
   unsigned long long* fb_keys = reinterpret_cast<unsigned long long*>(w + cnt_bytes + fb_bytes + stat_bytes + img_bytes);
-  KCMC_TRY(hip_check(hipMemsetAsync(fb_cnt, 0, (size_t)n_frames * sizeof(int32_t), s), "hipMemsetAsync"));
+  int32_t* fb_frames = fb_cnt + n_frames;
+  KCMC_TRY(hip_check(hipMemsetAsync(fb_cnt, 0, (size_t)(n_frames + 1) * sizeof(int32_t), s), "hipMemsetAsync"));
   KCMC_TRY(hip_check(hipMemsetAsync(Kst, 0, stat_bytes, s), "hipMemsetAsync"));
   hipLaunchKernelGGL(tpl_stats_kernel, dim3(ceil_div(n_tpl, kTplRowsPerWG)), dim3(256), 0, s, des_tpl, n_tpl, D, Kst);
   KCMC_TRY(launch_check("tpl_stats_kernel"));
@@ -758,14 +774,15 @@ int launch_knn_f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const 
   }
   hipLaunchKernelGGL(knn2_l2f32_kernel, dim3(ceil_div(n_tpl, kTplPerWG), n_frames), dim3(kThreads), 0, s, des_tpl,
                      n_tpl, D, des_q, q_off, img, tpf, Kst, reinterpret_cast<const float*>(fmax),
-                     reinterpret_cast<const float*>(fbeta), fbad, key_bits, out_idx, out_dist, fb, fb_cnt);
+                     reinterpret_cast<const float*>(fbeta), fbad, key_bits, out_idx, out_dist, fb, fb_cnt, fb_frames,
+                     fb_keys);
   KCMC_TRY(launch_check("knn2_l2f32_kernel"));
-  KCMC_TRY(hip_check(hipMemsetAsync(fb_keys, 0xff, key_bytes, s), "hipMemsetAsync"));
-  hipLaunchKernelGGL(knn2_l2f32_fallback_kernel, dim3(n_frames, kFbSplit, kFbLanes), dim3(kFbThreads), 0, s, des_tpl, n_tpl, D,
-                     des_q, q_off, fb, fb_cnt, fb_keys);
+  const int fb_grid = min(n_frames * kFbSplit * kFbLanes, 4 * device_cus());
+  hipLaunchKernelGGL(knn2_l2f32_fallback_kernel, dim3(fb_grid), dim3(kFbThreads), 0, s, des_tpl, n_tpl, D, des_q, q_off,
+                     fb, fb_cnt, fb_frames, fb_keys);
   KCMC_TRY(launch_check("knn2_l2f32_fallback_kernel"));
-  hipLaunchKernelGGL(knn2_l2f32_fallback_out_kernel, dim3(n_frames), dim3(256), 0, s, n_tpl, fb, fb_cnt, fb_keys,
-                     out_idx, out_dist);
+  hipLaunchKernelGGL(knn2_l2f32_fallback_out_kernel, dim3(min(n_frames, 1024)), dim3(256), 0, s, n_tpl, fb, fb_cnt,
+                     fb_frames, fb_keys, out_idx, out_dist);
   KCMC_TRY(launch_check("knn2_l2f32_fallback_out_kernel"));
   return workspace_free(ctx, ws, s);
 }

@@ -400,10 +400,15 @@ class OverlappedSlabs:
 
     def __init__(self, device, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
                  counts: Optional[List[int]] = None, group=None, depth: int = 2, corun: bool = True,
-                 ransac_grid: Optional[int] = None):
+                 ransac_grid: Optional[int] = None, match_beside: bool = False):
         if depth not in (2, 3):
             raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
+        if match_beside and not (corun and depth == 3):
+            raise ValueError("match_beside needs corun=True and depth=3")
         self.depth = depth
+        # match_beside: the match + vote of slab k also run on the analysis stream (behind
+        # lookup + RANSAC(k-1)), so the kernel stream carries only the warps
+        self.match_beside = bool(match_beside)
         if counts is not None and len(counts) > 1 and cfg.frame_downsample_rate != 1:
             # the rank's first frame is counted in sample frames, the affines in full-rate
             # frames: the same restriction as distributed.align_sharded
@@ -506,6 +511,15 @@ class OverlappedSlabs:
             for t in (inp.frames, out):
                 if t is not None:
                     t.record_stream(self.stream)
+            if self.match_beside:
+                # kernel stream: warp(k-2); analysis stream: lookup + RANSAC(k-1) -> match(k)
+                fitted, self._fitted = self._fitted, None
+                if fitted is not None and self._device_maps():
+                    self._warp_device_maps(fitted, mark)
+                if self._matched is not None:
+                    self._fitted = self._fit(self._matched, mark)
+                self._matched = self._match(inp, out, mark)
+                return self._finish(fitted, mark) if fitted is not None else None
             new = self._match(inp, out, mark)
             fitted, self._fitted = self._fitted, None
             if fitted is not None and self._device_maps():
@@ -530,10 +544,14 @@ class OverlappedSlabs:
         ev = torch.cuda.Event()
         ev.record(cur)
         self.stream.wait_event(ev)
+        if self.match_beside:  # the analysis stream reads the slab's keypoints
+            self.ana.wait_event(ev)
         self._queued()
 
     def _match(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
         """match(k) and its vote on the kernel stream; the (gathered) votes to the host."""
+        if self.match_beside:
+            return self._match_beside(inp, out, mark)
         self._at_tail(mark, "m0")
         match = match_stage(inp, self.cfg, stream=self._hs)
         n_tpl = inp.des_tpl.shape[0]
@@ -544,6 +562,27 @@ class OverlappedSlabs:
             votes = self._gather(votes)  # the kernel stream waits for the collective
             self._queued()
         ready = self._at_tail(mark)
+        slot = self._slots.pop() if self._slots else _Slot()
+        self._d2h(slot.buf("votes", votes.numel(), torch.int64), votes, ready, slot.votes_ev)
+        return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=matched)
+
+    def _match_beside(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
+        """match(k) and its vote on the analysis stream (allocated there), behind the lookup +
+        RANSAC of the previous slab; the (gathered) votes to the host."""
+        n_tpl = inp.des_tpl.shape[0]
+        with torch.cuda.stream(self.ana):
+            m0 = torch.cuda.Event(enable_timing=True)
+            m0.record(self.ana)
+            mark("m0", m0)
+            match = match_stage(inp, self.cfg, stream=self._ha)
+            votes = stages.consensus_vote(match.keep_bits, n_tpl, self._f0, stream=self._ha)
+            matched = torch.cuda.Event(enable_timing=True)
+            matched.record(self.ana)
+            mark("m1", matched)
+            if self._sharded():
+                votes = self._gather(votes)  # the analysis stream waits for the collective
+            ready = torch.cuda.Event()
+            ready.record(self.ana)
         slot = self._slots.pop() if self._slots else _Slot()
         self._d2h(slot.buf("votes", votes.numel(), torch.int64), votes, ready, slot.votes_ev)
         return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=matched)

@@ -33,6 +33,12 @@ int workspace_alloc(kcmc_ctx*, void** p, size_t n, hipStream_t) {
 }
 int workspace_free(kcmc_ctx*, void*, hipStream_t, size_t) { return 0; }
 #ifdef KNN_F32  // match_f32.hip's kcmc_match_frames_f32 calls match.hip's filter launcher
+int device_cus() {
+  int d = 0, n = 256;
+  (void)hipGetDevice(&d);
+  (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
+  return n;
+}
 int launch_match_filter(const int32_t*, const float*, const double*, const double*, const int32_t*, int, int, double,
                         double, double, double*, uint32_t*, int32_t*, hipStream_t) {
   return KCMC_EUNSUPPORTED;
