@@ -480,8 +480,8 @@ def main():
         stage_ms["host_and_transfers"] = round(ms_step - match_ms - ransac_ms - warp_ms, 3)
     else:  # step k+1's match/consensus/RANSAC/post-processing overlap step k's warp
         if args.match_beside:
-            stage_ms["schedule"] = ("pipelined: kernel stream warp(k-2); analysis stream lookup+RANSAC(k-1) -> "
-                                    "match+vote(k) beside it; host consensus merge under the warp")
+            stage_ms["schedule"] = ("pipelined: kernel stream warp(k-2); analysis stream match+vote(k) -> "
+                                    "lookup+RANSAC(k-1) beside it; host consensus merge under the warp")
         else:
             stage_ms["schedule"] = ("pipelined: match+vote(k) -> warp(k-1) -> lookup+RANSAC(k)" if args.pipeline_depth == 2
                                     else "pipelined: match+vote(k) -> warp(k-2) -> lookup+RANSAC(k-1)") + (

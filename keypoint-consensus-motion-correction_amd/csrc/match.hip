@@ -572,6 +572,134 @@ __global__ __launch_bounds__(64 * kFilterWaveFrames) void match_filter_wave_kern
   }
 }
 
+// The same for 512 < n_tpl <= 4096: one 512-thread workgroup per frame, template
+// i = 512 k + tid in register k of thread tid, and a 4096-slot bitonic sort (slot
+// e = 8 tid + k): strides < 8 within a thread, < 512 by shuffles inside a wave, and only
+// the strides 512..2048 (6 of the 78 stages) through LDS with barriers (the workgroup
+// kernel above synchronises at all 78).
+constexpr int kFilterWgThreads = 512;
+
+__global__ __launch_bounds__(kFilterWgThreads) void match_filter_wg_kernel(
+    const int32_t* __restrict__ idx, const float* __restrict__ dist, const double* __restrict__ kp_tpl,
+    const double* __restrict__ kp_q, const int32_t* __restrict__ q_off, int n_tpl, double ratio, double d_lo,
+    double d_hi, double* __restrict__ kp_ordered, uint32_t* __restrict__ keep_bits, int32_t* __restrict__ counts) {
+  __shared__ double sx[kFilterWgThreads * 8];
+  __shared__ int s_cnt[kFilterWgThreads / 64];
+  __shared__ double s_med[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int f = blockIdx.x;
+  const int q_begin = q_off[f];
+  const int words = (n_tpl + 31) >> 5;
+  double dv[8];
+  uint64_t okm[8];
+  int nr = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int i = kFilterWgThreads * k + tid;
+    bool ok = false;
+    double d = INFINITY;
+    if (i < n_tpl) {
+      const size_t o = ((size_t)f * n_tpl + i) * 2;
+      const int j0 = idx[o];
+      double qx = 0.0, qy = 0.0;
+      if (j0 >= 0) {
+        qx = kp_q[2 * (size_t)(q_begin + j0)];
+        qy = kp_q[2 * (size_t)(q_begin + j0) + 1];
+      }
+      kp_ordered[((size_t)f * n_tpl + i) * 2] = qx;
+      kp_ordered[((size_t)f * n_tpl + i) * 2 + 1] = qy;
+      ok = (double)dist[o] < ratio * (double)dist[o + 1];
+      if (ok) {
+        const double dx = kp_tpl[2 * i] - qx, dy = kp_tpl[2 * i + 1] - qy;
+        d = sqrt(dx * dx + dy * dy);
+      }
+    }
+    dv[k] = d;
+    okm[k] = __ballot(ok);
+    nr += __popcll(okm[k]);
+  }
+  if (lane == 0) s_cnt[wave] = nr;
+  __syncthreads();
+  nr = 0;
+#pragma unroll
+  for (int w = 0; w < kFilterWgThreads / 64; ++w) nr += s_cnt[w];
+  double v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = dv[k];
+#pragma unroll
+  for (int size = 2; size <= 8 * kFilterWgThreads; size <<= 1) {
+    const bool asc_t = (tid & (size >> 3)) == 0;  // (e & size) == 0 for size >= 8
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= 512) {  // partner in another wave: through LDS
+        const int ts = stride >> 3;
+        const bool lower = (tid & ts) == 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sx[8 * tid + k] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const double o = sx[8 * (tid ^ ts) + k];
+          v[k] = (lower == asc_t) ? fmin(v[k], o) : fmax(v[k], o);
+        }
+        __syncthreads();
+      } else if (stride >= 8) {
+        const int ls = stride >> 3;
+        const bool lower = (tid & ls) == 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const double o = __shfl_xor(v[k], ls, 64);
+          v[k] = (lower == asc_t) ? fmin(v[k], o) : fmax(v[k], o);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if ((k & stride) == 0) {
+            const bool asc = size >= 8 ? asc_t : (k & size) == 0;
+            cmpx(v[k], v[k | stride], asc);
+          }
+        }
+      }
+    }
+  }
+  // the median of the nr survivors: sorted slots (nr - 1) / 2 and nr / 2 (np.median, VA:210)
+  if (nr > 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int e = 8 * tid + k;
+      if (e == (nr >> 1)) s_med[1] = v[k];
+      if ((nr & 1) == 0 && e == (nr >> 1) - 1) s_med[0] = v[k];
+    }
+  }
+  __syncthreads();
+  double med = 0.0;
+  if (nr > 0) med = (nr & 1) ? s_med[1] : (s_med[0] + s_med[1]) / 2.0;
+  const double lo = d_lo * med, hi = d_hi * med;
+  int nk = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool keep = nr > 0 && ((okm[k] >> lane) & 1ull) && lo <= dv[k] && dv[k] <= hi;
+    const uint64_t m = __ballot(keep);
+    nk += __popcll(m);
+    const int w0 = (kFilterWgThreads * k + 64 * wave) >> 5;
+    if (lane == 0) {
+      if (w0 < words) keep_bits[(size_t)f * words + w0] = (uint32_t)m;
+      if (w0 + 1 < words) keep_bits[(size_t)f * words + w0 + 1] = (uint32_t)(m >> 32);
+    }
+  }
+  __syncthreads();  // s_cnt is reused
+  if (lane == 0) s_cnt[wave] = nk;
+  __syncthreads();
+  if (tid == 0) {
+    int tot = 0;
+    for (int w = 0; w < kFilterWgThreads / 64; ++w) tot += s_cnt[w];
+    counts[4 * (size_t)f + 0] = n_tpl;
+    counts[4 * (size_t)f + 1] = n_tpl;
+    counts[4 * (size_t)f + 2] = nr;
+    counts[4 * (size_t)f + 3] = tot;
+  }
+}
+
 // Workgroups that fill the device once (2 per CU at 8 waves, 4 at 4 waves: the kernels'
 // ~100 VGPRs allow 4 waves per SIMD), split evenly over the template groups.
 
@@ -636,6 +764,11 @@ int launch_match_filter(const int32_t* idx, const float* dist, const double* kp_
                        dim3(64 * kFilterWaveFrames), 0, s, idx, dist, kp_tpl, kp_q, q_off, n_frames, n_tpl, ratio,
                        d_lo, d_hi, kp_ordered, keep_bits, counts);
     return launch_check("match_filter_wave_kernel");
+  }
+  if (n_tpl <= 8 * kFilterWgThreads) {
+    hipLaunchKernelGGL(match_filter_wg_kernel, dim3(n_frames), dim3(kFilterWgThreads), 0, s, idx, dist, kp_tpl, kp_q,
+                       q_off, n_tpl, ratio, d_lo, d_hi, kp_ordered, keep_bits, counts);
+    return launch_check("match_filter_wg_kernel");
   }
   int P = 1;
   while (P < n_tpl) P <<= 1;

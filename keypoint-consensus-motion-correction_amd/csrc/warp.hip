@@ -781,12 +781,15 @@ __device__ __forceinline__ Box persp_box(const double* M, int xb, int yb, int H,
   const int xl = min(xb + kTileW, W) - 1, yl = min(yb + Cfg::kTileH, H) - 1;
   const int cx[4] = {xb, xl, xb, xl}, cy[4] = {yb, yb, yl, yl};
   double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY;
-  bool pos = true, neg = true;
+  bool pos = true, neg = true, wrange = true;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const double w = M[6] * cx[k] + M[7] * cy[k] + M[8];
     pos = pos && w > 0.0;
     neg = neg && w < 0.0;
+    // the staged path's division assumes 2^-60 <= |w| <= 2^60 (w is linear over the tile:
+    // its extremes are at the corners; a factor 2^4 of margin for the rounding)
+    wrange = wrange && fabs(w) >= 0x1p-56 && fabs(w) <= 0x1p56;
     const double sx = (M[0] * cx[k] + M[1] * cy[k] + M[2]) / w;
     const double sy = (M[3] * cx[k] + M[4] * cy[k] + M[5]) / w;
     mnx = fmin(mnx, sx);
@@ -806,7 +809,7 @@ __device__ __forceinline__ Box persp_box(const double* M, int xb, int yb, int H,
   const long long rows = sy1 - sy0 + 1;
   if (sx1 < 0 || sx0 > W - 1 || sy1 < 0 || sy0 > H - 1)
     b.mode = 1;
-  else if (pitch <= kMaxPitch && rows <= 8 * Cfg::kRowPasses && pitch * rows * C <= Cfg::kLdsElems)
+  else if (wrange && pitch <= kMaxPitch && rows <= 8 * Cfg::kRowPasses && pitch * rows * C <= Cfg::kLdsElems)
     b.mode = 0;
   b.ax0 = (int)ax0;
   b.sy0 = (int)sy0;
@@ -857,16 +860,44 @@ __device__ __forceinline__ uint16_t blend_exact(uint32_t v00, uint32_t v01, uint
 // X = cvRound(clamp((X0 + M0 x1) W)), Y likewise.  IN_RANGE: the tile's plan has bounded
 // every source coordinate of the tile within +-30000 px (a staged box), so OpenCV's clamp
 // to [INT_MIN, INT_MAX] is the identity and is left out.
+// 32 / w correctly rounded for 2^-60 <= |w| <= 2^60: the compiler's IEEE division sequence
+// without its range scaling (v_div_scale leaves both operands unscaled in that range and
+// v_div_fmas is then a plain fma) and without v_div_fixup (special values only): the same
+// reciprocal, two Newton steps, quotient, residual and correction, so the same bits.
+__device__ __forceinline__ double div32_in_range(double w) {
+  double y = __builtin_amdgcn_rcp(w);
+  double e = __builtin_fma(-w, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-w, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  const double q = 32.0 * y;
+  const double r = __builtin_fma(-w, q, 32.0);
+  return __builtin_fma(r, y, q);
+}
+
+// rint(x) for |x| < 2^31 as the low word of x + 1.5 * 2^52 (one round-to-nearest-even add
+// to an integer-ulp binade; two's complement for negative x)
+__device__ __forceinline__ int rint_small(double x) {
+  return (int)(uint32_t)__double_as_longlong(x + 0x1.8p52);
+}
+
 template <bool IN_RANGE>
 __device__ __forceinline__ void persp_px(double X0, double Y0, double W0, double m0x1, double m3x1, double m6x1,
                                          int& X, int& Y) {
   double w = W0 + m6x1;
+  if (IN_RANGE) {
+    // staged tiles: the plan kept |w| within [2^-60, 2^60] and every coordinate within
+    // +-30000 px, so the division needs no range handling and OpenCV's clamp to
+    // [INT_MIN, INT_MAX] is the identity
+    w = div32_in_range(w);
+    X = rint_small((X0 + m0x1) * w);
+    Y = rint_small((Y0 + m3x1) * w);
+    return;
+  }
   w = w != 0.0 ? 32.0 / w : 0.0;
   double fX = (X0 + m0x1) * w, fY = (Y0 + m3x1) * w;
-  if (!IN_RANGE) {
-    fX = fmax((double)INT_MIN, fmin((double)INT_MAX, fX));
-    fY = fmax((double)INT_MIN, fmin((double)INT_MAX, fY));
-  }
+  fX = fmax((double)INT_MIN, fmin((double)INT_MAX, fX));
+  fY = fmax((double)INT_MIN, fmin((double)INT_MAX, fY));
   X = (int)__builtin_rint(fX);
   Y = (int)__builtin_rint(fY);
 }

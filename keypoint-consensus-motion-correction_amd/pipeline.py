@@ -406,7 +406,7 @@ class OverlappedSlabs:
         if match_beside and not (corun and depth == 3):
             raise ValueError("match_beside needs corun=True and depth=3")
         self.depth = depth
-        # match_beside: the match + vote of slab k also run on the analysis stream (behind
+        # match_beside: the match + vote of slab k also run on the analysis stream (ahead of
         # lookup + RANSAC(k-1)), so the kernel stream carries only the warps
         self.match_beside = bool(match_beside)
         if counts is not None and len(counts) > 1 and cfg.frame_downsample_rate != 1:
@@ -512,13 +512,19 @@ class OverlappedSlabs:
                 if t is not None:
                     t.record_stream(self.stream)
             if self.match_beside:
-                # kernel stream: warp(k-2); analysis stream: lookup + RANSAC(k-1) -> match(k)
+                # kernel stream: warp(k-2); analysis stream: match(k) -> lookup + RANSAC(k-1).
+                # The merge of slab k-1 uses votes that were ready a step earlier, so the
+                # analysis stream never waits on the host; warp(k-1) (next submit) waits for
+                # RANSAC(k-1) only.  (RANSAC(k-1) first and match(k) behind it put the
+                # votes -> host merge -> RANSAC round trip of one slab on the warp's path:
+                # c3 0.83 ms per step.)
                 fitted, self._fitted = self._fitted, None
                 if fitted is not None and self._device_maps():
                     self._warp_device_maps(fitted, mark)
+                new = self._match(inp, out, mark)
                 if self._matched is not None:
                     self._fitted = self._fit(self._matched, mark)
-                self._matched = self._match(inp, out, mark)
+                self._matched = new
                 return self._finish(fitted, mark) if fitted is not None else None
             new = self._match(inp, out, mark)
             fitted, self._fitted = self._fitted, None
@@ -567,7 +573,7 @@ class OverlappedSlabs:
         return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=matched)
 
     def _match_beside(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
-        """match(k) and its vote on the analysis stream (allocated there), behind the lookup +
+        """match(k) and its vote on the analysis stream (allocated there), ahead of the lookup +
         RANSAC of the previous slab; the (gathered) votes to the host."""
         n_tpl = inp.des_tpl.shape[0]
         with torch.cuda.stream(self.ana):

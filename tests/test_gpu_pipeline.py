@@ -134,7 +134,7 @@ def test_overlapped_slabs_equal_align_slab(dev, depth, corun, grid, beside):
     """OverlappedSlabs (depth 2: device order match(k) -> warp(k-1) -> RANSAC(k); depth 3:
     match(k) -> warp(k-2) -> RANSAC(k-1); corun: RANSAC on a second stream beside the
     warp, optionally on a narrow grid of workgroups that walk the frames; beside: the match
-    on that stream too, behind RANSAC(k-1)) gives the same affines and warped frames as the
+    on that stream too, ahead of RANSAC(k-1)) gives the same affines and warped frames as the
     sequential align_slab."""
     F, H, W = 24, 270, 480
     cfg = pipeline.AlignConfig(n_kp_global=60)
