@@ -294,6 +294,42 @@ __device__ __forceinline__ float score_fast(const double (&h)[9], const Pts& P, 
   return S;
 }
 
+// The same over the frame's points packed as (x, y, dx, dy) in LDS (frames with N <= 128):
+// two ds_read_b128 with immediate offsets per point and two points per iteration, so the
+// reads of a pair are in flight together (the SoA loop issued four address moves and four
+// 8-byte reads per point and waited on each point's reads).  Same operations, same order.
+struct __attribute__((aligned(16))) PackedPt {
+  double2 s, d;  // (x, y), (dx, dy)
+};
+
+template <int MODEL>
+__device__ __forceinline__ float score_fast_packed(const double (&h)[9], const PackedPt* __restrict__ pk, int N,
+                                                   double tq, int& cnt) {
+  float S = 0.f;
+  auto one = [&](const PackedPt p) {
+    double X = fma(p.s.y, h[1], p.s.x * h[0]) + h[2];
+    double Y = fma(p.s.y, h[4], p.s.x * h[3]) + h[5];
+    if (MODEL == KCMC_MODEL_PROJECTIVE) {
+      double w = fma(p.s.y, h[7], p.s.x * h[6]) + h[8];
+      if (w == 0.0) w = DBL_EPSILON;
+      X = X / w;
+      Y = Y / w;
+    }
+    const double ex = X - p.d.x, ey = Y - p.d.y;
+    const double q = ex * ex + ey * ey;
+    cnt += (q < tq) ? 1 : 0;
+    S += (float)q;
+  };
+  int k = 0;
+  for (; k + 2 <= N; k += 2) {
+    const PackedPt a = pk[k], b = pk[k + 1];
+    one(a);
+    one(b);
+  }
+  if (k < N) one(pk[k]);
+  return S;
+}
+
 template <int MODEL>
 __device__ __forceinline__ HModel fit_trial(const Pts& P, uint64_t pr) {
   if constexpr (MODEL == KCMC_MODEL_AFFINE) {
@@ -369,7 +405,9 @@ __device__ __forceinline__ void ransac_model_score_frame(
   double* sy = sx + N;
   double* dxs = sy + N;
   double* dys = dxs + N;
-  double* tS = dys + N;
+  // !LARGE: the points again as (x, y, dx, dy) for phase A (16-byte aligned: smem is)
+  PackedPt* pk = reinterpret_cast<PackedPt*>(smem + ((4 * N + 1) & ~1));
+  double* tS = LARGE ? dys + N : reinterpret_cast<double*>(pk + N);
   double* stk = tS + T;
   double* wvals = stk + (LARGE ? kMaxStack * kThreads : 0);
   int* tC = reinterpret_cast<int*>(wvals + kThreads / 64 * 128);
@@ -377,8 +415,10 @@ __device__ __forceinline__ void ransac_model_score_frame(
     s_plan.n = 0;
     plan_gen<kPwDepth>(s_plan, 0, N);
   }
-  for (int k = tid; k < N; k += kThreads)
+  for (int k = tid; k < N; k += kThreads) {
     gather_point(src, dst, pt_idx, src_stride, f, p0 + k, sx[k], sy[k], dxs[k], dys[k]);
+    if (!LARGE) pk[k] = PackedPt{make_double2(sx[k], sy[k]), make_double2(dxs[k], dys[k])};
+  }
   if (tid == 0) s_any_zero = 0;
   __syncthreads();
 
@@ -398,7 +438,7 @@ __device__ __forceinline__ void ransac_model_score_frame(
       float S32 = NAN;
       if (m.ok) {
         cnt = 0;
-        S32 = score_fast<MODEL>(m.h, P, N, tq, cnt);
+        S32 = LARGE ? score_fast<MODEL>(m.h, P, N, tq, cnt) : score_fast_packed<MODEL>(m.h, pk, N, tq, cnt);
         if (!s32_certain(S32)) flag = 1;
       }
       tC[t] = cnt;
@@ -834,8 +874,8 @@ static int ransac_model_impl(kcmc_ctx* ctx, int model, const double* src, const 
   const int need = max_n < ms + 1 ? ms + 1 : max_n;
   const int n_small = need < 128 ? need : 128;
   const size_t wvals = (size_t)kThreads / 64 * 128 * sizeof(double);
-  const size_t lds_small =
-      (size_t)n_small * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) + wvals + 16;
+  const size_t lds_small = (size_t)(n_small + 1) * 4 * sizeof(double) + (size_t)n_small * 4 * sizeof(double) +
+                           (size_t)trials * (sizeof(double) + sizeof(int)) + wvals + 16;
   const size_t lds_large = (size_t)need * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) + wvals +
                            (size_t)kMaxStack * kThreads * sizeof(double) + 16;
   if ((max_n > 128 ? lds_large : lds_small) > 150 * 1024)
