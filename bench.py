@@ -380,6 +380,9 @@ def main():
     ap.add_argument("--match-beside", action="store_true",
                     help="the match + vote also on the analysis stream, beside the warp (depth 3; "
                          "OverlappedSlabs match_beside=True); default: the config's")
+    ap.add_argument("--fit-first", action="store_true",
+                    help="depth 3: queue lookup + RANSAC(k-1) before warp(k-2) (OverlappedSlabs fit_first=True; "
+                         "measured slower at c3)")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
@@ -418,7 +421,8 @@ def main():
     ov = None if args.serial else pipeline.OverlappedSlabs(dev, cfg, counts=counts if world > 1 else None,
                                                             depth=args.pipeline_depth, corun=not args.no_corun,
                                                             ransac_grid=args.ransac_grid,
-                                                            match_beside=args.match_beside)
+                                                            match_beside=args.match_beside,
+                                                            fit_first=args.fit_first)
 
     def step(timer):
         if ov is None:

@@ -400,7 +400,7 @@ class OverlappedSlabs:
 
     def __init__(self, device, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
                  counts: Optional[List[int]] = None, group=None, depth: int = 2, corun: bool = True,
-                 ransac_grid: Optional[int] = None, match_beside: bool = False):
+                 ransac_grid: Optional[int] = None, match_beside: bool = False, fit_first: bool = False):
         if depth not in (2, 3):
             raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
         if match_beside and not (corun and depth == 3):
@@ -409,6 +409,10 @@ class OverlappedSlabs:
         # match_beside: the match + vote of slab k also run on the analysis stream (ahead of
         # lookup + RANSAC(k-1)), so the kernel stream carries only the warps
         self.match_beside = bool(match_beside)
+        # fit_first (depth 3, corun): queue lookup + RANSAC(k-1) before waiting for RANSAC(k-2),
+        # so it starts beside match(k).  Measured slower at c3 (2.36 M vs 2.91 M frames/s,
+        # same box: RANSAC then shares the CUs with the match and the warp), so off.
+        self.fit_first = bool(fit_first)
         if counts is not None and len(counts) > 1 and cfg.frame_downsample_rate != 1:
             # the rank's first frame is counted in sample frames, the affines in full-rate
             # frames: the same restriction as distributed.align_sharded
@@ -528,6 +532,16 @@ class OverlappedSlabs:
                 return self._finish(fitted, mark) if fitted is not None else None
             new = self._match(inp, out, mark)
             fitted, self._fitted = self._fitted, None
+            if self.depth == 3 and self.corun and self.fit_first:
+                # lookup + RANSAC(k-1) go to the analysis stream before the host waits for
+                # RANSAC(k-2): they start beside match(k) (meant to end inside warp(k-2); the
+                # c3 trace had RANSAC queued after the warp started spill 0.15 ms past it)
+                nxt = self._fit(self._matched, mark) if self._matched is not None else None
+                if fitted is not None and self._device_maps():
+                    self._warp_device_maps(fitted, mark)
+                self._fitted = nxt
+                self._matched = new
+                return self._finish(fitted, mark) if fitted is not None else None
             if fitted is not None and self._device_maps():
                 self._warp_device_maps(fitted, mark)  # warp(k-depth+1) queued behind match(k)
             if self.depth == 2:

@@ -128,13 +128,16 @@ def test_config2_slab_end_to_end(dev):
         assert np.array_equal(out[f], oracle.warp_affine_u16(base, res.affines[f]))
 
 
-@pytest.mark.parametrize("depth,corun,grid,beside", [(2, False, 0, False), (3, False, 0, False), (2, True, 0, False),
-                                                     (3, True, 0, False), (2, True, 5, False), (3, True, 0, True)])
-def test_overlapped_slabs_equal_align_slab(dev, depth, corun, grid, beside):
+@pytest.mark.parametrize("depth,corun,grid,beside,first", [(2, False, 0, False, True), (3, False, 0, False, True),
+                                                           (2, True, 0, False, True), (3, True, 0, False, True),
+                                                           (3, True, 0, False, False), (2, True, 5, False, True),
+                                                           (3, True, 0, True, True)])
+def test_overlapped_slabs_equal_align_slab(dev, depth, corun, grid, beside, first):
     """OverlappedSlabs (depth 2: device order match(k) -> warp(k-1) -> RANSAC(k); depth 3:
     match(k) -> warp(k-2) -> RANSAC(k-1); corun: RANSAC on a second stream beside the
     warp, optionally on a narrow grid of workgroups that walk the frames; beside: the match
-    on that stream too, ahead of RANSAC(k-1)) gives the same affines and warped frames as the
+    on that stream too, ahead of RANSAC(k-1); first: at depth 3 RANSAC(k-1) queued before
+    the host waits for RANSAC(k-2)) gives the same affines and warped frames as the
     sequential align_slab."""
     F, H, W = 24, 270, 480
     cfg = pipeline.AlignConfig(n_kp_global=60)
@@ -155,7 +158,8 @@ def test_overlapped_slabs_equal_align_slab(dev, depth, corun, grid, beside):
                                          torch.from_numpy(ks.kp_q).to(dev), torch.from_numpy(ks.q_off).to(dev),
                                          ks.q_off))
     ref = [pipeline.align_slab(s, cfg) for s in slabs]
-    ov = pipeline.OverlappedSlabs(dev, cfg, depth=depth, corun=corun, ransac_grid=grid, match_beside=beside)
+    ov = pipeline.OverlappedSlabs(dev, cfg, depth=depth, corun=corun, ransac_grid=grid, match_beside=beside,
+                                  fit_first=first)
     got = [ov.submit(s) for s in slabs]
     assert all(g is None for g in got[:depth - 1])
     got = got[depth - 1:] + ov.flush()
