@@ -265,6 +265,7 @@ __global__ __launch_bounds__(kImgThreads) void frame_images_kernel(const float* 
   const float sK = sqrtf(K);
   const float sT = pow2_scale(__uint_as_float(Kst[1]));
   const float sf = frame_scale(Kst);
+  const float isf = 1.f / sf;  // exact: s_f is a power of 2 in [2^-68, 2^52]
   const float sc = sT * sf;
   const float dA = __uint_as_float(Kst[2]);
   const int rr = tid >> 4, col = (tid & 15) * 8;
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(kImgThreads) void frame_images_kernel(const float* 
     const float y = x[k] * sf;
     big |= !(fabsf(y) <= 65504.f);  // also NaN
     h[k] = (_Float16)y;
-    const float d = x[k] - (float)h[k] / sf;  // the rounding error, exact
+    const float d = x[k] - (float)h[k] * isf;  // the rounding error, exact (isf = 1 / s_f, a power of 2)
     e2 = fmaf(d, d, e2);
   }
 #pragma unroll
