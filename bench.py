@@ -67,6 +67,10 @@ class BenchConfig:
     # slabs in flight (pipeline.OverlappedSlabs depth): 3 where the host's per-step work
     # (consensus + launch chain, ~0.9 ms) is as long as the warp it hides under (c3)
     pipeline_depth: int = 2
+    # the match + vote on the analysis stream beside the warp (OverlappedSlabs match_beside,
+    # depth 3): c4, whose 12 ms RGB warp absorbs part of the 1.5 ms match (+1.5-2 %,
+    # profiles/r03_b5_bench_c4_*.json); slower at c2 / c3 / c5
+    match_beside: bool = False
 
 
 # BASELINE.json configs.  c2 (configs[1]) is the headline line; the others are the
@@ -81,7 +85,7 @@ CONFIGS = {
                       512, 512, 1, 500, 61, 50, "affine", 2500, 60, pipeline_depth=3),
     "c4": BenchConfig("c4", "BASELINE config[3]: 4K RGB u16 (2160x3840x3), 5000 frames over 8 GPUs (625 per GPU), "
                       "4096 keypoints/frame template, D=61 B, affine RANSAC 1000 trials, n_kp_global=500",
-                      2160, 3840, 3, 4096, 61, 500, "affine", 625, 4),
+                      2160, 3840, 3, 4096, 61, 500, "affine", 625, 4, pipeline_depth=3, match_beside=True),
     "c5": BenchConfig("c5", "BASELINE config[4]: 1080p u16, float SIFT-style descriptors (n_tpl=4096, D=128 f32, "
                       "~4500/frame), homography RANSAC 1000 trials, n_kp_global=200, warpPerspective; "
                       "500 frames per GPU", 1080, 1920, 1, 4096, 128, 200, "projective", 500, 2, "f32"),
@@ -377,9 +381,11 @@ def main():
                     help="RANSAC behind the warp on the one kernel stream (OverlappedSlabs corun=False)")
     ap.add_argument("--ransac-grid", type=int, default=None,
                     help="workgroups of the RANSAC launches beside the warp (default 0: one per frame)")
-    ap.add_argument("--match-beside", action="store_true",
+    ap.add_argument("--match-beside", action="store_true", default=None,
                     help="the match + vote also on the analysis stream, beside the warp (depth 3; "
-                         "OverlappedSlabs match_beside=True); default: the config's")
+                         "OverlappedSlabs match_beside=True); default: the config's (c4)")
+    ap.add_argument("--no-match-beside", dest="match_beside", action="store_false",
+                    help="the match + vote on the kernel stream ahead of the warp")
     ap.add_argument("--fit-first", action="store_true",
                     help="depth 3: queue lookup + RANSAC(k-1) before warp(k-2) (OverlappedSlabs fit_first=True; "
                          "measured slower at c3)")
@@ -391,6 +397,8 @@ def main():
         args.frames = bc.frames_per_gpu
     if args.pipeline_depth is None:
         args.pipeline_depth = bc.pipeline_depth
+    if args.match_beside is None:
+        args.match_beside = bc.match_beside and not args.no_corun and args.pipeline_depth == 3
     if args.cpu_sample is None:
         args.cpu_sample = bc.cpu_sample * max(1, args.cpu_procs) // 2
 

@@ -700,10 +700,6 @@ __global__ __launch_bounds__(kFilterWgThreads) void match_filter_wg_kernel(
   }
 }
 
-// Workgroups that fill the device once (2 per CU at 8 waves, 4 at 4 waves: the kernels'
-// ~100 VGPRs allow 4 waves per SIMD), split evenly over the template groups.
-
-
 // persistent grid: n_tg template groups x G frame strides, G = the resident workgroups
 // per template group (workgroups never wait on each other, so a wrong residency count
 // costs balance, not progress)

@@ -21,8 +21,8 @@
 //
 // knn2_l2f32_kernel -- one workgroup = 256 template rows x one frame (8 waves x one block
 //   of 32 rows, the template operand fp16(-s_T a) in registers).  Tiles reach LDS by
-//   LDS-DMA (three buffers: two tiles in flight ahead of the one in use, one barrier per
-//   tile).  One v_mfma_f32_32x32x16_f16 per 16-wide k-step and 32-row half tile, the
+//   LDS-DMA (two buffers: one tile in flight ahead of the one in use, one barrier per
+//   tile; 36 KB, so three workgroups = 6 waves per SIMD fit a CU).  One v_mfma_f32_32x32x16_f16 per 16-wide k-step and 32-row half tile, the
 //   accumulator started at C':
 //     v~ = s_T s_f ((|b|^2 + K) / 2 + beta_j - a.b + e_j),  |e_j| <= beta_j
 //   (fp16 products are exact in fp32; e_j = the fp16 roundings of a and b, the fp32
@@ -48,7 +48,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
-constexpr int kNBuf = 3;                  // tile buffers: two tiles in flight ahead of the one in use
+constexpr int kNBuf = 2;                  // tile buffers: one tile in flight ahead of the one in use
 constexpr int kTplPerWG = kWaves * 32;    // 256 template rows per workgroup
 constexpr int kDP = 128;                  // padded descriptor length
 constexpr int kKSteps = kDP / 16;         // k-steps of v_mfma_f32_32x32x16_f16
@@ -372,8 +372,10 @@ __device__ __forceinline__ void dma_tile(const uint8_t* __restrict__ src, uint8_
   }
 }
 
-// 4 waves per SIMD (<= 128 VGPRs)
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void knn2_l2f32_kernel(
+// 6 waves per SIMD (<= 80 VGPRs; the epilogue spills a few, the tile loop none): the
+// waits on LDS and the MFMA results hide behind the other waves' top-6 VALU work
+// (c5 lab 4.56 -> 4.38 ms against 4 waves per SIMD with three tile buffers)
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 6))) void knn2_l2f32_kernel(
     const float* __restrict__ des_tpl, int n_tpl, int D, const float* __restrict__ des_q,
     const int32_t* __restrict__ q_off, const uint8_t* __restrict__ img, int tpf,
     const unsigned* __restrict__ Kst, const float* __restrict__ fmax, const float* __restrict__ fbeta,
@@ -397,11 +399,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
   const int n_tiles = min((n_q + kTile - 1) / kTile, tpf);
   const uint8_t* fimg = img + (size_t)f * tpf * kImgBytes;
   if (n_tiles > 0) dma_tile(fimg, tbuf[0], wave, lane);
-  if (n_tiles > 1) dma_tile(fimg + kImgBytes, tbuf[1], wave, lane);
-  // LDS-DMA pieces this wave issues per tile (wave-uniform): the count left in flight
-  // while tile t + 1 is still landing
-  const bool many = wave < kPieces % kWaves;
-  static_assert(kPieces / kWaves == 2 && kPieces % kWaves != 0, "vmcnt counts below assume 2 or 3 pieces per wave");
 
   // ---- template fragment (B operand, fp16(-s_T a)) kept in registers: lane (c, h) holds
   // row i's elements k = 16 s + 8 h + j of k-step s
@@ -425,60 +422,47 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
   uint32_t ithr = 0xffffffffu;
   int cur = 0;  // t % kNBuf
   for (int t = 0; t < n_tiles; ++t) {
-    // tile t has landed (this wave's pieces: vmcnt, leaving tile t + 1's in flight; the
-    // others': the barrier) and every wave is done with tile t - 1, whose buffer the copy
-    // of tile t + 2 overwrites.  A raw s_barrier: __syncthreads() would wait vmcnt(0).
-    if (t + 1 == n_tiles)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (many)
-      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    // tile t has landed (this wave's pieces: vmcnt; the others': the barrier) and every
+    // wave is done with tile t - 1, whose buffer the copy of tile t + 1 overwrites.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 2 < n_tiles) {
-      const int nb = cur >= 1 ? cur - 1 : kNBuf - 1;  // (t + 2) % kNBuf
-      dma_tile(fimg + (size_t)(t + 2) * kImgBytes, tbuf[nb], wave, lane);
-    }
+    if (t + 1 < n_tiles) dma_tile(fimg + (size_t)(t + 1) * kImgBytes, tbuf[cur ^ 1], wave, lane);
     const uint8_t* tbp = tbuf[cur];
-    cur = cur + 1 == kNBuf ? 0 : cur + 1;
+    cur ^= 1;
     // accumulators start at the rows' C': half hh, lane's 16 rows 32 hh + (r & 3) + 8 (r >> 2) + 4h
     const float* cq = reinterpret_cast<const float*>(tbp + kImgC);
-    v16f acc[2];
+    const uint32_t tbase = (uint32_t)t << 5;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
+    for (int hh = 0; hh < 2; ++hh) {
+      v16f acc;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 q4 = *reinterpret_cast<const float4*>(cq + 32 * hh + 8 * g + 4 * h);
-        acc[hh][4 * g] = q4.x;
-        acc[hh][4 * g + 1] = q4.y;
-        acc[hh][4 * g + 2] = q4.z;
-        acc[hh][4 * g + 3] = q4.w;
+        acc[4 * g] = q4.x;
+        acc[4 * g + 1] = q4.y;
+        acc[4 * g + 2] = q4.z;
+        acc[4 * g + 3] = q4.w;
       }
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
       const _Float16* ap = reinterpret_cast<const _Float16*>(tbp) + (32 * hh + c) * kRowB + 8 * h;
 #pragma unroll
       for (int st = 0; st < kKSteps; ++st)
-        acc[hh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*reinterpret_cast<const f16x8*>(ap + 16 * st), btpl[st],
-                                                         acc[hh], 0, 0, 0);
-    }
-    // a value whose bits are >= ithr = (last key | low bits) cannot enter the list: its key
-    // would be >= the last key's truncated value, which already bounds every unlisted row.
-    // After the first few hundred rows most distances of a wave skip the insertion (the
-    // branch is per wave): 8 -> ~1 + 9 P VALU per distance (c5 lab 5.15 -> 4.65 ms)
-    const uint32_t tbase = (uint32_t)t << 5;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*reinterpret_cast<const f16x8*>(ap + 16 * st), btpl[st], acc, 0,
+                                                     0, 0);
+      // a value whose bits are >= ithr = (last key | low bits) cannot enter the list: its
+      // key would be >= the last key's truncated value, which already bounds every unlisted
+      // row.  After the first few hundred rows most distances of a wave skip the insertion
+      // (the branch is per wave): 8 -> ~1 + 9 P VALU per distance (c5 lab 5.15 -> 4.65 ms)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const uint32_t xb = __float_as_uint(acc[hh][r]);
+        const uint32_t xb = __float_as_uint(acc[r]);
         if (xb < ithr) {
           topk_key(ck, ((xb & kmask) | (uint32_t)(hh * 16 + r)) | tbase);
           ithr = ck[kTop - 1] | ~kmask;
         }
       }
+    }
   }
 
   // ---- decode (value truncated to the key, frame row) and merge the two row halves
