@@ -9,7 +9,7 @@
 //           vote_key_kernel (one workgroup: flags the first frames and writes the keys).
 //   lookup: list(consensus_idxs.intersection(kp_idxs_list[i])) (VA:274) per frame:
 //           lookup_count_kernel (counts + exclusive scan = CSR offsets, one workgroup) +
-//           lookup_order_kernel (one thread per frame writes its list in set order).
+//           lookup_order_kernel (one wave per frame writes its list in set order).
 //
 // CPython set order: a set of non-negative ints (hash(k) == k) built by insertions only
 // iterates in table-slot order.  When every key is below the final table size (which
@@ -117,7 +117,7 @@ constexpr int kVoteThreads = 256;
 constexpr int kKeyThreads = 256;
 constexpr int kEmuLanes = 64;     // vote_key_kernel replays of non-ascending first frames
 constexpr int kCountThreads = 64;
-constexpr uint32_t kOrderLdsCap = 2048;  // lookup_order_kernel keeps result tables up to this size in LDS
+constexpr uint32_t kOrderLdsCap = 2048;  // lookup_order_kernel keeps set tables up to this size in LDS
 
 // cnt[t] += frames of the chunk holding t; first_enc[t] = max(0x7fffffff - first frame):
 // scratch in the key row of the output (zeroed before the launch).
@@ -270,16 +270,30 @@ __device__ __forceinline__ int wave_max(int x) {
 
 // One wave per frame: its consensus points in CPython set-iteration order at pt_off[f].
 // Ascending results (every key below the final table size) are written by the whole wave
-// (lane = bitmask word, wave prefix sums); the others are replayed by lane 0 in the wave's
-// LDS tables (global scratch when a table exceeds kOrderLdsCap entries) and compacted in
-// slot order by the whole wave.  The frame's own set (the intersection iterates it when it
-// is not larger than the consensus) is replayed in global scratch when its order is not
-// ascending.
+// (lane = bitmask word, wave prefix sums).  The others are replayed by lane 0 in set tables
+// in LDS (global scratch when they do not fit), fed from a list of keys the whole wave
+// stages in LDS in insertion order first: the serial part then touches only LDS (round 3:
+// the replay loop's own global loads, two per consensus key, were most of the kernel's
+// time -- c2 lookup 51.6 us).  The insertion order is set_intersection's (VA:274): the
+// consensus in its own iteration order when the frame's set is larger, else the frame's
+// set in its table order (ascending, or replayed first when its keys exceed its table).
+__device__ __forceinline__ int wave_compact(bool take, int32_t key, int32_t* dst, int n, uint64_t below) {
+  const uint64_t hit = __ballot(take);
+  if (take) dst[n + __popcll(hit & below)] = key;
+  return n + __popcll(hit);
+}
+
 __global__ __launch_bounds__(64) void lookup_order_kernel(
     const uint32_t* __restrict__ keep, int F, int W, const int32_t* __restrict__ cons_iter, int nc,
     const uint32_t* __restrict__ cons_bits, const int32_t* __restrict__ pt_off, int32_t* __restrict__ pt_idx,
-    int32_t* __restrict__ scratch, uint32_t cap) {
-  extern __shared__ int32_t tab[];  // [2 * cap] when cap <= kOrderLdsCap
+    int32_t* __restrict__ scratch, uint32_t cap, int r_lds, int s_lds) {
+  // LDS: [W] frame words, [W] consensus words, [nc] staged keys, then the R tables
+  // [2 cap] when r_lds and the S tables [2 cap] when s_lds
+  extern __shared__ uint32_t lds[];
+  uint32_t* rowS = lds;
+  uint32_t* consS = rowS + W;
+  int32_t* keyS = reinterpret_cast<int32_t*>(lds + 2 * W);
+  int32_t* tabS = keyS + nc;
   const int f = blockIdx.x;
   const int lane = threadIdx.x;
   const int o = pt_off[f];
@@ -288,60 +302,86 @@ __global__ __launch_bounds__(64) void lookup_order_kernel(
   const uint32_t* row = keep + (size_t)f * W;
   int flen = 0, fmax = -1, top = -1;
   for (int w = lane; w < W; w += 64) {
-    const uint32_t v = row[w];
+    const uint32_t v = row[w], cb = cons_bits[w];
+    rowS[w] = v;
+    consS[w] = cb;
     flen += __popc(v);
     if (v) fmax = 32 * w + 31 - __clz(v);
-    const uint32_t h = v & cons_bits[w];
+    const uint32_t h = v & cb;
     if (h) top = 32 * w + 31 - __clz(h);
   }
   flen = wave_sum(flen);
   fmax = wave_max(fmax);
   top = wave_max(top);
+  __syncthreads();  // one wave: the staged words are visible to every lane
   int32_t* out = pt_idx + o;
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  if ((uint32_t)top < pyset_table_size((uint32_t)m)) {  // every key in its home slot: ascending
+  // the bits of rowS & mask in ascending key order, compacted into dst (returns the count)
+  auto stage_bits = [&](const uint32_t* mask, int32_t* dst) {
     int n = 0;
     for (int w0 = 0; w0 < W; w0 += 64) {
       const int w = w0 + lane;
-      uint32_t h = w < W ? row[w] & cons_bits[w] : 0u;
-      int c = __popc(h);
+      uint32_t h = w < W ? rowS[w] & (mask ? mask[w] : ~0u) : 0u;
+      const int c = __popc(h);
       int x = c;  // inclusive prefix over the lanes
       for (int d = 1; d < 64; d <<= 1) {
         const int y = __shfl_up(x, d, 64);
         if (lane >= d) x += y;
       }
       int k = n + x - c;
-      for (; h; h &= h - 1) out[k++] = 32 * w + __ffs(h) - 1;
+      for (; h; h &= h - 1) dst[k++] = 32 * w + __ffs(h) - 1;
       n += __shfl(x, 63, 64);
     }
+    return n;
+  };
+  if ((uint32_t)top < pyset_table_size((uint32_t)m)) {  // every key in its home slot: ascending
+    stage_bits(consS, out);
     return;
   }
-  int32_t* R0 = cap <= kOrderLdsCap ? tab : scratch + (size_t)f * 4 * cap;
+  int32_t* R0 = r_lds ? tabS : scratch + (size_t)f * 4 * cap;
   int32_t* R1 = R0 + cap;
-  int32_t* S0 = scratch + (size_t)f * 4 * cap + 2 * cap;
+  int32_t* S0 = s_lds ? tabS + 2 * cap : scratch + (size_t)f * 4 * cap + 2 * cap;
+  // ---- the result's keys in insertion order -> keyS[0, m)
+  if ((uint32_t)flen > (uint32_t)nc) {  // set_intersection iterates the smaller set: the consensus
+    int n = 0;
+    for (int k0 = 0; k0 < nc; k0 += 64) {
+      const int k = k0 + lane;
+      const int32_t key = k < nc ? cons_iter[k] : 0;
+      n = wave_compact(k < nc && ((rowS[key >> 5] >> (key & 31)) & 1u), key, keyS, n, below);
+    }
+  } else if ((uint32_t)fmax < pyset_table_size((uint32_t)flen)) {  // the frame's set, ascending
+    stage_bits(consS, keyS);
+  } else {  // the frame's set in its own table order: replay it, then read its slots
+    int32_t* fk = keyS;  // the frame's keys ascending (flen <= nc entries), then reused
+    stage_bits(nullptr, fk);
+    __syncthreads();
+    uint32_t smask = 0;
+    int ssel = 0;
+    if (lane == 0) {
+      DevPySet S;
+      S.init(S0, S0 + cap);
+      for (int i = 0; i < flen; ++i) S.add(fk[i]);
+      smask = S.mask;
+      ssel = S.t != S0;
+    }
+    __syncthreads();
+    smask = __shfl(smask, 0, 64);
+    ssel = __shfl(ssel, 0, 64);
+    const int32_t* T = ssel ? S0 + cap : S0;
+    int n = 0;
+    for (uint32_t s0 = 0; s0 <= smask; s0 += 64) {
+      const uint32_t slot = s0 + lane;
+      const int32_t key = slot <= smask ? T[slot] : -1;
+      n = wave_compact(key >= 0 && ((consS[key >> 5] >> (key & 31)) & 1u), key, keyS, n, below);
+    }
+  }
+  __syncthreads();
   uint32_t rmask = 0;
   int rsel = 0;
   if (lane == 0) {
     DevPySet R;
     R.init(R0, R1);
-    if ((uint32_t)flen > (uint32_t)nc) {  // set_intersection iterates the smaller set: the consensus
-      for (int k = 0; k < nc; ++k) {
-        const int32_t key = cons_iter[k];
-        if ((row[key >> 5] >> (key & 31)) & 1u) R.add(key);
-      }
-    } else if ((uint32_t)fmax < pyset_table_size((uint32_t)flen)) {  // the frame's set, ascending
-      for (int w = 0; w < W; ++w)
-        for (uint32_t b = row[w] & cons_bits[w]; b; b &= b - 1) R.add(32 * w + __ffs(b) - 1);
-    } else {  // the frame's set in its own table order
-      DevPySet S;
-      S.init(S0, S0 + cap);
-      for (int w = 0; w < W; ++w)
-        for (uint32_t b = row[w]; b; b &= b - 1) S.add(32 * w + __ffs(b) - 1);
-      for (uint32_t slot = 0; slot <= S.mask; ++slot) {
-        const int32_t key = S.t[slot];
-        if (key >= 0 && ((cons_bits[key >> 5] >> (key & 31)) & 1u)) R.add(key);
-      }
-    }
+    for (int i = 0; i < m; ++i) R.add(keyS[i]);
     rmask = R.mask;
     rsel = R.t == R1;
   }
@@ -353,9 +393,7 @@ __global__ __launch_bounds__(64) void lookup_order_kernel(
   for (uint32_t s0 = 0; s0 <= rmask; s0 += 64) {
     const uint32_t slot = s0 + lane;
     const int32_t key = slot <= rmask ? T[slot] : -1;
-    const uint64_t hit = __ballot(key >= 0);
-    if (key >= 0) out[n + __popcll(hit & below)] = key;
-    n += __popcll(hit);
+    n = wave_compact(key >= 0, key, out, n, below);
   }
 }
 
@@ -454,9 +492,10 @@ extern "C" int kcmc_consensus_lookup(kcmc_ctx* ctx, const uint32_t* keep_bits, i
   hipLaunchKernelGGL(lookup_scan_kernel, dim3(1), dim3(64), 0, s, n_frames, out_pt_off);
   KCMC_TRY(launch_check("lookup_scan_kernel"));
   const uint32_t cap = pyset_table_size((uint32_t)nc);
-  const size_t lds = cap <= kOrderLdsCap ? (size_t)2 * cap * sizeof(int32_t) : 0;
+  const int r_lds = cap <= kOrderLdsCap, s_lds = cap <= kOrderLdsCap / 2;
+  const size_t lds = ((size_t)2 * W + nc + (r_lds ? 2 * cap : 0) + (s_lds ? 2 * cap : 0)) * sizeof(int32_t);
   hipLaunchKernelGGL(lookup_order_kernel, dim3(n_frames), dim3(64), lds, s, keep_bits, n_frames, W, cons_pack, nc,
-                     cons_bits, out_pt_off, out_pt_idx, reinterpret_cast<int32_t*>(scratch), cap);
+                     cons_bits, out_pt_off, out_pt_idx, reinterpret_cast<int32_t*>(scratch), cap, r_lds, s_lds);
   return launch_check("lookup_order_kernel");
 }
 
