@@ -82,7 +82,8 @@ float timeit(L launch, int reps) {
 }
 
 int main(int argc, char** argv) {
-  const int F = argc > 1 ? atoi(argv[1]) : 2000, H = 1080, W = 1920, reps = 10;
+  const int F = argc > 1 ? atoi(argv[1]) : 2000, reps = 10;
+  const int H = argc > 3 ? atoi(argv[3]) : 1080, W = argc > 4 ? atoi(argv[4]) : 1920;
   const size_t n = (size_t)F * H * W;
   uint16_t *src, *dst;
   CK(hipMalloc(&src, n * 2));
@@ -97,7 +98,8 @@ int main(int argc, char** argv) {
     printf("%-34s %.3f ms  %.2f TB/s  (full-frame equivalent %.3f ms)\n", name, ms, gb * frac / ms, ms / frac);
   };
   auto tiles = [&](int TW, int TH) { return F * (W / TW) * ((H + TH - 1) / TH); };
-  const bool more = argc > 2;
+  const bool more = argc > 2 && argv[2][0] == 'm';
+  const bool c3 = argc > 2 && argv[2][0] == 'c';
   for (int round = 0; round < 2; ++round) {
     report("linear uint4 copy", timeit([&] { hipLaunchKernelGGL(copy_lin, dim3(8192), dim3(256), 0, 0, (const uint4*)src, (uint4*)dst, n / 8); }, reps));
     report("linear uint4 copy, nt", timeit([&] { hipLaunchKernelGGL(copy_lin_nt, dim3(8192), dim3(256), 0, 0, (const uint4*)src, (uint4*)dst, n / 8); }, reps));
@@ -108,6 +110,12 @@ int main(int argc, char** argv) {
     report("tile 256x28, 16-B nt stores", timeit([&] { hipLaunchKernelGGL((copy_tile<256, 28, 16, true>), dim3(tiles(256, 28)), dim3(256), 0, 0, src, dst, H, W); }, reps), 256);
     report("tile 640x12, 16-B nt stores", timeit([&] { hipLaunchKernelGGL((copy_tile<640, 12, 16, true>), dim3(tiles(640, 12)), dim3(256), 0, 0, src, dst, H, W); }, reps), 640);
     report("tile 1920x4, 16-B nt stores", timeit([&] { hipLaunchKernelGGL((copy_tile<1920, 4, 16, true>), dim3(tiles(1920, 4)), dim3(256), 0, 0, src, dst, H, W); }, reps), 1920);
+    if (c3) {  // 512 x 512 frames: the warp's 128 x 64 tiles and others
+      report("tile 128x64, 4-B nt stores", timeit([&] { hipLaunchKernelGGL((copy_tile<128, 64, 4, true>), dim3(tiles(128, 64)), dim3(256), 0, 0, src, dst, H, W); }, reps), 128);
+      report("tile 256x32, 4-B nt stores", timeit([&] { hipLaunchKernelGGL((copy_tile<256, 32, 4, true>), dim3(tiles(256, 32)), dim3(256), 0, 0, src, dst, H, W); }, reps), 256);
+      report("tile 512x16, 4-B nt stores", timeit([&] { hipLaunchKernelGGL((copy_tile<512, 16, 4, true>), dim3(tiles(512, 16)), dim3(256), 0, 0, src, dst, H, W); }, reps), 512);
+      report("tile 128x32, 4-B nt stores", timeit([&] { hipLaunchKernelGGL((copy_tile<128, 32, 4, true>), dim3(tiles(128, 32)), dim3(256), 0, 0, src, dst, H, W); }, reps), 128);
+    }
     if (!more) continue;
     report("tile 128x28, 4-B nt stores", timeit([&] { hipLaunchKernelGGL((copy_tile<128, 28, 4, true>), dim3(tiles(128, 28)), dim3(256), 0, 0, src, dst, H, W); }, reps), 128);
     report("tile 128x112, 4-B nt stores", timeit([&] { hipLaunchKernelGGL((copy_tile<128, 112, 4, true>), dim3(tiles(128, 112)), dim3(256), 0, 0, src, dst, H, W); }, reps), 128);
