@@ -95,7 +95,8 @@ __device__ __forceinline__ bool center_normalize(const double* px, const double*
 }
 
 // Affine model through 3 correspondences: L = [v1 v2][u1 u2]^-1 (u_k = s_k - s_0,
-// v_k = d_k - d_0), t = c_d - L c_s.
+// v_k = d_k - d_0), t = c_d - L c_s.  The reference form, with skimage's normalisation
+// scales and its degeneracy test evaluated as written (affine_fit3_fast's fallback).
 __device__ __forceinline__ HModel affine_fit3(const Pts& P, const int (&sel)[3]) {
   HModel m;
   m.ok = false;
@@ -117,6 +118,108 @@ __device__ __forceinline__ HModel affine_fit3(const Pts& P, const int (&sel)[3])
   const double g = nfd / nfs;
   const double hn2 = g * g * (((l00 * l00 + l01 * l01) + l10 * l10) + l11 * l11);
   if (1.0 / sqrt(1.0 + hn2) <= 1e-8) return m;
+  m.h[0] = l00;
+  m.h[1] = l01;
+  m.h[2] = cdx - (l00 * csx + l01 * csy);
+  m.h[3] = l10;
+  m.h[4] = l11;
+  m.h[5] = cdy - (l10 * csx + l11 * csy);
+  m.h[8] = 1.0;
+  m.ok = true;
+  return m;
+}
+
+// RN(a / 3) for 2^-600 <= |a| <= 2^600: q = RN(a y) with y = RN(1/3) is within an ulp of
+// a / 3, the residual a - 3 q is exact (fma), and RN(q + r y) is then the correctly rounded
+// quotient (Markstein); checked bit for bit against a / 3.0 on 4e8 doubles on the host.
+// At a == 0, a * y keeps the sign of the zero like the division.
+__device__ __forceinline__ double div3(double a) {
+  constexpr double y = 1.0 / 3.0;
+  const double q = a * y;
+  return a == 0.0 ? q : fma(fma(-q, 3.0, a), y, q);
+}
+__device__ __forceinline__ bool div_operand_ok(double a) {
+  const double m = fabs(a);
+  return m == 0.0 || (m >= 0x1p-600 && m <= 0x1p600);
+}
+
+// a / b for a reciprocal y = recip_newton(b) of 2^-60 <= |b| <= 2^60 and |a| in
+// div_operand_ok's range: the compiler's IEEE division sequence (v_div_scale leaves such
+// operands unscaled, v_div_fmas is then an fma, v_div_fixup changes nothing but the zero
+// numerator, whose signed zero a * y gives), so the same bits; one reciprocal serves every
+// numerator over the same b.
+__device__ __forceinline__ double recip_newton(double b) {
+  double y = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-b, y, 1.0);
+  return fma(y, e, y);
+}
+__device__ __forceinline__ double div_by(double a, double b, double y) {
+  const double q = a * y;
+  return a == 0.0 ? q : fma(fma(-b, q, a), y, q);
+}
+
+// The same model with the per-trial divisions and square roots of the reference form
+// removed (round 3; the fit was ~40 % of the f64 work of a c3 trial): the four means by
+// div3, the four quotients by det through one reciprocal, skimage's rms == 0 tests as
+// sum-of-squares <= 2^-1074 (sqrt(ss / 3) == 0 exactly there), and its
+// np.isclose(V[-1,-1], 0) test (1/sqrt(1 + g^2 |L|^2) <= 1e-8, g = nf_d / nf_s) decided
+// from g^2 ~ ss_s / ss_d: far below 1e16 it cannot hold.  Any operand outside the ranges
+// above, or |L|^2 g^2 >= 1e14, sets need_exact: the caller takes the reference form
+// (kept out of the scoring loop, whose registers it would otherwise share).  Bit-identical
+// models.
+__device__ __forceinline__ HModel affine_fit3_fast(const Pts& P, const int (&sel)[3], bool& need_exact) {
+  need_exact = false;
+  const double x0 = P.sx[sel[0]], x1 = P.sx[sel[1]], x2 = P.sx[sel[2]];
+  const double y0 = P.sy[sel[0]], y1 = P.sy[sel[1]], y2 = P.sy[sel[2]];
+  const double p0 = P.dx[sel[0]], p1 = P.dx[sel[1]], p2 = P.dx[sel[2]];
+  const double q0 = P.dy[sel[0]], q1 = P.dy[sel[1]], q2 = P.dy[sel[2]];
+  // center_normalize's sums: ((0 + v0) + v1) + v2
+  double sx = 0.0, sy = 0.0, sp = 0.0, sq = 0.0;
+  sx += x0; sx += x1; sx += x2;
+  sy += y0; sy += y1; sy += y2;
+  sp += p0; sp += p1; sp += p2;
+  sq += q0; sq += q1; sq += q2;
+  HModel m;
+  m.ok = false;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) m.h[k] = 0.0;
+  if (!(div_operand_ok(sx) && div_operand_ok(sy) && div_operand_ok(sp) && div_operand_ok(sq))) {
+    need_exact = true;
+    return m;
+  }
+  const double csx = div3(sx), csy = div3(sy), cdx = div3(sp), cdy = div3(sq);
+  auto ss6 = [](double a0, double a1, double a2, double b0, double b1, double b2, double ca, double cb) {
+    const double e0 = a0 - ca, f0 = b0 - cb, e1 = a1 - ca, f1 = b1 - cb, e2 = a2 - ca, f2 = b2 - cb;
+    double ss = 0.0;  // dev order (x0, y0, x1, y1, x2, y2), sequential (2K < 8)
+    ss += e0 * e0; ss += f0 * f0; ss += e1 * e1; ss += f1 * f1; ss += e2 * e2; ss += f2 * f2;
+    return ss;
+  };
+  const double ss_s = ss6(x0, x1, x2, y0, y1, y2, csx, csy);
+  if (ss_s <= 0x1p-1074) return m;  // rms == 0: ZeroDivisionError in skimage, no model
+  const double ss_d = ss6(p0, p1, p2, q0, q1, q2, cdx, cdy);
+  if (ss_d <= 0x1p-1074) return m;
+  const double u1x = x1 - x0, u1y = y1 - y0, u2x = x2 - x0, u2y = y2 - y0;
+  const double v1x = p1 - p0, v1y = q1 - q0, v2x = p2 - p0, v2y = q2 - q0;
+  const double det = u1x * u2y - u2x * u1y;
+  if (det == 0.0) return m;
+  const double n00 = v1x * u2y - v2x * u1y, n01 = v2x * u1x - v1x * u2x;
+  const double n10 = v1y * u2y - v2y * u1y, n11 = v2y * u1x - v1y * u2x;
+  const double adet = fabs(det);
+  if (!(adet >= 0x1p-60 && adet <= 0x1p60 && div_operand_ok(n00) && div_operand_ok(n01) && div_operand_ok(n10) &&
+        div_operand_ok(n11))) {
+    need_exact = true;
+    return m;
+  }
+  const double y = recip_newton(det);
+  const double l00 = div_by(n00, det, y), l01 = div_by(n01, det, y);
+  const double l10 = div_by(n10, det, y), l11 = div_by(n11, det, y);
+  const double L2 = ((l00 * l00 + l01 * l01) + l10 * l10) + l11 * l11;
+  if (!(L2 * (ss_s * __builtin_amdgcn_rcp(ss_d)) < 1e14)) {
+    need_exact = true;
+    return m;
+  }
   m.h[0] = l00;
   m.h[1] = l01;
   m.h[2] = cdx - (l00 * csx + l01 * csy);
@@ -330,6 +433,21 @@ __device__ __forceinline__ float score_fast_packed(const double (&h)[9], const P
   return S;
 }
 
+// Phase A's fit: affine through affine_fit3_fast (need_exact: the trial must be fitted
+// again by fit_trial), projective as fit_trial.
+template <int MODEL>
+__device__ __forceinline__ HModel fit_trial_fast(const Pts& P, uint64_t pr, bool& need_exact) {
+  if constexpr (MODEL == KCMC_MODEL_AFFINE) {
+    const int sel[3] = {(int)(pr & 0xffffu), (int)((pr >> 16) & 0xffffu), (int)((pr >> 32) & 0xffffu)};
+    return affine_fit3_fast(P, sel, need_exact);
+  } else {
+    need_exact = false;
+    const int sel[4] = {(int)(pr & 0xffffu), (int)((pr >> 16) & 0xffffu), (int)((pr >> 32) & 0xffffu),
+                        (int)((pr >> 48) & 0xffffu)};
+    return projective_fit4(P, sel);
+  }
+}
+
 template <int MODEL>
 __device__ __forceinline__ HModel fit_trial(const Pts& P, uint64_t pr) {
   if constexpr (MODEL == KCMC_MODEL_AFFINE) {
@@ -432,8 +550,10 @@ __device__ __forceinline__ void ransac_model_score_frame(
   const bool fast = tq == tq;
   int mcount = -1, flag = fast ? 0 : 1;
   if (fast) {
+    bool deferred = false;
     for (int t = tid; t < T; t += kThreads) {
-      const HModel m = fit_trial<MODEL>(P, H[t]);
+      bool need_exact;
+      const HModel m = fit_trial_fast<MODEL>(P, H[t], need_exact);
       int cnt = -1;
       float S32 = NAN;
       if (m.ok) {
@@ -441,9 +561,27 @@ __device__ __forceinline__ void ransac_model_score_frame(
         S32 = LARGE ? score_fast<MODEL>(m.h, P, N, tq, cnt) : score_fast_packed<MODEL>(m.h, pk, N, tq, cnt);
         if (!s32_certain(S32)) flag = 1;
       }
-      tC[t] = cnt;
+      deferred |= need_exact;
+      tC[t] = need_exact ? INT_MIN : cnt;
       tS[t] = (double)S32;
       mcount = max(mcount, cnt);
+    }
+    // trials whose fast fit fell outside its ranges (in practice none): the reference fit
+    if (deferred) {
+      for (int t = tid; t < T; t += kThreads) {
+        if (tC[t] != INT_MIN) continue;
+        const HModel m = fit_trial<MODEL>(P, H[t]);
+        int cnt = -1;
+        float S32 = NAN;
+        if (m.ok) {
+          cnt = 0;
+          S32 = LARGE ? score_fast<MODEL>(m.h, P, N, tq, cnt) : score_fast_packed<MODEL>(m.h, pk, N, tq, cnt);
+          if (!s32_certain(S32)) flag = 1;
+        }
+        tC[t] = cnt;
+        tS[t] = (double)S32;
+        mcount = max(mcount, cnt);
+      }
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
