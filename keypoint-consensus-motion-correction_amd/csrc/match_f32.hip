@@ -128,6 +128,47 @@ __device__ __forceinline__ void topk_key(uint32_t (&k)[kTop], uint32_t x) {
   k[0] = min(k[0], x);
 }
 
+// One distance of the tile loop: if its value bits are below ithr (some lane of the wave
+// takes the branch), key = (bits & kmask) | id enters the sorted top-6 in place and ithr
+// follows the new last key.  Hand-written because the backend gave the updated list fresh
+// registers on every insertion and copied it back (6-10 v_mov per insertion, ~15 VALU
+// instead of 9); same operations as topk_key.  kmask, id, nkmask are wave-uniform (SGPRs).
+// AFTER_MFMA: xb was written by the MFMA just issued; hipcc pads nothing inside an asm
+// string, so the string opens with the 12 wait states an 8-pass XDL result needs before a
+// VALU reads it (the later values of the tile are read more than 12 states later).
+#define KCMC_TOPK_TRY6_BODY                            \
+  "v_cmp_lt_u32 vcc, %[x], %[thr]\n\t"                 \
+  "s_and_saveexec_b64 %[sv], vcc\n\t"                  \
+  "s_cbranch_execz 1f\n\t"                             \
+  "v_and_b32 %[x], %[km], %[x]\n\t"                    \
+  "v_or_b32 %[x], %[id], %[x]\n\t"                     \
+  "v_med3_u32 %[k5], %[k4], %[k5], %[x]\n\t"           \
+  "v_med3_u32 %[k4], %[k3], %[k4], %[x]\n\t"           \
+  "v_med3_u32 %[k3], %[k2], %[k3], %[x]\n\t"           \
+  "v_med3_u32 %[k2], %[k1], %[k2], %[x]\n\t"           \
+  "v_med3_u32 %[k1], %[k0], %[k1], %[x]\n\t"           \
+  "v_min_u32 %[k0], %[k0], %[x]\n\t"                   \
+  "v_or_b32 %[thr], %[nm], %[k5]\n"                     \
+  "1:\n\t"                                             \
+  "s_or_b64 exec, exec, %[sv]"
+#define KCMC_TOPK_TRY6_OPERANDS                                                                                 \
+  : [k0] "+v"(k[0]), [k1] "+v"(k[1]), [k2] "+v"(k[2]), [k3] "+v"(k[3]), [k4] "+v"(k[4]), [k5] "+v"(k[5]),      \
+    [thr] "+v"(ithr), [x] "+v"(xb), [sv] "=&s"(saved)                                                         \
+  : [km] "s"(kmask), [id] "s"(id), [nm] "s"(nkmask)                                                           \
+  : "vcc"
+template <bool AFTER_MFMA>
+__device__ __forceinline__ void topk_try6(uint32_t (&k)[kTop], uint32_t& ithr, uint32_t xb, uint32_t kmask,
+                                          uint32_t id, uint32_t nkmask) {
+  static_assert(kTop == 6, "topk_try6 keeps a top-6");
+  uint64_t saved;
+  if constexpr (AFTER_MFMA)
+    asm volatile("s_nop 11\n\t" KCMC_TOPK_TRY6_BODY KCMC_TOPK_TRY6_OPERANDS);
+  else
+    asm volatile(KCMC_TOPK_TRY6_BODY KCMC_TOPK_TRY6_OPERANDS);
+}
+#undef KCMC_TOPK_TRY6_BODY
+#undef KCMC_TOPK_TRY6_OPERANDS
+
 // Sorted approximate top-kTop values with the frame rows of the first kTop - 1.
 struct TopK {
   float v[kTop];
@@ -453,15 +494,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 6))
       // a value whose bits are >= ithr = (last key | low bits) cannot enter the list: its
       // key would be >= the last key's truncated value, which already bounds every unlisted
       // row.  After the first few hundred rows most distances of a wave skip the insertion
-      // (the branch is per wave): 8 -> ~1 + 9 P VALU per distance (c5 lab 5.15 -> 4.65 ms)
+      // (the branch is per wave): 1 + 9 P VALU per distance, P = the share of the wave's
+      // values some lane inserts (~0.3 on the c5 data, simulated)
+      topk_try6<true>(ck, ithr, __float_as_uint(acc[0]), kmask, (uint32_t)(hh * 16) | tbase, ~kmask);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const uint32_t xb = __float_as_uint(acc[r]);
-        if (xb < ithr) {
-          topk_key(ck, ((xb & kmask) | (uint32_t)(hh * 16 + r)) | tbase);
-          ithr = ck[kTop - 1] | ~kmask;
-        }
-      }
+      for (int r = 1; r < 16; ++r)
+        topk_try6<false>(ck, ithr, __float_as_uint(acc[r]), kmask, (uint32_t)(hh * 16 + r) | tbase, ~kmask);
     }
   }
 
