@@ -382,8 +382,8 @@ def main():
     ap.add_argument("--ransac-grid", type=int, default=None,
                     help="workgroups of the RANSAC launches beside the warp (default 0: one per frame)")
     ap.add_argument("--match-beside", action="store_true", default=None,
-                    help="the match + vote also on the analysis stream, beside the warp (depth 3; "
-                         "OverlappedSlabs match_beside=True); default: the config's (c4)")
+                    help="the match + vote also on the analysis stream, beside the warp (OverlappedSlabs "
+                         "match_beside=True); default: the config's (c4)")
     ap.add_argument("--no-match-beside", dest="match_beside", action="store_false",
                     help="the match + vote on the kernel stream ahead of the warp")
     ap.add_argument("--fit-first", action="store_true",
@@ -492,8 +492,10 @@ def main():
         stage_ms["host_and_transfers"] = round(ms_step - match_ms - ransac_ms - warp_ms, 3)
     else:  # step k+1's match/consensus/RANSAC/post-processing overlap step k's warp
         if args.match_beside:
-            stage_ms["schedule"] = ("pipelined: kernel stream warp(k-2); analysis stream match+vote(k) -> "
-                                    "lookup+RANSAC(k-1) beside it; host consensus merge under the warp")
+            stage_ms["schedule"] = (("pipelined: kernel stream warp(k-1); analysis stream match+vote(k) -> "
+                                     "lookup+RANSAC(k) beside it" if args.pipeline_depth == 2 else
+                                     "pipelined: kernel stream warp(k-2); analysis stream match+vote(k) -> "
+                                     "lookup+RANSAC(k-1) beside it") + "; host consensus merge under the warp")
         else:
             stage_ms["schedule"] = ("pipelined: match+vote(k) -> warp(k-1) -> lookup+RANSAC(k)" if args.pipeline_depth == 2
                                     else "pipelined: match+vote(k) -> warp(k-2) -> lookup+RANSAC(k-1)") + (

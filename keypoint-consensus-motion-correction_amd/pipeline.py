@@ -403,11 +403,13 @@ class OverlappedSlabs:
                  ransac_grid: Optional[int] = None, match_beside: bool = False, fit_first: bool = False):
         if depth not in (2, 3):
             raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
-        if match_beside and not (corun and depth == 3):
-            raise ValueError("match_beside needs corun=True and depth=3")
+        if match_beside and not corun:
+            raise ValueError("match_beside needs corun=True")
         self.depth = depth
-        # match_beside: the match + vote of slab k also run on the analysis stream (ahead of
-        # lookup + RANSAC(k-1)), so the kernel stream carries only the warps
+        # match_beside: the match + vote of slab k also run on the analysis stream, so the
+        # kernel stream carries only the warps: depth 3 queues match(k) ahead of lookup +
+        # RANSAC(k-1) beside warp(k-2); depth 2 runs match(k), then lookup + RANSAC(k),
+        # beside warp(k-1)
         self.match_beside = bool(match_beside)
         # fit_first (depth 3, corun): queue lookup + RANSAC(k-1) before waiting for RANSAC(k-2),
         # so it starts beside match(k).  Measured slower at c3 (2.36 M vs 2.91 M frames/s,
@@ -515,6 +517,15 @@ class OverlappedSlabs:
             for t in (inp.frames, out):
                 if t is not None:
                     t.record_stream(self.stream)
+            if self.match_beside and self.depth == 2:
+                # kernel stream: warp(k-1); analysis stream: match(k) -> lookup + RANSAC(k),
+                # all of slab k beside warp(k-1); warp(k) (next submit) waits for RANSAC(k)
+                fitted, self._fitted = self._fitted, None
+                new = self._match(inp, out, mark)
+                if fitted is not None and self._device_maps():
+                    self._warp_device_maps(fitted, mark)
+                self._fitted = self._fit(new, mark)
+                return self._finish(fitted, mark) if fitted is not None else None
             if self.match_beside:
                 # kernel stream: warp(k-2); analysis stream: match(k) -> lookup + RANSAC(k-1).
                 # The merge of slab k-1 uses votes that were ready a step earlier, so the

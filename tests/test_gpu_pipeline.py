@@ -131,12 +131,13 @@ def test_config2_slab_end_to_end(dev):
 @pytest.mark.parametrize("depth,corun,grid,beside,first", [(2, False, 0, False, True), (3, False, 0, False, True),
                                                            (2, True, 0, False, True), (3, True, 0, False, True),
                                                            (3, True, 0, False, False), (2, True, 5, False, True),
-                                                           (3, True, 0, True, True)])
+                                                           (3, True, 0, True, True), (2, True, 0, True, False)])
 def test_overlapped_slabs_equal_align_slab(dev, depth, corun, grid, beside, first):
     """OverlappedSlabs (depth 2: device order match(k) -> warp(k-1) -> RANSAC(k); depth 3:
     match(k) -> warp(k-2) -> RANSAC(k-1); corun: RANSAC on a second stream beside the
     warp, optionally on a narrow grid of workgroups that walk the frames; beside: the match
-    on that stream too, ahead of RANSAC(k-1); first: at depth 3 RANSAC(k-1) queued before
+    on that stream too (depth 3: ahead of RANSAC(k-1); depth 2: match(k) and RANSAC(k) both
+    beside warp(k-1)); first: at depth 3 RANSAC(k-1) queued before
     the host waits for RANSAC(k-2)) gives the same affines and warped frames as the
     sequential align_slab."""
     F, H, W = 24, 270, 480
