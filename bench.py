@@ -64,12 +64,12 @@ class BenchConfig:
     frames_per_gpu: int
     cpu_sample: int
     descriptor: str = "u8"
-    # slabs in flight (pipeline.OverlappedSlabs depth): 3 where the host's per-step work
-    # (consensus + launch chain, ~0.9 ms) is as long as the warp it hides under (c3)
+    # slabs in flight (pipeline.OverlappedSlabs depth)
     pipeline_depth: int = 2
-    # the match + vote on the analysis stream beside the warp (OverlappedSlabs match_beside,
-    # depth 3): c4, whose 12 ms RGB warp absorbs part of the 1.5 ms match (+1.5-2 %,
-    # profiles/r03_b5_bench_c4_*.json); slower at c2 / c3 / c5
+    # the match + vote on the analysis stream beside the warp (OverlappedSlabs match_beside):
+    # c2 / c3 / c4 at depth 2 (match(k), lookup + RANSAC(k) beside warp(k-1): +0.9 % / +3.9 %
+    # / +3.5 %, profiles/r03_b9_*, r03_b10_*); c5's
+    # 4 ms float match beside its 1.6 ms warp is 12 % slower
     match_beside: bool = False
 
 
@@ -79,13 +79,13 @@ class BenchConfig:
 CONFIGS = {
     "c2": BenchConfig("c2", "BASELINE config[1]: 1080p grayscale u16, 2000 frames per GPU, ORB-like keypoints "
                       "(n_tpl=500, D=32 B, ~550/frame), rigid RANSAC 1000 trials, n_kp_global=100",
-                      1080, 1920, 1, 500, 32, 100, "euclidean", 2000, 240),
+                      1080, 1920, 1, 500, 32, 100, "euclidean", 2000, 240, match_beside=True),
     "c3": BenchConfig("c3", "BASELINE config[2]: 512x512 two-photon-style u16, 20000 frames over 8 GPUs (2500 per GPU), "
                       "n_tpl=500, D=61 B (AKAZE-sized), affine RANSAC 1000 trials, n_kp_global=50",
-                      512, 512, 1, 500, 61, 50, "affine", 2500, 60, pipeline_depth=3),
+                      512, 512, 1, 500, 61, 50, "affine", 2500, 60, match_beside=True),
     "c4": BenchConfig("c4", "BASELINE config[3]: 4K RGB u16 (2160x3840x3), 5000 frames over 8 GPUs (625 per GPU), "
                       "4096 keypoints/frame template, D=61 B, affine RANSAC 1000 trials, n_kp_global=500",
-                      2160, 3840, 3, 4096, 61, 500, "affine", 625, 4, pipeline_depth=3, match_beside=True),
+                      2160, 3840, 3, 4096, 61, 500, "affine", 625, 4, match_beside=True),
     "c5": BenchConfig("c5", "BASELINE config[4]: 1080p u16, float SIFT-style descriptors (n_tpl=4096, D=128 f32, "
                       "~4500/frame), homography RANSAC 1000 trials, n_kp_global=200, warpPerspective; "
                       "500 frames per GPU", 1080, 1920, 1, 4096, 128, 200, "projective", 500, 2, "f32"),
@@ -376,7 +376,7 @@ def main():
                          "detection + the hot path (pipeline.align_frames); reported as `with_detection`")
     ap.add_argument("--pipeline-depth", type=int, default=None, choices=(2, 3),
                     help="slabs in flight in the pipelined schedule (pipeline.OverlappedSlabs depth; "
-                         "default: the config's, 3 for c3 and 2 otherwise)")
+                         "default: the config's, 2)")
     ap.add_argument("--no-corun", action="store_true",
                     help="RANSAC behind the warp on the one kernel stream (OverlappedSlabs corun=False)")
     ap.add_argument("--ransac-grid", type=int, default=None,
@@ -398,7 +398,7 @@ def main():
     if args.pipeline_depth is None:
         args.pipeline_depth = bc.pipeline_depth
     if args.match_beside is None:
-        args.match_beside = bc.match_beside and not args.no_corun and args.pipeline_depth == 3
+        args.match_beside = bc.match_beside and not args.no_corun
     if args.cpu_sample is None:
         args.cpu_sample = bc.cpu_sample * max(1, args.cpu_procs) // 2
 
