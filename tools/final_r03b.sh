@@ -3,7 +3,7 @@
 # GPU tests, smoke, tools/profile_round.sh at c2 and at c4 (bench line with the CPU
 # baseline, rocprofv3 kernel summary, warp PMC passes), the c3 / c5 bench lines.
 set -u
-OUT=${1:-gpurun_out/r03_close}
+OUT=${1:-gpurun_out/r03_close2}
 mkdir -p "$OUT"
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
 echo "tests rc=$?" >> "$OUT/gpu_tests.log"; tail -2 "$OUT/gpu_tests.log"
