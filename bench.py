@@ -71,6 +71,9 @@ class BenchConfig:
     # / +3.5 %, profiles/r03_b9_*, r03_b10_*); c5's
     # 4 ms float match beside its 1.6 ms warp is 12 % slower
     match_beside: bool = False
+    # CUs per shader engine of the analysis stream's fixed CU slice (OverlappedSlabs
+    # ana_cus_per_se; 0: both streams share every CU)
+    ana_cus_per_se: int = 0
 
 
 # BASELINE.json configs.  c2 (configs[1]) is the headline line; the others are the
@@ -217,6 +220,27 @@ def isolated_stage_ms(inp, cfg, out, reps=7):
             "warp": round(warp_ms, 4)}, cons
 
 
+def host_cpus():
+    """(usable CPUs, os.cpu_count(), sched_getaffinity size, cgroup CPU quota or None) of
+    this host.  The reference sizes its joblib pool with multiprocessing.cpu_count() (VA:21,
+    VA:462); the processes it can actually run at once are the affinity set, bounded by the
+    container's CPU quota (cgroup v2 cpu.max) when there is one."""
+    import math
+
+    total = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, math.ceil(quota)))
+    return usable, total, aff, quota
+
+
 def _cpu_pool(procs: int, initargs):
     """`procs` spawned worker processes (oracle/cpu_baseline_workers.py).  The children
     must not re-run this script's imports (torch, the HIP library), so the main module's
@@ -229,7 +253,7 @@ def _cpu_pool(procs: int, initargs):
     saved = main.__dict__.pop("__file__", None)
     try:
         pool = mp.get_context("spawn").Pool(procs, initializer=W.init, initargs=initargs)
-        pool.map(W.ping, range(procs))
+        pool.map(W.ping, range(procs), chunksize=1)
     finally:
         if saved is not None:
             main.__file__ = saved
@@ -241,38 +265,51 @@ def cpu_baseline(bc: BenchConfig, ks, n_sample: int, procs: int):
     like the reference: the per-frame stages (C knnMatch + the reference's numpy filters;
     the numpy/LAPACK restatement of skimage 0.18.3 ransac with per-trial SVD; C warp) in
     `procs` single-threaded worker processes over frame chunks (the reference's joblib
-    pool, VA:460-465), CPython consensus in the parent."""
+    pool, VA:460-465), CPython consensus in the parent.  `procs` defaults to the host's
+    usable CPUs (host_cpus): the reference's cpu_count()-sized pool as this host runs it."""
+    import shutil
+    import tempfile
+
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # cpu_baseline leg: the oracle is what is timed here
     import cpu_baseline_workers as W
     from threadpoolctl import threadpool_limits
 
+    usable, total, aff, quota = host_cpus()
     base = make_texture(bc)
-    initargs = (ks.des_tpl, ks.kp_tpl, ks.des_q, ks.kp_q, ks.q_off, base, bc.model, bc.descriptor)
     procs = max(1, min(procs, n_sample))
+    arrays = dict(des_tpl=ks.des_tpl, kp_tpl=ks.kp_tpl, des_q=ks.des_q, kp_q=ks.kp_q, q_off=ks.q_off, base=base)
+    tmp = None
     chunks = [c.tolist() for c in np.array_split(np.arange(n_sample), procs)]
     with threadpool_limits(1):
         if procs == 1:
-            W.init(*initargs)
+            W.init(arrays, bc.model, bc.descriptor)
             run = lambda fn, args: [fn(a) for a in args]  # noqa: E731
             pool = None
         else:
-            pool = _cpu_pool(procs, initargs)
-            run = pool.map
-        t0 = time.perf_counter()
-        res = run(W.match_chunk, chunks)
-        sets = [s for r in res for s, _ in r]
-        kqs = [kq for r in res for _, kq in r]
-        t1 = time.perf_counter()
-        cons, _, _ = oracle.consensus(sets, bc.n_kp_global)
-        lists = oracle.lookup(cons, sets)
-        t2 = time.perf_counter()
-        run(W.ransac_warp_chunk, [[(kqs[f], lists[f]) for f in c] for c in chunks])
-        t3 = time.perf_counter()
-        if pool is not None:
-            pool.close()
-            pool.join()
-    total = t3 - t0
+            tmp = tempfile.mkdtemp(prefix="kcmc_cpu_", dir="/tmp")
+            for k, a in arrays.items():
+                np.save(os.path.join(tmp, k + ".npy"), np.ascontiguousarray(a))
+            pool = _cpu_pool(procs, (tmp, bc.model, bc.descriptor))
+            run = lambda fn, args: pool.map(fn, args, chunksize=1)  # noqa: E731
+        try:
+            t0 = time.perf_counter()
+            res = run(W.match_chunk, chunks)
+            sets = [s for r in res for s, _ in r]
+            kqs = [kq for r in res for _, kq in r]
+            t1 = time.perf_counter()
+            cons, _, _ = oracle.consensus(sets, bc.n_kp_global)
+            lists = oracle.lookup(cons, sets)
+            t2 = time.perf_counter()
+            run(W.ransac_warp_chunk, [[(kqs[f], lists[f]) for f in c] for c in chunks])
+            t3 = time.perf_counter()
+        finally:
+            if pool is not None:
+                pool.close()
+                pool.join()
+            if tmp is not None:
+                shutil.rmtree(tmp, ignore_errors=True)
+    total_s = t3 - t0
     calib = ""
     try:  # the port against the reference's own code, measured in the build container
         with open(os.path.join(REPO, "profiles", "r03_cpu_reference_calibration.json")) as f:
@@ -285,17 +322,23 @@ def cpu_baseline(bc: BenchConfig, ks, n_sample: int, procs: int):
     except (OSError, ValueError, KeyError):
         pass
     return {
-        "value": n_sample / total,
+        "value": n_sample / total_s,
         "unit": "aligned frames/s",
-        "cores": procs,
+        "cores": min(procs, usable),
         "kind": "port",
+        "processes": procs,
+        "host": {"usable_cpus": usable, "os_cpu_count": total, "sched_getaffinity": aff,
+                 "cgroup_cpu_quota": quota},
         "sample": (f"{n_sample} frames of {bc.name} ({bc.H}x{bc.W}x{bc.C} u16, n_tpl={bc.n_tpl}, D={bc.D}, "
                    f"n_kp_global={bc.n_kp_global}, {bc.model}), {procs} single-threaded worker process(es) "
-                   f"like the reference's joblib pool: match {1e3 * (t1 - t0):.0f} ms "
+                   f"like the reference's joblib pool (VA:21 sizes it by multiprocessing.cpu_count() = "
+                   f"{total} here; this host runs {usable} at once: sched_getaffinity {aff}, cgroup quota "
+                   f"{'none' if quota is None else f'{quota:g} CPUs'}; {n_sample / procs:.1f} frames per process): "
+                   f"match {1e3 * (t1 - t0):.0f} ms "
                    f"(C oracle knnMatch + reference numpy filters), consensus {1e3 * (t2 - t1):.1f} ms "
                    f"(CPython set/Counter, parent), RANSAC + warp {1e3 * (t3 - t2):.0f} ms "
                    f"(numpy/LAPACK restatement of skimage 0.18.3 with 1000 trials; C warp)" + calib),
-        "seconds": total,
+        "seconds": total_s,
     }
 
 
@@ -366,8 +409,11 @@ def main():
                     help="BASELINE workload (c2 = configs[1], the headline line)")
     ap.add_argument("--frames", type=int, default=None, help="frames per GPU (default: the config's)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="frames in the CPU-baseline sample (0: skip)")
-    ap.add_argument("--cpu-procs", type=int, default=8,
-                    help="worker processes of the CPU baseline (the reference's per-core pool)")
+    ap.add_argument("--cpu-procs", type=int, default=None,
+                    help="worker processes of the CPU baseline (default: the host's usable CPUs, the "
+                         "reference's cpu_count()-sized pool as this host runs it)")
+    ap.add_argument("--cpu-procs-secondary", type=int, default=8,
+                    help="also time the CPU baseline at this many processes (the round-1..3 figure; 0: skip)")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the PCIe-inclusive path: frames in pinned host memory, streamed through "
                          "the warp in slabs (pipeline.align_streamed); reported as `end_to_end`, not `value`")
@@ -389,6 +435,11 @@ def main():
     ap.add_argument("--fit-first", action="store_true",
                     help="depth 3: queue lookup + RANSAC(k-1) before warp(k-2) (OverlappedSlabs fit_first=True; "
                          "measured slower at c3)")
+    ap.add_argument("--ana-cus", type=int, default=None,
+                    help="CUs per shader engine (of 8) reserved for the analysis stream (OverlappedSlabs "
+                         "ana_cus_per_se; default: the config's, 0 = no CU split)")
+    ap.add_argument("--warp-shares", action="store_true",
+                    help="with --ana-cus: the warp stream keeps every CU (only the analysis is confined)")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
@@ -397,10 +448,16 @@ def main():
         args.frames = bc.frames_per_gpu
     if args.pipeline_depth is None:
         args.pipeline_depth = bc.pipeline_depth
+    if args.ana_cus is None:
+        args.ana_cus = bc.ana_cus_per_se if not args.no_corun else 0
     if args.match_beside is None:
         args.match_beside = bc.match_beside and not args.no_corun
+    if args.cpu_procs is None:
+        args.cpu_procs = host_cpus()[0]
     if args.cpu_sample is None:
-        args.cpu_sample = bc.cpu_sample * max(1, args.cpu_procs) // 2
+        # at least 4 frames per process, within the frames the config makes
+        args.cpu_sample = min(max(bc.cpu_sample * max(1, args.cpu_procs) // 2, 4 * args.cpu_procs),
+                              args.frames if args.frames else bc.frames_per_gpu)
 
     # KCMC_BENCH_BACKEND=gloo + KCMC_BENCH_ONE_DEVICE=1: rehearsal of the multi-rank
     # path with every rank on cuda:0 (a 1-GPU box cannot host two RCCL ranks)
@@ -430,7 +487,9 @@ def main():
                                                             depth=args.pipeline_depth, corun=not args.no_corun,
                                                             ransac_grid=args.ransac_grid,
                                                             match_beside=args.match_beside,
-                                                            fit_first=args.fit_first)
+                                                            fit_first=args.fit_first,
+                                                            ana_cus_per_se=args.ana_cus,
+                                                            warp_exclusive=not args.warp_shares)
 
     def step(timer):
         if ov is None:
@@ -501,6 +560,10 @@ def main():
                                     else "pipelined: match+vote(k) -> warp(k-2) -> lookup+RANSAC(k-1)") + (
                                         " on one stream" if args.no_corun else ", RANSAC on a second stream beside the warp"
                                     ) + ", host consensus merge under the warp"
+        if args.ana_cus:
+            stage_ms["schedule"] += (f"; analysis stream on {args.ana_cus} of 8 CUs per shader engine"
+                                     + (", the warp on every CU" if args.warp_shares else ", the warp on the other "
+                                        f"{8 - args.ana_cus}"))
         stage_ms["step_minus_warp"] = round(ms_step - warp_ms, 3)
         # rank 0's host seconds per step blocked in event waits / inside the all-gathers, and
         # its consensus merge / post-processing (OverlappedSlabs.stats)
@@ -600,6 +663,10 @@ def main():
         result["with_detection"] = with_detection(inp, cfg, dev, world)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         result["cpu_baseline"] = cpu_baseline(bc, ks, args.cpu_sample, args.cpu_procs)
+        p2 = args.cpu_procs_secondary
+        if p2 and p2 != args.cpu_procs:
+            sec = cpu_baseline(bc, ks, min(args.cpu_sample, max(4 * p2, bc.cpu_sample * p2 // 2)), p2)
+            result["cpu_baseline"]["secondary"] = {k: sec[k] for k in ("value", "cores", "processes", "seconds")}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

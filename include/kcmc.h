@@ -71,6 +71,16 @@ const char* kcmc_last_error(void);
  * transfers of a pipelined caller (e.g. kcmc_amd.pipeline) without a runtime binding of its own. */
 int kcmc_memcpy_async(void* dst, const void* src, size_t bytes, kcmc_stream_t stream);
 
+/* A stream of `device` whose kernels run on a fixed CU subset (hipExtStreamCreateWithCUMask):
+ * the first `cus_per_se` CUs of EVERY shader engine of every XCD, or with `complement` the
+ * other CUs of every shader engine.  The pipeline's analysis / warp stream split (no
+ * reference counterpart: the reference's joblib pool has no device).  Every XCD and every
+ * shader engine keeps CUs in both halves (a mask that empties an XCD can leave a dispatch's
+ * workgroups unplaceable); KCMC_EUNSUPPORTED on a device whose CU count is not 8 XCDs x 4
+ * shader engines x 8 CUs (the layout verified on MI355X). */
+int kcmc_stream_create_cu_split(int device, int cus_per_se, int complement, kcmc_stream_t* out);
+int kcmc_stream_destroy(kcmc_stream_t stream);
+
 /* Create / destroy the per-device context (holds the uploaded RANSAC hypothesis
  * tables).  `device` is a HIP device ordinal. */
 int kcmc_create(int device, kcmc_ctx** out);
@@ -189,8 +199,8 @@ int kcmc_consensus_merge(const int64_t* votes_host, int world, int n_tpl, int n_
                          int32_t* out_cons_pack_host);
 /* Device lookup: cons_pack_dev = kcmc_consensus_merge's pack (nc entries + bitmask words);
  * out_pt_off_dev [n_frames + 1], out_pt_idx_dev [n_frames * nc]; scratch_dev of at least
- * kcmc_consensus_lookup_scratch_bytes(n_frames, nc) bytes (CPython set emulation tables of the
- * frames whose order is not ascending). */
+ * kcmc_consensus_lookup_scratch_bytes(n_frames, nc) bytes (the CPython set emulation tables
+ * that do not fit in LDS; 0 bytes -- scratch_dev may be NULL -- while nc < 308). */
 long long kcmc_consensus_lookup_scratch_bytes(int n_frames, int nc);
 int kcmc_consensus_lookup(kcmc_ctx* ctx, const uint32_t* keep_bits_dev, int n_frames, int n_tpl,
                           const int32_t* cons_pack_dev, int nc, int32_t* out_pt_off_dev,

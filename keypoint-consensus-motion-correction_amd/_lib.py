@@ -25,6 +25,8 @@ EXPORTED_SYMBOLS = (
     "kcmc_abi_version",
     "kcmc_last_error",
     "kcmc_memcpy_async",
+    "kcmc_stream_create_cu_split",
+    "kcmc_stream_destroy",
     "kcmc_create",
     "kcmc_destroy",
     "kcmc_knn2_l2u8",
@@ -89,6 +91,8 @@ _SIGNATURES = {
     "kcmc_abi_version": ([], I),
     "kcmc_last_error": ([], ctypes.c_char_p),
     "kcmc_memcpy_async": ([P, P, ctypes.c_size_t, P], I),
+    "kcmc_stream_create_cu_split": ([I, I, I, ctypes.POINTER(P)], I),
+    "kcmc_stream_destroy": ([P], I),
     "kcmc_create": ([I, ctypes.POINTER(P)], I),
     "kcmc_destroy": ([P], I),
     "kcmc_knn2_l2u8": ([P, P, I, I, P, P, I, I, P, P, P], I),

@@ -5,6 +5,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "kcmc_internal.h"
 
 namespace kcmc {
@@ -42,6 +44,47 @@ extern "C" int kcmc_memcpy_async(void* dst, const void* src, size_t bytes, kcmc_
   if (bytes == 0) return KCMC_OK;
   if (!dst || !src) return fail(KCMC_EINVAL, "kcmc_memcpy_async: NULL pointer");
   return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)stream), "hipMemcpyAsync");
+}
+
+// CU-mask layout of a 256-CU MI355X (tools/cu_mask_lab.hip, profiles/r02_cu_mask_layout.txt):
+// bit b of the mask selects XCD b % 8, shader engine (b / 8) % 4 of it and CU b / 32 of that
+// shader engine, so bits [0, 32 n) are the first n CUs of every shader engine.
+constexpr int kMaskXcds = 8, kMaskSes = 4, kMaskCusPerSe = 8;
+constexpr int kMaskBits = kMaskXcds * kMaskSes * kMaskCusPerSe;
+
+extern "C" int kcmc_stream_create_cu_split(int device, int cus_per_se, int complement, kcmc_stream_t* out) {
+  if (!out) return fail(KCMC_EINVAL, "kcmc_stream_create_cu_split: out is NULL");
+  if (cus_per_se < 1 || cus_per_se >= kMaskCusPerSe)
+    return fail(KCMC_EINVAL, "kcmc_stream_create_cu_split: cus_per_se must be in [1, 7] (both halves keep CUs "
+                             "in every shader engine)");
+  int n = 0;
+  KCMC_TRY(hip_check(hipGetDeviceCount(&n), "hipGetDeviceCount"));
+  if (device < 0 || device >= n) return fail(KCMC_EINVAL, "kcmc_stream_create_cu_split: device out of range");
+  int cus = 0;
+  KCMC_TRY(hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device),
+                     "hipDeviceGetAttribute(CU count)"));
+  if (cus != kMaskBits)
+    return fail(KCMC_EUNSUPPORTED, "kcmc_stream_create_cu_split: the CU-mask layout is known for 256-CU devices "
+                                   "only (this one has " + std::to_string(cus) + ")");
+  uint32_t mask[kMaskBits / 32];
+  for (int w = 0; w < kMaskBits / 32; ++w) {
+    const bool first = w < cus_per_se;  // word w = CU w of every (XCD, shader engine)
+    mask[w] = (first != (complement != 0)) ? 0xffffffffu : 0u;
+  }
+  int prev = 0;
+  hipGetDevice(&prev);
+  KCMC_TRY(hip_check(hipSetDevice(device), "hipSetDevice"));
+  hipStream_t s = nullptr;
+  const int rc = hip_check(hipExtStreamCreateWithCUMask(&s, kMaskBits / 32, mask), "hipExtStreamCreateWithCUMask");
+  hipSetDevice(prev);
+  KCMC_TRY(rc);
+  *out = (kcmc_stream_t)s;
+  return KCMC_OK;
+}
+
+extern "C" int kcmc_stream_destroy(kcmc_stream_t stream) {
+  if (!stream) return KCMC_OK;
+  return hip_check(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
 }
 
 extern "C" int kcmc_create(int device, kcmc_ctx** out) {
@@ -181,12 +224,15 @@ extern "C" int kcmc_ransac_prepare(kcmc_ctx* ctx, const int32_t* n_values, int c
   if (!ctx) return fail(KCMC_EINVAL, "kcmc_ransac_prepare: ctx is NULL");
   if (count < 0 || (count > 0 && !n_values) || trials < 1)
     return fail(KCMC_EINVAL, "kcmc_ransac_prepare: bad arguments");
+  // one (trials, seed) table set per context: another seed or trial count replaces it, and
+  // the device copy must follow even when no count is new
+  bool changed = ctx->hyp == nullptr;
   if (ctx->hyp_trials != trials || ctx->hyp_seed != seed) {
     ctx->hyp_host.clear();
     ctx->hyp_trials = trials;
     ctx->hyp_seed = seed;
+    changed = true;
   }
-  bool changed = ctx->hyp == nullptr;
   std::vector<int32_t> tab((size_t)trials * 2);
   for (int k = 0; k < count; ++k) {
     const int n = n_values[k];
@@ -241,12 +287,13 @@ extern "C" int kcmc_ransac_prepare_samples(kcmc_ctx* ctx, int min_samples, const
   if (count < 0 || (count > 0 && !n_values) || trials < 1)
     return fail(KCMC_EINVAL, "kcmc_ransac_prepare_samples: bad arguments");
   HypTables& T = ctx->mhyp[min_samples];
+  bool changed = T.dev == nullptr;
   if (T.trials != trials || T.seed != seed) {
     T.host.clear();
     T.trials = trials;
     T.seed = seed;
+    changed = true;
   }
-  bool changed = T.dev == nullptr;
   std::vector<int32_t> tab((size_t)trials * min_samples);
   for (int k = 0; k < count; ++k) {
     const int n = n_values[k];

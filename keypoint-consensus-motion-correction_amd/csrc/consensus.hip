@@ -119,6 +119,13 @@ constexpr int kEmuLanes = 64;     // vote_key_kernel replays of non-ascending fi
 constexpr int kCountThreads = 64;
 constexpr uint32_t kOrderLdsCap = 2048;  // lookup_order_kernel keeps set tables up to this size in LDS
 
+// lookup_order_kernel's set tables: R (the result, 2 cap words) in LDS when cap <= kOrderLdsCap,
+// S (the frame's own set, 2 cap words) when cap <= kOrderLdsCap / 2; the tables that do not
+// fit live in a per-frame global scratch of this many words
+__host__ __device__ inline uint32_t lookup_scratch_words(uint32_t cap) {
+  return (cap <= kOrderLdsCap ? 0u : 2u * cap) + (cap <= kOrderLdsCap / 2 ? 0u : 2u * cap);
+}
+
 // cnt[t] += frames of the chunk holding t; first_enc[t] = max(0x7fffffff - first frame):
 // scratch in the key row of the output (zeroed before the launch).
 __global__ __launch_bounds__(kVoteThreads) void vote_count_kernel(const uint32_t* __restrict__ keep, int F, int n_tpl,
@@ -338,9 +345,10 @@ __global__ __launch_bounds__(64) void lookup_order_kernel(
     stage_bits(consS, out);
     return;
   }
-  int32_t* R0 = r_lds ? tabS : scratch + (size_t)f * 4 * cap;
+  int32_t* fscr = scratch + (size_t)f * lookup_scratch_words(cap);  // r_lds / s_lds follow the same rule
+  int32_t* R0 = r_lds ? tabS : fscr;
   int32_t* R1 = R0 + cap;
-  int32_t* S0 = s_lds ? tabS + 2 * cap : scratch + (size_t)f * 4 * cap + 2 * cap;
+  int32_t* S0 = s_lds ? tabS + 2 * cap : fscr + (r_lds ? 0 : 2 * cap);
   // ---- the result's keys in insertion order -> keyS[0, m)
   if ((uint32_t)flen > (uint32_t)nc) {  // set_intersection iterates the smaller set: the consensus
     int n = 0;
@@ -468,7 +476,8 @@ extern "C" int kcmc_consensus_vote(kcmc_ctx* ctx, const uint32_t* keep_bits, int
 
 extern "C" long long kcmc_consensus_lookup_scratch_bytes(int n_frames, int nc) {
   if (n_frames < 0 || nc < 0) return -1;
-  return (long long)n_frames * 4 * (long long)pyset_table_size((uint32_t)nc) * (long long)sizeof(int32_t);
+  return (long long)n_frames * (long long)lookup_scratch_words(pyset_table_size((uint32_t)nc)) *
+         (long long)sizeof(int32_t);
 }
 
 extern "C" int kcmc_consensus_lookup(kcmc_ctx* ctx, const uint32_t* keep_bits, int n_frames, int n_tpl,
@@ -482,7 +491,8 @@ extern "C" int kcmc_consensus_lookup(kcmc_ctx* ctx, const uint32_t* keep_bits, i
   if (nc == 0 || n_tpl == 0)
     return hip_check(hipMemsetAsync(out_pt_off, 0, (size_t)(n_frames + 1) * sizeof(int32_t), s),
                      "hipMemsetAsync(pt_off)");
-  if (!keep_bits || !cons_pack || !out_pt_idx || !scratch)
+  const uint32_t cap = pyset_table_size((uint32_t)nc);
+  if (!keep_bits || !cons_pack || !out_pt_idx || (!scratch && lookup_scratch_words(cap) > 0))
     return fail(KCMC_EINVAL, "kcmc_consensus_lookup: NULL pointer");
   const int W = (n_tpl + 31) / 32;
   const uint32_t* cons_bits = reinterpret_cast<const uint32_t*>(cons_pack + nc);
@@ -491,7 +501,6 @@ extern "C" int kcmc_consensus_lookup(kcmc_ctx* ctx, const uint32_t* keep_bits, i
   KCMC_TRY(launch_check("lookup_count_kernel"));
   hipLaunchKernelGGL(lookup_scan_kernel, dim3(1), dim3(64), 0, s, n_frames, out_pt_off);
   KCMC_TRY(launch_check("lookup_scan_kernel"));
-  const uint32_t cap = pyset_table_size((uint32_t)nc);
   const int r_lds = cap <= kOrderLdsCap, s_lds = cap <= kOrderLdsCap / 2;
   const size_t lds = ((size_t)2 * W + nc + (r_lds ? 2 * cap : 0) + (s_lds ? 2 * cap : 0)) * sizeof(int32_t);
   hipLaunchKernelGGL(lookup_order_kernel, dim3(n_frames), dim3(64), lds, s, keep_bits, n_frames, W, cons_pack, nc,

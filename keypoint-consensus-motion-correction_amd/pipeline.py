@@ -209,6 +209,9 @@ def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.C
     Device point lists (device_consensus / lookup_stage) run with the tables of every
     count up to n_kp_global; host lists (consensus_stage) are uploaded first unless
     ``lists_dev`` holds them already."""
+    if cfg.ransac_model == "euclidean" and cfg.ransac_min_samples != 2:
+        # every path (host or device lists) fits EuclideanTransform's 2-point model
+        raise ValueError("rigid RANSAC uses min_samples=2 (EuclideanTransform, VA:312)")
     dev = kp_tpl.device
     F, n_tpl = match.kp_ordered.shape[:2]
     src = match.kp_ordered.view(F * n_tpl, 2)
@@ -400,7 +403,8 @@ class OverlappedSlabs:
 
     def __init__(self, device, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
                  counts: Optional[List[int]] = None, group=None, depth: int = 2, corun: bool = True,
-                 ransac_grid: Optional[int] = None, match_beside: bool = False, fit_first: bool = False):
+                 ransac_grid: Optional[int] = None, match_beside: bool = False, fit_first: bool = False,
+                 ana_cus_per_se: int = 0, warp_exclusive: bool = True):
         if depth not in (2, 3):
             raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
         if match_beside and not corun:
@@ -425,13 +429,25 @@ class OverlappedSlabs:
         self.logger = logger
         self.counts = counts
         self.group = group
-        self.stream = torch.cuda.Stream(self.dev)
+        # ana_cus_per_se: the analysis stream's kernels run on the first n CUs of every
+        # shader engine (a fixed CU slice, stages.cu_split_stream), and with warp_exclusive
+        # the kernel stream's on the other 8 - n; 0 = both streams on every CU
+        self.ana_cus_per_se = int(ana_cus_per_se or 0)
+        if self.ana_cus_per_se and not corun:
+            raise ValueError("ana_cus_per_se needs corun=True (an analysis stream)")
+        if self.ana_cus_per_se and warp_exclusive:
+            self.stream = stages.cu_split_stream(self.dev, self.ana_cus_per_se, complement=True)
+        else:
+            self.stream = torch.cuda.Stream(self.dev)
         self.copy = torch.cuda.Stream(self.dev)  # vote / consensus / params / map transfers
         # corun: lookup + RANSAC(k) on an analysis stream, beside warp(k-1) instead of behind
         # it (the warp of slab k waits for it).  Same-box A/B: faster at
         # c2, c3 and c5; the match stays on the kernel stream (beside the warp it starves).
         self.corun = bool(corun)
-        self.ana = torch.cuda.Stream(self.dev) if self.corun else None
+        if self.ana_cus_per_se:
+            self.ana = stages.cu_split_stream(self.dev, self.ana_cus_per_se)
+        else:
+            self.ana = torch.cuda.Stream(self.dev) if self.corun else None
         self._hs = self.stream.cuda_stream
         self._hc = self.copy.cuda_stream
         self._ha = self.ana.cuda_stream if self.corun else self._hs
@@ -584,6 +600,8 @@ class OverlappedSlabs:
         if self.match_beside:
             return self._match_beside(inp, out, mark)
         self._at_tail(mark, "m0")
+        for t in (inp.des_tpl, inp.kp_tpl, inp.des_q, inp.kp_q, inp.q_off):
+            t.record_stream(self.stream)
         match = match_stage(inp, self.cfg, stream=self._hs)
         n_tpl = inp.des_tpl.shape[0]
         votes = stages.consensus_vote(match.keep_bits, n_tpl, self._f0, stream=self._hs)
@@ -602,6 +620,10 @@ class OverlappedSlabs:
         RANSAC of the previous slab; the (gathered) votes to the host."""
         n_tpl = inp.des_tpl.shape[0]
         with torch.cuda.stream(self.ana):
+            # the match reads the slab's descriptors / keypoints on the analysis stream: keep
+            # their memory from being reused by the caller's stream until it has
+            for t in (inp.des_tpl, inp.kp_tpl, inp.des_q, inp.kp_q, inp.q_off):
+                t.record_stream(self.ana)
             m0 = torch.cuda.Event(enable_timing=True)
             m0.record(self.ana)
             mark("m0", m0)
@@ -669,9 +691,13 @@ class OverlappedSlabs:
             self._d2h(p.slot.buf("bound", bound.numel(), torch.float64), bound, after, p.slot.params_ev)
         else:
             after.record()
-        self._d2h(p.slot.buf("params", params.numel(), torch.float64), params, after, p.slot.params_ev)
         if logging_enabled(self.logger):
-            _log_low_counts(self.logger, np.diff(p.cons.pt_off), self.cfg, p.f0)
+            # the point counts for VA:279-283's log lines travel with the parameters (the
+            # lines are written in _finish): reading pt_off here would block the host on the
+            # analysis stream and break the overlap
+            self._d2h(p.slot.buf("pt_off", p.cons.pt_off_dev.numel(), torch.int32), p.cons.pt_off_dev, after,
+                      p.slot.params_ev)
+        self._d2h(p.slot.buf("params", params.numel(), torch.float64), params, after, p.slot.params_ev)
 
     def _warp_device_maps(self, p: _SlabInFlight, mark) -> None:
         if p.fitted_ev is not None:
@@ -689,6 +715,9 @@ class OverlappedSlabs:
         """Host post-processing of slab p (VA:143-145) and the warps that need its maps."""
         self._wait(p.slot.params_ev)  # after RANSAC(k): its parameters are on the host
         n = p.inp.frames.shape[0]
+        if logging_enabled(self.logger) and "pt_off" in p.slot.bufs:
+            pt_off = p.slot.buf("pt_off", p.cons.pt_off_dev.numel(), torch.int32).numpy()
+            _log_low_counts(self.logger, np.diff(pt_off), self.cfg, p.f0)
         shape = tuple(p.rr.params.shape)
         params = p.slot.buf("params", p.rr.params.numel(), torch.float64).numpy().reshape(shape)
         t0 = time.perf_counter()

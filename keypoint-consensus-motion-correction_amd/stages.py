@@ -75,6 +75,27 @@ def _ctx(device: torch.device) -> _lib.Context:
     return _lib.context(device.index if device.index is not None else torch.cuda.current_device())
 
 
+_CU_SPLIT_STREAMS = {}
+
+
+def cu_split_stream(device, cus_per_se: int, complement: bool = False) -> torch.cuda.ExternalStream:
+    """A stream whose kernels run on the first ``cus_per_se`` CUs of every shader engine
+    (``complement``: on the other CUs), as a torch ExternalStream (C ABI
+    kcmc_stream_create_cu_split).  One per (device, split, half), created on first use and
+    kept for the life of the process (in-flight work may still reference it)."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = (idx, int(cus_per_se), bool(complement))
+    st = _CU_SPLIT_STREAMS.get(key)
+    if st is None:
+        h = _P()
+        _lib.check(_lib.load().kcmc_stream_create_cu_split(idx, int(cus_per_se), int(bool(complement)),
+                                                          ctypes.byref(h)))
+        st = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+        _CU_SPLIT_STREAMS[key] = st
+    return st
+
+
 # ----------------------------------------------------------------------- K1
 @dataclass
 class MatchResult:
@@ -325,7 +346,9 @@ def consensus_lookup(keep_bits: torch.Tensor, n_tpl: int, pack_dev: torch.Tensor
     L = _lib.load()
     pt_off = torch.empty(F + 1, dtype=torch.int32, device=dev)
     pt_idx = torch.empty(max(F * nc, 1), dtype=torch.int32, device=dev)
-    scratch = torch.empty(max(int(L.kcmc_consensus_lookup_scratch_bytes(F, nc)), 4), dtype=torch.uint8, device=dev)
+    # the set tables that do not fit in LDS (0 bytes for nc < 308: table size <= 1024)
+    sb = int(L.kcmc_consensus_lookup_scratch_bytes(F, nc))
+    scratch = torch.empty(sb, dtype=torch.uint8, device=dev) if sb > 0 else None
     _lib.check(L.kcmc_consensus_lookup(_ctx(dev).handle, _ptr(keep_bits), F, int(n_tpl), _ptr(pack_dev), int(nc),
                                        _ptr(pt_off), _ptr(pt_idx), _ptr(scratch), _stream(dev, stream)))
     return pt_off, pt_idx
@@ -509,26 +532,27 @@ def ransac_model(
     return res
 
 
-_PREPARED_RANGES = set()
-
-
 def ransac_prepare_range(device, model: str, n_lo: int, n_hi: int, trials: int = 1000, seed: int = 42) -> None:
-    """Upload the hypothesis tables of every point count in [n_lo, n_hi] once (the device
-    lookup's point counts are not seen by the host; every count a frame can have is ready)."""
+    """Make the hypothesis tables of every point count in [n_lo, n_hi] current on the
+    device (the device lookup's point counts are not seen by the host; every count a frame
+    can have is ready).  Called before every device-list RANSAC: the context keeps ONE
+    (trials, seed) table set per min_samples, and another caller on the same context
+    (ransac_rigid / ransac_model, or an aligner with another RANDOM_SEED) may have
+    replaced it since; the C side regenerates only the counts it lacks and re-uploads
+    only when the set changed, so a repeat call is one host loop over the range."""
     dev = torch.device(device)
     ctx = _ctx(dev)
     ms = _lib.MODEL_MIN_SAMPLES[model]
     n_lo = max(int(n_lo), ms + 1, 3)
-    key = (id(ctx), ms, n_lo, int(n_hi), int(trials), int(seed) & 0xFFFFFFFF)
-    if key in _PREPARED_RANGES or n_hi < n_lo:
+    if int(n_hi) < n_lo:
         return
     n_run = np.arange(n_lo, int(n_hi) + 1, dtype=np.int32)
     L = _lib.load()
+    seed = int(seed) & 0xFFFFFFFF
     if ms == 2:
-        _lib.check(L.kcmc_ransac_prepare(ctx.handle, _np_ptr(n_run), int(n_run.size), int(trials), key[-1]))
+        _lib.check(L.kcmc_ransac_prepare(ctx.handle, _np_ptr(n_run), int(n_run.size), int(trials), seed))
     else:
-        _lib.check(L.kcmc_ransac_prepare_samples(ctx.handle, ms, _np_ptr(n_run), int(n_run.size), int(trials), key[-1]))
-    _PREPARED_RANGES.add(key)
+        _lib.check(L.kcmc_ransac_prepare_samples(ctx.handle, ms, _np_ptr(n_run), int(n_run.size), int(trials), seed))
 
 
 def ransac_lists(model: str, src: torch.Tensor, dst: torch.Tensor, pt_off: torch.Tensor, pt_idx: torch.Tensor,

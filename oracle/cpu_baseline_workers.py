@@ -17,14 +17,21 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 _S = {}
 
 
-def init(des_tpl, kp_tpl, des_q, kp_q, q_off, base, model, descriptor):
+ARRAYS = ("des_tpl", "kp_tpl", "des_q", "kp_q", "q_off", "base")
+
+
+def init(data, model, descriptor):
+    """``data``: the arrays themselves (a single in-process worker) or the directory they
+    were saved to as .npy files (pool workers memory-map them: with one process per core
+    of a large host, pickling ~50 MB of keypoints into every worker would dominate)."""
     from threadpoolctl import threadpool_limits
 
     threadpool_limits(1)  # one single-threaded process per core, like the reference's pool
     import oracle
 
-    _S.update(des_tpl=des_tpl, kp_tpl=kp_tpl, des_q=des_q, kp_q=kp_q, q_off=q_off, base=base, model=model,
-              descriptor=descriptor, oracle=oracle)
+    if isinstance(data, str):
+        data = {k: np.load(os.path.join(data, k + ".npy"), mmap_mode="r") for k in ARRAYS}
+    _S.update(data, model=model, descriptor=descriptor, oracle=oracle)
 
 
 def ping(_):

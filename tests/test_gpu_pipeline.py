@@ -140,8 +140,49 @@ def test_overlapped_slabs_equal_align_slab(dev, depth, corun, grid, beside, firs
     beside warp(k-1)); first: at depth 3 RANSAC(k-1) queued before
     the host waits for RANSAC(k-2)) gives the same affines and warped frames as the
     sequential align_slab."""
-    F, H, W = 24, 270, 480
     cfg = pipeline.AlignConfig(n_kp_global=60)
+    slabs = _gap_slabs(dev)
+    ref = [pipeline.align_slab(s, cfg) for s in slabs]
+    ov = pipeline.OverlappedSlabs(dev, cfg, depth=depth, corun=corun, ransac_grid=grid, match_beside=beside,
+                                  fit_first=first)
+    _check_overlapped(ov, slabs, ref, depth)
+
+
+@pytest.mark.parametrize("cus,exclusive,beside", [(1, True, True), (2, False, True), (3, True, False)])
+def test_overlapped_slabs_cu_split(dev, cus, exclusive, beside):
+    """The analysis stream on a fixed CU slice (the first `cus` CUs of every shader engine;
+    the warp on the others, or on every CU) gives the same results as align_slab."""
+    cfg = pipeline.AlignConfig(n_kp_global=60)
+    slabs = _gap_slabs(dev)
+    ref = [pipeline.align_slab(s, cfg) for s in slabs]
+    ov = pipeline.OverlappedSlabs(dev, cfg, match_beside=beside, ana_cus_per_se=cus, warp_exclusive=exclusive)
+    _check_overlapped(ov, slabs, ref, 2)
+
+
+def test_cu_split_stream_arguments(dev):
+    from kcmc_amd import _lib
+    for bad in (0, 8, -1):
+        with pytest.raises(ValueError):
+            stages.cu_split_stream(dev, bad)
+    assert stages.cu_split_stream(dev, 2) is stages.cu_split_stream(dev, 2)
+    assert _lib.load().kcmc_stream_destroy(None) == 0
+
+
+def _check_overlapped(ov, slabs, ref, depth):
+    got = [ov.submit(s) for s in slabs]
+    assert all(g is None for g in got[:depth - 1])
+    got = got[depth - 1:] + ov.flush()
+    assert ov.flush() == []
+    ov.synchronize()
+    assert [len(r.skipped) for r in ref] == [3, 4, 0]
+    for r, g in zip(ref, got):
+        assert np.array_equal(r.affines, g.affines, equal_nan=True)
+        assert r.skipped == g.skipped and r.interpolated == g.interpolated
+        assert torch.equal(r.aligned, g.aligned)
+
+
+def _gap_slabs(dev):
+    F, H, W = 24, 270, 480
     slabs = []
     for seed in (11, 12, 13):
         ks = synthetic.make_keypoints(F, 300, 32, (H, W), seed=seed)
@@ -158,19 +199,65 @@ def test_overlapped_slabs_equal_align_slab(dev, depth, corun, grid, beside, firs
                                          torch.from_numpy(ks.kp_tpl).to(dev), torch.from_numpy(ks.des_q).to(dev),
                                          torch.from_numpy(ks.kp_q).to(dev), torch.from_numpy(ks.q_off).to(dev),
                                          ks.q_off))
-    ref = [pipeline.align_slab(s, cfg) for s in slabs]
-    ov = pipeline.OverlappedSlabs(dev, cfg, depth=depth, corun=corun, ransac_grid=grid, match_beside=beside,
-                                  fit_first=first)
-    got = [ov.submit(s) for s in slabs]
-    assert all(g is None for g in got[:depth - 1])
-    got = got[depth - 1:] + ov.flush()
-    assert ov.flush() == []
-    ov.synchronize()
-    assert [len(r.skipped) for r in ref] == [3, 4, 0]
-    for r, g in zip(ref, got):
-        assert np.array_equal(r.affines, g.affines, equal_nan=True)
-        assert r.skipped == g.skipped and r.interpolated == g.interpolated
-        assert torch.equal(r.aligned, g.aligned)
+    return slabs
+
+
+def test_device_lists_follow_the_seed_after_host_list_ransac(dev, caplog):
+    """The device-list RANSAC (align_slab, OverlappedSlabs) re-installs its own seed's
+    hypothesis tables when another call on the same context has replaced them (a host-list
+    ransac_rigid with another RANDOM_SEED); OverlappedSlabs writes VA:279-283's low-count
+    log lines from the point counts it copied with the parameters."""
+    F, H, W = 16, 270, 480
+    ks = synthetic.make_keypoints(F, 300, 32, (H, W), seed=21)
+    for f in (2, 3):  # two frames without a model: low-count log lines
+        a, b = ks.q_off[f], ks.q_off[f + 1]
+        ks.des_q[a:b] = ks.des_q[a]
+    base = synthetic.make_texture((H, W), seed=21)
+    frames = torch.from_numpy(np.broadcast_to(base, (F, H, W)).copy()).to(dev)
+    inp = pipeline.SlabInputs(frames, torch.from_numpy(ks.des_tpl).to(dev), torch.from_numpy(ks.kp_tpl).to(dev),
+                              torch.from_numpy(ks.des_q).to(dev), torch.from_numpy(ks.kp_q).to(dev),
+                              torch.from_numpy(ks.q_off).to(dev), ks.q_off)
+    cfg42, cfg7 = pipeline.AlignConfig(n_kp_global=60), pipeline.AlignConfig(n_kp_global=60, seed=7)
+    a42 = pipeline.align_slab(inp, cfg42, keep_intermediates=True)
+    # a host-list RANSAC with seed 7 on the same device replaces the context's tables
+    po, pi = a42.consensus.pt_off, a42.consensus.pt_idx
+    kq = a42.match.kp_ordered.cpu().numpy()
+    r7 = stages.ransac_rigid(a42.match.kp_ordered.view(-1, 2), inp.kp_tpl, torch.from_numpy(po).to(dev), po,
+                             pt_idx=torch.from_numpy(pi if pi.size else np.zeros(1, np.int32)).to(dev),
+                             src_frame_stride=300, seed=7)
+    p7 = r7.params.cpu().numpy()
+    b42 = pipeline.align_slab(inp, cfg42)
+    assert np.array_equal(a42.affines, b42.affines, equal_nan=True)
+    assert torch.equal(a42.aligned, b42.aligned)
+    # and the device lists with seed 7 give the host-list seed-7 result and the oracle's
+    a7 = pipeline.align_slab(inp, cfg7)
+    ok = ~np.isnan(p7).any(axis=(1, 2))
+    assert np.array_equal(a7.affines[ok], p7[ok])
+    for f in np.flatnonzero(ok)[::5]:
+        L = pi[po[f]:po[f + 1]]
+        p, _, _, _ = oracle.ransac_rigid(kq[f][L], ks.kp_tpl[L], seed=7)
+        np.testing.assert_allclose(a7.affines[f], p, rtol=1e-9, atol=1e-9)
+    logger = logging.getLogger("test_seed_lists")
+    with caplog.at_level(logging.INFO, logger="test_seed_lists"):
+        ov = pipeline.OverlappedSlabs(dev, cfg42, logger=logger, match_beside=True)
+        got = [r for r in (ov.submit(inp), ov.submit(inp)) if r is not None] + ov.flush()
+        ov.synchronize()
+    low = [r.getMessage() for r in caplog.records if "low keypoint count" in r.getMessage()]
+    n_low = int((np.diff(po) < cfg42.n_kp_frame_skip).sum())
+    assert len(got) == 2 and n_low >= 2 and len(low) == 2 * n_low
+    for g in got:
+        assert np.array_equal(g.affines, a42.affines, equal_nan=True)
+
+
+def test_euclidean_min_samples_other_than_two_raises(dev):
+    F, H, W = 4, 96, 128
+    ks = synthetic.make_keypoints(F, 64, 32, (H, W), seed=1)
+    frames = torch.zeros((F, H, W), dtype=torch.uint16, device=dev)
+    inp = pipeline.SlabInputs(frames, torch.from_numpy(ks.des_tpl).to(dev), torch.from_numpy(ks.kp_tpl).to(dev),
+                              torch.from_numpy(ks.des_q).to(dev), torch.from_numpy(ks.kp_q).to(dev),
+                              torch.from_numpy(ks.q_off).to(dev), ks.q_off)
+    with pytest.raises(ValueError, match="min_samples=2"):
+        pipeline.align_slab(inp, pipeline.AlignConfig(n_kp_global=30, ransac_min_samples=3))
 
 
 @pytest.mark.parametrize("model,rate,depth,corun", [("euclidean", 2, 2, True), ("euclidean", 2, 3, False),

@@ -1,0 +1,56 @@
+#!/bin/bash
+# One parametrised GPU-box batch (replaces the round-3 one-shot batch_r03*.sh scripts).
+# From the repo root on the GPU box:
+#   bash tools/gpu_batch.sh <out_dir> <step> [<step> ...]
+# Steps (run in order; the batch stops at the first failing step):
+#   probe                 host CPU facts (cpu_count, affinity, cgroup quota) -> <out>/probe.txt
+#   tests[:<-k expr>]     pytest -m gpu (optionally -k) -> <out>/tests.log
+#   smoke                 __graft_entry__.smoke() -> <out>/smoke.log
+#   bench:<cfg>[:<tag>][:<args,comma,separated>]
+#                         bench.py --config <cfg> --cpu-sample 0 [args] -> <out>/<cfg>_<tag>.json
+#   cpubench:<cfg>        bench.py --config <cfg> with its CPU baseline -> <out>/<cfg>_cpu.json
+#   profile:<cfg>         tools/profile_round.sh (bench + rocprofv3 summary + warp PMC) -> <out>/<cfg>/
+#   lab:<binary>[:<tag>]  a lab binary (tools/ or ab/) -> <out>/lab_<tag>.txt
+set -u
+OUT=${1:?out dir}
+shift
+mkdir -p "$OUT"
+for step in "$@"; do
+  IFS=: read -r kind a b c <<< "$step"
+  case "$kind" in
+    probe)
+      { python -c "import os; print('cpu_count', os.cpu_count()); print('affinity', len(os.sched_getaffinity(0)))"
+        cat /sys/fs/cgroup/cpu.max 2>/dev/null || echo "no cgroup v2 cpu.max"
+        nproc; free -g | head -2; } > "$OUT/probe.txt" 2>&1
+      cat "$OUT/probe.txt" ;;
+    tests)
+      K=()
+      [ -n "${a:-}" ] && K=(-k "$a")
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread "${K[@]}" \
+        > "$OUT/tests.log" 2>&1
+      rc=$?
+      echo "tests rc=$rc" >> "$OUT/tests.log"; tail -3 "$OUT/tests.log"
+      [ $rc -eq 0 ] || exit 1 ;;
+    smoke)
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit 1
+      tail -1 "$OUT/smoke.log" ;;
+    bench)
+      tag=${b:-1}
+      IFS=, read -r -a X <<< "${c:-}"
+      timeout -k 10 300 python bench.py --config "$a" --cpu-sample 0 "${X[@]}" > "$OUT/${a}_$tag.json" \
+        2>> "$OUT/bench.err" || exit 1
+      echo "$a $tag: $(head -c 160 "$OUT/${a}_$tag.json")" ;;
+    cpubench)
+      timeout -k 10 400 python bench.py --config "$a" > "$OUT/${a}_cpu.json" 2>> "$OUT/bench.err" || exit 1
+      echo "$a cpu: $(head -c 160 "$OUT/${a}_cpu.json")" ;;
+    profile)
+      bash tools/profile_round.sh "$OUT/$a" --config "$a" || exit 1 ;;
+    lab)
+      tag=${b:-$(basename "$a")}
+      timeout -k 10 240 "$a" > "$OUT/lab_$tag.txt" 2>&1 || exit 1
+      tail -4 "$OUT/lab_$tag.txt" ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo done
