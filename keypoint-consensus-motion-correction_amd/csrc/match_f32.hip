@@ -128,37 +128,37 @@ __device__ __forceinline__ void topk_key(uint32_t (&k)[kTop], uint32_t x) {
   k[0] = min(k[0], x);
 }
 
-// One distance of the tile loop: if its value bits are below ithr (some lane of the wave
-// takes the branch), key = (bits & kmask) | id enters the sorted top-6 in place and ithr
-// follows the new last key.  Hand-written because the backend gave the updated list fresh
-// registers on every insertion and copied it back (6-10 v_mov per insertion, ~15 VALU
-// instead of 9); same operations as topk_key.  kmask, id, nkmask are wave-uniform (SGPRs).
-// AFTER_MFMA: xb was written by the MFMA just issued; hipcc pads nothing inside an asm
+// One distance of the tile loop: if its value bits x are below the list's last key k5
+// (some lane of the wave takes the branch), key = (x & kmask) | id enters the sorted top-6
+// in place (v_and_or_b32 + 5 v_med3_u32 + v_min_u32: 7 VALU).  Comparing the raw bits with
+// k5 keeps the bound the certification needs: a rejected x >= k5 truncates to >= the last
+// listed value, and so does every key the list pushes out.  Hand-written because the
+// backend gave the updated list fresh registers on every insertion and copied it back
+// (6-10 v_mov per insertion); id is wave-uniform (an SGPR), kmask a VGPR (a VOP3 reads
+// one SGPR at most).
+// AFTER_MFMA: x was written by the MFMA just issued; hipcc pads nothing inside an asm
 // string, so the string opens with the 12 wait states an 8-pass XDL result needs before a
 // VALU reads it (the later values of the tile are read more than 12 states later).
 #define KCMC_TOPK_TRY6_BODY                            \
-  "v_cmp_lt_u32 vcc, %[x], %[thr]\n\t"                 \
+  "v_cmp_lt_u32 vcc, %[x], %[k5]\n\t"                  \
   "s_and_saveexec_b64 %[sv], vcc\n\t"                  \
   "s_cbranch_execz 1f\n\t"                             \
-  "v_and_b32 %[x], %[km], %[x]\n\t"                    \
-  "v_or_b32 %[x], %[id], %[x]\n\t"                     \
+  "v_and_or_b32 %[x], %[x], %[km], %[id]\n\t"          \
   "v_med3_u32 %[k5], %[k4], %[k5], %[x]\n\t"           \
   "v_med3_u32 %[k4], %[k3], %[k4], %[x]\n\t"           \
   "v_med3_u32 %[k3], %[k2], %[k3], %[x]\n\t"           \
   "v_med3_u32 %[k2], %[k1], %[k2], %[x]\n\t"           \
   "v_med3_u32 %[k1], %[k0], %[k1], %[x]\n\t"           \
-  "v_min_u32 %[k0], %[k0], %[x]\n\t"                   \
-  "v_or_b32 %[thr], %[nm], %[k5]\n"                     \
+  "v_min_u32 %[k0], %[k0], %[x]\n"                      \
   "1:\n\t"                                             \
   "s_or_b64 exec, exec, %[sv]"
 #define KCMC_TOPK_TRY6_OPERANDS                                                                                 \
   : [k0] "+v"(k[0]), [k1] "+v"(k[1]), [k2] "+v"(k[2]), [k3] "+v"(k[3]), [k4] "+v"(k[4]), [k5] "+v"(k[5]),      \
-    [thr] "+v"(ithr), [x] "+v"(xb), [sv] "=&s"(saved)                                                         \
-  : [km] "s"(kmask), [id] "s"(id), [nm] "s"(nkmask)                                                           \
+    [x] "+v"(xb), [sv] "=&s"(saved)                                                                           \
+  : [km] "v"(kmask), [id] "s"(id)                                                                             \
   : "vcc"
 template <bool AFTER_MFMA>
-__device__ __forceinline__ void topk_try6(uint32_t (&k)[kTop], uint32_t& ithr, uint32_t xb, uint32_t kmask,
-                                          uint32_t id, uint32_t nkmask) {
+__device__ __forceinline__ void topk_try6(uint32_t (&k)[kTop], uint32_t xb, uint32_t kmask, uint32_t id) {
   static_assert(kTop == 6, "topk_try6 keeps a top-6");
   uint64_t saved;
   if constexpr (AFTER_MFMA)
@@ -460,7 +460,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 6))
   uint32_t ck[kTop];
 #pragma unroll
   for (int k = 0; k < kTop; ++k) ck[k] = 0xffffffffu;
-  uint32_t ithr = 0xffffffffu;
   int cur = 0;  // t % kNBuf
   for (int t = 0; t < n_tiles; ++t) {
     // tile t has landed (this wave's pieces: vmcnt; the others': the barrier) and every
@@ -491,15 +490,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 6))
       for (int st = 0; st < kKSteps; ++st)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*reinterpret_cast<const f16x8*>(ap + 16 * st), btpl[st], acc, 0,
                                                      0, 0);
-      // a value whose bits are >= ithr = (last key | low bits) cannot enter the list: its
-      // key would be >= the last key's truncated value, which already bounds every unlisted
-      // row.  After the first few hundred rows most distances of a wave skip the insertion
-      // (the branch is per wave): 1 + 9 P VALU per distance, P = the share of the wave's
-      // values some lane inserts (~0.3 on the c5 data, simulated)
-      topk_try6<true>(ck, ithr, __float_as_uint(acc[0]), kmask, (uint32_t)(hh * 16) | tbase, ~kmask);
+      // a value whose bits are >= the last key cannot enter the list (its truncation is >=
+      // the last listed value, which already bounds every unlisted row).  After the first
+      // few hundred rows most distances of a wave skip the insertion (the branch is per
+      // wave): 1 + 7 P VALU per distance, P = the share of the wave's values some lane
+      // inserts (0.31 on the c5 data, simulated; 0.34 from the round-3 PMC's INT32 count)
+      topk_try6<true>(ck, __float_as_uint(acc[0]), kmask, (uint32_t)(hh * 16) | tbase);
 #pragma unroll
       for (int r = 1; r < 16; ++r)
-        topk_try6<false>(ck, ithr, __float_as_uint(acc[r]), kmask, (uint32_t)(hh * 16 + r) | tbase, ~kmask);
+        topk_try6<false>(ck, __float_as_uint(acc[r]), kmask, (uint32_t)(hh * 16 + r) | tbase);
     }
   }
 
@@ -528,8 +527,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 6))
       // the partner's last value bounds every row it did not report
       best.v[kTop - 1] = fminf(best.v[kTop - 1], ov[kTop - 1]);
     }
+    // the merged list to both halves: they share the exact re-rank below
+#pragma unroll
+    for (int k = 0; k < kTop; ++k) best.v[k] = __shfl(best.v[k], c, 64);
+#pragma unroll
+    for (int k = 0; k < kTop - 1; ++k) best.j[k] = __shfl(best.j[k], c, 64);
   }
-  if (h != 0 || i >= n_tpl) return;
+  if (i >= n_tpl) return;
 
   // ---- certify and re-rank with the exact distance.  In scaled units (sc = s_T s_f):
   // v~_j is in [sc v_j, sc (v_j + 2B)] with B = max_j beta_j (fbeta), and a listed
@@ -559,6 +563,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 6))
   }
   const size_t o = ((size_t)f * n_tpl + i) * 2;
   if (ncand < 0) {  // frame f's list (room for every template row)
+    if (h != 0) return;
     const int slot = atomicAdd(&fb_cnt[f], 1);
     fallback[(size_t)f * n_tpl + slot] = i;
     fb_keys[2 * ((size_t)f * n_tpl + slot)] = ~0ull;  // the merge keys of the entry start empty
@@ -566,16 +571,27 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 6))
     if (slot == 0) fb_frames[1 + atomicAdd(&fb_frames[0], 1)] = f;  // the frame's first entry lists it
     return;
   }
+  // the candidates' exact distances, shared by the two lanes of the row: lane half h takes
+  // candidates 2m + h (one pass for the usual two candidates instead of two)
   float d0 = FLT_MAX, d1 = FLT_MAX;
   int j0 = -1, j1 = -1;
   const float* a = des_tpl + (size_t)i * D;
   const float* fb = des_q + (size_t)q_begin * D;
 #pragma unroll
-  for (int k = 0; k < kTop - 1; ++k) {
-    const int j = best.j[k];
+  for (int m = 0; 2 * m < kTop - 1; ++m) {
+    const int k = 2 * m + h;
+    int j = best.j[2 * m];
+    if (2 * m + 1 < kTop - 1 && h) j = best.j[2 * m + 1];
     if (k < ncand && (unsigned)j < (unsigned)n_q)  // (always in range; the guard keeps reads inside the frame)
       top2_insert_exact(d0, j0, d1, j1, exact_dist_any(a, fb + (size_t)j * D, D), j);
   }
+  {
+    const float e0 = __shfl_xor(d0, 32), e1 = __shfl_xor(d1, 32);
+    const int k0 = __shfl_xor(j0, 32), k1 = __shfl_xor(j1, 32);
+    if (k0 >= 0) top2_insert_exact(d0, j0, d1, j1, e0, k0);
+    if (k1 >= 0) top2_insert_exact(d0, j0, d1, j1, e1, k1);
+  }
+  if (h != 0) return;
   out_idx[o] = j0;
   out_idx[o + 1] = j1;
   out_dist[o] = d0;
