@@ -448,6 +448,186 @@ __device__ __forceinline__ void fast_rows(const uint16_t* stile, const int2* __r
   }
 }
 
+// Fast staged path for C = 3 / 4 (mode 3 of a multi-channel frame, round 4).  The
+// interleaved box is de-interleaved while it lands: each thread loads one 8-pixel group of
+// a box row (C 16-byte chunks, 16-byte aligned because ax0 and W are multiples of 8) and
+// writes C planar 16-byte pieces (v_perm_b32 pairs), one per channel plane, at the fixed
+// pitch.  A pixel's taps then sit at the same offset in every plane (immediate offsets), so
+// the coordinate work of a pixel is shared by its C channels, and each lane's C output
+// dwords (pixels 2l, 2l+1) leave in ONE 12- / 16-byte store: a wave's store covers 768 /
+// 1024 contiguous bytes of the row.  The general multi-channel path (mode 0) reads
+// interleaved taps with per-channel addressing and stores C separate dwords per lane at a
+// 12-byte lane stride (round 3: 148 VALU, 49 SALU, 25 LDS instructions per wave row at c4).
+#ifndef KCMC_FASTC_PITCH
+#define KCMC_FASTC_PITCH 144
+#endif
+template <class Cfg, int C>
+struct FastC {
+  static constexpr int kPitch = KCMC_FASTC_PITCH;                        // plane row pitch (pixels)
+  static constexpr int kRows = (Cfg::kLdsElems - 8) / (C * kPitch);      // the last 16 bytes: flags
+  static constexpr int kPlane = kRows * kPitch;                          // elements per channel plane
+  static constexpr int kFlagWord = Cfg::kLdsElems / 2 - 4;
+  static constexpr int kGroups = kPitch / 8;                             // 8-pixel groups per staged row
+  static constexpr int kPasses = (kRows * kGroups + kThreads - 1) / kThreads;
+  static_assert(C * kPlane <= 2 * kFlagWord, "planes overlap the flag words");
+};
+
+template <class Cfg, int C>
+__device__ __forceinline__ void fastc_stage_issue(const uint16_t* __restrict__ S, int ax0, int sy0, int gpr, int rows,
+                                                  int H, int W, int tid,
+                                                  uint4 (&g)[FastC<Cfg, C>::kPasses][C]) {
+#pragma unroll
+  for (int k = 0; k < FastC<Cfg, C>::kPasses; ++k) {
+    const int q = tid + kThreads * k;
+    const int r = q / FastC<Cfg, C>::kGroups, c = q - r * FastC<Cfg, C>::kGroups;
+    const int gy = sy0 + r, gx = ax0 + 8 * c;
+    const bool ok = r < rows && c < gpr && (unsigned)gx < (unsigned)W && (unsigned)gy < (unsigned)H;
+#pragma unroll
+    for (int j = 0; j < C; ++j) g[k][j] = make_uint4(0u, 0u, 0u, 0u);
+    if (ok) {
+      const uint4* src = reinterpret_cast<const uint4*>(S + ((size_t)gy * W + gx) * C);
+#pragma unroll
+      for (int j = 0; j < C; ++j) g[k][j] = src[j];
+    }
+  }
+}
+
+// word i of plane k of an 8-pixel group: elements C (2i) + k and C (2i + 1) + k of the
+// interleaved group (dwords d[e / 2], halves e % 2), as one v_perm_b32
+template <int C, int K, int I>
+__device__ __forceinline__ uint32_t plane_word(const uint32_t (&d)[4 * C]) {
+  constexpr int e0 = C * 2 * I + K, e1 = C * (2 * I + 1) + K;
+  constexpr uint32_t sel = ((e0 & 1) ? 0x0302u : 0x0100u) | ((e1 & 1) ? 0x07060000u : 0x05040000u);
+  return __builtin_amdgcn_perm(d[e1 / 2], d[e0 / 2], sel);
+}
+
+template <int C, int K>
+__device__ __forceinline__ uint4 plane_piece(const uint32_t (&d)[4 * C]) {
+  return make_uint4(plane_word<C, K, 0>(d), plane_word<C, K, 1>(d), plane_word<C, K, 2>(d), plane_word<C, K, 3>(d));
+}
+
+template <class Cfg, int C>
+__device__ __forceinline__ uint32_t fastc_stage_land(uint16_t* stile, int gpr, int rows, int tid,
+                                                     const uint4 (&g)[FastC<Cfg, C>::kPasses][C]) {
+  uint32_t nb = 0;  // bright (>= 16384) groups of this wave
+#pragma unroll
+  for (int k = 0; k < FastC<Cfg, C>::kPasses; ++k) {
+    const int q = tid + kThreads * k;
+    const int r = q / FastC<Cfg, C>::kGroups, c = q - r * FastC<Cfg, C>::kGroups;
+    uint32_t d[4 * C], any = 0;  // the group's 8 C elements, two per dword
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      d[4 * j] = g[k][j].x;
+      d[4 * j + 1] = g[k][j].y;
+      d[4 * j + 2] = g[k][j].z;
+      d[4 * j + 3] = g[k][j].w;
+      any |= g[k][j].x | g[k][j].y | g[k][j].z | g[k][j].w;
+    }
+    nb += __builtin_popcountll(__builtin_amdgcn_ballot_w64((any & 0xc000c000u) != 0));
+    if (r < rows && c < gpr) {
+      uint4* dst = reinterpret_cast<uint4*>(stile + r * FastC<Cfg, C>::kPitch + 8 * c);
+      dst[0] = plane_piece<C, 0>(d);
+      dst[FastC<Cfg, C>::kPlane / 8] = plane_piece<C, 1>(d);
+      dst[2 * FastC<Cfg, C>::kPlane / 8] = plane_piece<C, 2>(d);
+      if constexpr (C == 4) dst[3 * FastC<Cfg, C>::kPlane / 8] = plane_piece<C, 3>(d);
+    }
+  }
+  return nb;
+}
+
+// Output rows of a multi-channel mode-3 tile: fast_rows with C planes (same coordinate
+// scheme, same three blends, the blend decided once per tile or per row over every
+// channel's taps) and one b96 / b128 buffer store per lane and row.
+template <class Cfg, int C, int BLEND, bool INTERIOR>
+__device__ __forceinline__ void fastc_rows(const uint16_t* stile, const int2* __restrict__ rt, int ox, int oy,
+                                           uint16_t* __restrict__ Dst, int H, int W, int xb, int yb, int wave,
+                                           int lane, const int (&ad)[2], const int (&bd)[2]) {
+  static_assert(C == 3 || C == 4, "planar fast path: RGB / RGBA");
+  constexpr int kPlane = FastC<Cfg, C>::kPlane, kPitch = FastC<Cfg, C>::kPitch;
+  const uint32_t xoff = 2u * C * (uint32_t)(xb + 2 * lane);  // byte offset of the lane's pixel pair
+  const bool store_ok = INTERIOR || xb + 2 * lane + 2 <= W;   // W is a multiple of 8 here
+  const __amdgpu_buffer_rsrc_t dst_rsrc = __builtin_amdgcn_make_buffer_rsrc(Dst, 0, 2 * C * H * W, 0x00020000);
+  int2 org[Cfg::kTileH / 4];
+#pragma unroll
+  for (int i = 0; i < Cfg::kTileH / 4; ++i) org[i] = rt[i];
+  uint32_t ad6[2], bd6[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    ad6[p] = (uint32_t)ad[p] << 6;
+    bd6[p] = (uint32_t)bd[p] << 6;
+  }
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 pitch2 = {(unsigned short)2, (unsigned short)(2 * kPitch)};
+  const char* sbytes = reinterpret_cast<const char*>(stile);
+#pragma unroll
+  for (int i = 0; i < Cfg::kTileH / 4; ++i) {
+    const int y = yb + wave + 4 * i;  // wave-uniform
+    if (!INTERIOR && y >= H) break;
+    const uint32_t X0 = (uint32_t)(org[i].x - ox) << 6, Y0 = (uint32_t)(org[i].y - oy) << 6;  // scalar
+    uint32_t v[C][2][4], fx[2], fy[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const uint32_t tX = X0 + ad6[p], tY = Y0 + bd6[p];
+      fx[p] = bfe_11_5(tX);
+      fy[p] = bfe_11_5(tY);
+      const uint32_t cr = __builtin_amdgcn_perm(tY, tX, 0x07060302u);  // (column, row) as u16 x 2
+      const uint32_t off = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, cr), pitch2, 0u, false);
+      const uint16_t* t = reinterpret_cast<const uint16_t*>(sbytes + off);
+#pragma unroll
+      for (int k = 0; k < C; ++k) {
+        v[k][p][0] = t[k * kPlane];
+        v[k][p][1] = t[k * kPlane + 1];
+        v[k][p][2] = t[k * kPlane + kPitch];
+        v[k][p][3] = t[k * kPlane + kPitch + 1];
+      }
+    }
+    bool use_float = BLEND == kBright;
+    if constexpr (BLEND == kMixed) {
+      uint32_t taps = 0;
+#pragma unroll
+      for (int k = 0; k < C; ++k)
+        taps |= (v[k][0][0] | v[k][0][1] | v[k][0][2]) | (v[k][0][3] | v[k][1][0] | v[k][1][1]) |
+                (v[k][1][2] | v[k][1][3]);
+      use_float = __builtin_amdgcn_ballot_w64((taps & 0xc000u) != 0) != 0;  // wave-uniform
+    }
+    f32x2 q[C];
+    if (use_float) {
+#pragma unroll
+      for (int k = 0; k < C; ++k) q[k] = blend_float2(v[k], fx, fy);
+    } else {
+#pragma unroll
+      for (int k = 0; k < C; ++k) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const uint32_t ax = 32 - fx[p], ay = 32 - fy[p];
+          uint32_t h0 = __umul24(v[k][p][0], ax) + __umul24(v[k][p][1], fx[p]);
+          uint32_t h1 = __umul24(v[k][p][2], ax) + __umul24(v[k][p][3], fx[p]);
+          asm volatile("" : "+v"(h0), "+v"(h1));  // keep the separable form (see output_rows)
+          q[k][p] = (float)(__umul24(h0, ay) + __umul24(h1, fy[p]));
+        }
+        q[k] += 0x1.8p33f;  // rint(S / 1024) in the low bits (fast_rows)
+      }
+    }
+    // the lane's 2 C channel values in interleaved order, two per dword
+#define KCMC_Q(px, ch) __float_as_uint(q[ch][px])
+    if constexpr (C == 3) {
+      typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+      const u32x3 o = {__builtin_amdgcn_perm(KCMC_Q(0, 1), KCMC_Q(0, 0), 0x05040100u),
+                       __builtin_amdgcn_perm(KCMC_Q(1, 0), KCMC_Q(0, 2), 0x05040100u),
+                       __builtin_amdgcn_perm(KCMC_Q(1, 2), KCMC_Q(1, 1), 0x05040100u)};
+      if (store_ok) __builtin_amdgcn_raw_buffer_store_b96(o, dst_rsrc, xoff, 2 * C * y * W, 2);
+    } else {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 o = {__builtin_amdgcn_perm(KCMC_Q(0, 1), KCMC_Q(0, 0), 0x05040100u),
+                       __builtin_amdgcn_perm(KCMC_Q(0, 3), KCMC_Q(0, 2), 0x05040100u),
+                       __builtin_amdgcn_perm(KCMC_Q(1, 1), KCMC_Q(1, 0), 0x05040100u),
+                       __builtin_amdgcn_perm(KCMC_Q(1, 3), KCMC_Q(1, 2), 0x05040100u)};
+      if (store_ok) __builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, xoff, 2 * C * y * W, 2);
+    }
+#undef KCMC_Q
+  }
+}
+
 // Per-tile plan made by warp_plan_kernel.
 struct TilePlan {
   int mode, ax0, sy0;
@@ -621,7 +801,11 @@ __global__ __launch_bounds__(256) void warp_plan_kernel(const double* __restrict
   if (t2 == 0)
     for (int k = 0; k < 6; ++k) minv[6 * (size_t)f + k] = M[k];
   Box b = source_box<Cfg, C>(M, xb, yb, H, W);
-  if (C == 1 && (W & 7) == 0 && b.mode == 0 && b.pitch <= kFastPitch && b.rows <= Fast<Cfg>::kRows) b.mode = 3;
+  if constexpr (C == 1) {
+    if ((W & 7) == 0 && b.mode == 0 && b.pitch <= kFastPitch && b.rows <= Fast<Cfg>::kRows) b.mode = 3;
+  } else if constexpr (C == 3 || C == 4) {
+    if ((W & 7) == 0 && b.mode == 0 && b.pitch <= FastC<Cfg, C>::kPitch && b.rows <= FastC<Cfg, C>::kRows) b.mode = 3;
+  }
   if (map_has_nan(M, 6)) b.mode = 1;  // a NaN map (a frame RANSAC could not fit) warps to zeros
   plan[t] = TilePlan{b.mode, b.ax0, b.sy0, b.pitch | (b.rows << 16)};
   for (int j = tx; j < Cfg::kTileH && yb + j < H; j += ntx) {
@@ -687,6 +871,38 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
           fast_rows<Cfg, kMixed, false>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
       } else {
         fast_rows<Cfg, kBright, false>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+      }
+      return;
+    }
+  }
+  if constexpr ((C == 3 || C == 4) && VARIANT == 0) {
+    if (box.mode == 3) {
+      const int gpr = box.pitch >> 3;
+      uint4 g[FastC<Cfg, C>::kPasses][C];
+      fastc_stage_issue<Cfg, C>(S, box.ax0, box.sy0, gpr, box.rows, H, W, tid, g);  // loads first
+      int ad[2], bd[2];
+      lane_cols(minv + 6 * (size_t)f, xb, W, lane, ad, bd);
+      const uint32_t nb = fastc_stage_land<Cfg, C>(stile, gpr, box.rows, tid, g);
+      uint32_t* flags = reinterpret_cast<uint32_t*>(stile) + FastC<Cfg, C>::kFlagWord;
+      if (lane == 0) flags[wave] = nb;
+      __syncthreads();
+      const uint4 fl = *reinterpret_cast<const uint4*>(flags);
+      const uint32_t bright = fl.x + fl.y + fl.z + fl.w;
+      const int2* rt = rowtab + ((size_t)f * 4 + wave) * hq + (yb >> 2);
+      const int ox = box.ax0 * 1024, oy = box.sy0 * 1024;
+      const bool interior = yb + Cfg::kTileH <= H && xb + kTileW <= W;
+      if (bright == 0) {
+        if (interior)
+          fastc_rows<Cfg, C, kDark, true>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+        else
+          fastc_rows<Cfg, C, kDark, false>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+      } else if ((int)bright * kBrightShare <= box.rows * (box.pitch >> 3)) {
+        if (interior)
+          fastc_rows<Cfg, C, kMixed, true>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+        else
+          fastc_rows<Cfg, C, kMixed, false>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
+      } else {
+        fastc_rows<Cfg, C, kBright, false>(stile, rt, ox, oy, Dst, H, W, xb, yb, wave, lane, ad, bd);
       }
       return;
     }
@@ -773,6 +989,20 @@ __device__ __forceinline__ void invert_perspective(const double* S, double* M) {
   M[8] = (S[0] * S[4] - S[1] * S[3]) * d;
 }
 
+// Per-tile row table of the perspective warp (round 4): WarpPerspectiveInvoker's per-(row,
+// block) values X0 = M0 xo + M1 y + M2, Y0 = M3 xo + M4 y + M5, W0 = M6 xo + M7 y + M8 for
+// the tile's kTileH rows and its two 64-column blocks (bw0 = 64 for every frame with
+// H >= 16 and W >= 64), computed once per workgroup into the last bytes of the LDS budget
+// instead of by every lane for every row (9 of a row's 39 fp64 operations per lane); the
+// staged box gets the budget minus the table.
+template <class Cfg>
+struct PerspTab {
+  static constexpr int kEntries = Cfg::kTileH * 2;                  // (row, block)
+  static constexpr int kElems = kEntries * 3 * 4;                   // u16 elements of 3 doubles each
+  static constexpr int kBoxElems = Cfg::kLdsElems - kElems;         // the staged box's budget
+  static_assert((kBoxElems * 2) % 8 == 0, "table alignment");
+};
+
 // Source box of a tile: when the projective denominator has one sign over the tile,
 // the tile's image is the convex hull of its corner images; one pixel of margin on each
 // side absorbs the 1/32-px rounding and the second tap.  Otherwise: direct gather.
@@ -809,7 +1039,7 @@ __device__ __forceinline__ Box persp_box(const double* M, int xb, int yb, int H,
   const long long rows = sy1 - sy0 + 1;
   if (sx1 < 0 || sx0 > W - 1 || sy1 < 0 || sy0 > H - 1)
     b.mode = 1;
-  else if (wrange && pitch <= kMaxPitch && rows <= 8 * Cfg::kRowPasses && pitch * rows * C <= Cfg::kLdsElems)
+  else if (wrange && pitch <= kMaxPitch && rows <= 8 * Cfg::kRowPasses && pitch * rows * C <= PerspTab<Cfg>::kBoxElems)
     b.mode = 0;
   b.ax0 = (int)ax0;
   b.sy0 = (int)sy0;
@@ -902,19 +1132,20 @@ __device__ __forceinline__ void persp_px(double X0, double Y0, double W0, double
   Y = (int)__builtin_rint(fY);
 }
 
-template <class Cfg, int C, int MODE>
+template <class Cfg, int C, int MODE, bool TAB>
 __device__ __forceinline__ void persp_rows(const uint16_t* stile, const Box& box, const uint16_t* __restrict__ S,
                                            uint16_t* __restrict__ Dst, const double* M, int H, int W, int xb, int yb,
-                                           int wave, int lane, int bw0) {
+                                           int wave, int lane, int bw0, const double* ptab) {
   const int x = xb + 2 * lane;
   const bool pair_store = C == 1 && (W & 1) == 0 && x + 2 <= W;
-  int xo[2], x1[2];
+  int xo[2], x1[2], tb[2];
   double m0x1[2], m3x1[2], m6x1[2], dxo[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int xc = min(x + q, W - 1);  // columns past the edge reuse the last column's taps
     xo[q] = xc - xc % bw0;
     x1[q] = xc - xo[q];
+    tb[q] = (xo[q] - xb) >> 6;  // TAB (bw0 == 64): the pixel's block of the tile (0 or 1)
     // row-invariant: the column products and the block origin (round 3: hoisted out of
     // the row loop, and X0 / Y0 / W0 evaluated once per row for the lane's pixel pair)
     m0x1[q] = M[0] * x1[q];
@@ -931,16 +1162,26 @@ __device__ __forceinline__ void persp_rows(const uint16_t* stile, const Box& box
     uint16_t o[2 * C];
     const double dy = (double)y;
     double X0[2], Y0[2], W0[2];
-    X0[0] = mx0 + M[1] * dy + M[2];
-    Y0[0] = mx3 + M[4] * dy + M[5];
-    W0[0] = mx6 + M[7] * dy + M[8];
-    X0[1] = X0[0];
-    Y0[1] = Y0[0];
-    W0[1] = W0[0];
-    if (!one_block) {
-      X0[1] = M[0] * dxo[1] + M[1] * dy + M[2];
-      Y0[1] = M[3] * dxo[1] + M[4] * dy + M[5];
-      W0[1] = M[6] * dxo[1] + M[7] * dy + M[8];
+    if (TAB) {  // the workgroup's table (same expressions, evaluated once per (row, block))
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const double* e = ptab + 3 * (2 * (wave + 4 * i) + tb[p]);
+        X0[p] = e[0];
+        Y0[p] = e[1];
+        W0[p] = e[2];
+      }
+    } else {
+      X0[0] = mx0 + M[1] * dy + M[2];
+      Y0[0] = mx3 + M[4] * dy + M[5];
+      W0[0] = mx6 + M[7] * dy + M[8];
+      X0[1] = X0[0];
+      Y0[1] = Y0[0];
+      W0[1] = W0[0];
+      if (!one_block) {
+        X0[1] = M[0] * dxo[1] + M[1] * dy + M[2];
+        Y0[1] = M[3] * dxo[1] + M[4] * dy + M[5];
+        W0[1] = M[6] * dxo[1] + M[7] * dy + M[8];
+      }
     }
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
@@ -1007,6 +1248,16 @@ warp_perspective_u16_kernel(const uint16_t* __restrict__ src, uint16_t* __restri
   double M[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) M[k] = minv[9 * (size_t)f + k];
+  double* ptab = reinterpret_cast<double*>(stile + PerspTab<Cfg>::kBoxElems);
+  const bool tab = bw0 == 64 && box.mode != 1;  // uniform
+  if (tab) {
+    for (int e = tid; e < PerspTab<Cfg>::kEntries; e += kThreads) {
+      const double dy = (double)(yb + (e >> 1)), dxo = (double)(xb + 64 * (e & 1));
+      ptab[3 * e] = M[0] * dxo + M[1] * dy + M[2];
+      ptab[3 * e + 1] = M[3] * dxo + M[4] * dy + M[5];
+      ptab[3 * e + 2] = M[6] * dxo + M[7] * dy + M[8];
+    }
+  }
   if (box.mode == 0) {
     if (vec_stage) {
       stage_land<Cfg>(stile, box, tid, chunk);
@@ -1016,12 +1267,18 @@ warp_perspective_u16_kernel(const uint16_t* __restrict__ src, uint16_t* __restri
       stage_scalar<C>(S, stile, box, H, W, tid);
   }
   __syncthreads();
-  if (box.mode == 0)
-    persp_rows<Cfg, C, 0>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0);
-  else if (box.mode == 1)
-    persp_rows<Cfg, C, 1>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0);
-  else
-    persp_rows<Cfg, C, 2>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0);
+  if (box.mode == 1)
+    persp_rows<Cfg, C, 1, false>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0, ptab);
+  else if (tab) {
+    if (box.mode == 0)
+      persp_rows<Cfg, C, 0, true>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0, ptab);
+    else
+      persp_rows<Cfg, C, 2, true>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0, ptab);
+  } else if (box.mode == 0) {
+    persp_rows<Cfg, C, 0, false>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0, ptab);
+  } else {
+    persp_rows<Cfg, C, 2, false>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0, ptab);
+  }
 }
 
 template <class Cfg>

@@ -422,6 +422,32 @@ def test_warp_identity_inverse_map_and_extreme_maps(dev):
     assert np.array_equal(out[0], imgs[0])
 
 
+@pytest.mark.parametrize("C,shape", [(3, (3, 240, 512)), (4, (2, 250, 520)), (3, (2, 250, 520))])
+@pytest.mark.parametrize("values", ["14bit", "hot", "blobs", "full"])
+def test_warp_multichannel_fast_path_value_ranges(dev, C, shape, values):
+    """The planar fast path of C = 3 / 4 (boxes de-interleaved into channel planes at the
+    fixed pitch, one b96 / b128 store per lane and row): dark, per-row mixed and bright
+    blends, whole and partial tiles (W = 520, H = 250), near-identity maps."""
+    F, H, W = shape
+    rng = np.random.default_rng(C * 1000 + H)
+    if values == "14bit":
+        imgs = rng.integers(0, 16384, (F, H, W, C))
+    elif values == "hot":
+        imgs = rng.integers(0, 16384, (F, H, W, C))
+        imgs[rng.random((F, H, W, C)) < 2e-4] = 65535
+    elif values == "blobs":
+        imgs = rng.integers(0, 8192, (F, H, W, C))
+        blk = rng.random((F, H // 32 + 1, W // 32 + 1, 1)) < 0.15
+        imgs = np.where(np.repeat(np.repeat(blk, 32, 1), 32, 2)[:, :H, :W], imgs + 36000, imgs)
+    else:
+        imgs = rng.integers(0, 65536, (F, H, W, C))
+    imgs = imgs.astype(np.uint16)
+    Ms = np.stack([synthetic.rigid(rng.normal(0, 0.02), rng.normal(0, 5), rng.normal(0, 5)) for _ in range(F)])
+    out = stages.warp_affine_u16(_t(imgs, dev), _t(Ms, dev)).cpu().numpy()
+    for f in range(F):
+        assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], Ms[f])), f
+
+
 @pytest.mark.parametrize("C", [3, 4])
 def test_warp_multichannel(dev, C):
     rng = np.random.default_rng(C)

@@ -2,6 +2,7 @@
 same-box A/B runs: KCMC_LIB_PATH=ab/<name>.so python tools/match_rates.py ...
 
     python tools/ab_build.py <name> [<git-rev>]     (no rev: the working tree)
+    KCMC_AB_FLAGS="-DKCMC_FASTC_PITCH=192" python tools/ab_build.py p192   (extra compile flags)
 """
 import os
 import shutil
@@ -39,6 +40,7 @@ def main():
                 shutil.copy(os.path.join(REPO, f), dst)
         srcs = [s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))]
         flags = [f if not f.startswith("-I") else f"-I{os.path.join(tmp, 'include')}" for f in B.COMMON_FLAGS]
+        flags += os.environ.get("KCMC_AB_FLAGS", "").split()  # e.g. -DKCMC_FASTC_PITCH=192
         objs = []
         for s in srcs:
             o = os.path.join(tmp, s + ".o")

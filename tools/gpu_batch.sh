@@ -8,9 +8,11 @@
 #   smoke                 __graft_entry__.smoke() -> <out>/smoke.log
 #   bench:<cfg>[:<tag>][:<args,comma,separated>]
 #                         bench.py --config <cfg> --cpu-sample 0 [args] -> <out>/<cfg>_<tag>.json
+#   abbench:<lib>:<cfg>:<tag>  the same against KCMC_LIB_PATH=<lib> (tools/ab_build.py) -> <out>/<cfg>_<tag>.json
+#   envbench:<VAR=val>:<cfg>:<tag>  the same with one extra environment variable
 #   cpubench:<cfg>        bench.py --config <cfg> with its CPU baseline -> <out>/<cfg>_cpu.json
 #   profile:<cfg>         tools/profile_round.sh (bench + rocprofv3 summary + warp PMC) -> <out>/<cfg>/
-#   lab:<binary>[:<tag>]  a lab binary (tools/ or ab/) -> <out>/lab_<tag>.txt
+#   lab:<binary>[:<tag>][:<args,comma,separated>]  a lab binary (tools/ or ab/) -> <out>/lab_<tag>.txt
 set -u
 OUT=${1:?out dir}
 shift
@@ -40,6 +42,14 @@ for step in "$@"; do
       timeout -k 10 300 python bench.py --config "$a" --cpu-sample 0 "${X[@]}" > "$OUT/${a}_$tag.json" \
         2>> "$OUT/bench.err" || exit 1
       echo "$a $tag: $(head -c 160 "$OUT/${a}_$tag.json")" ;;
+    abbench)  # abbench:<ab/lib.so>:<cfg>:<tag>  the bench against another build of the library
+      KCMC_LIB_PATH="$a" timeout -k 10 300 python bench.py --config "$b" --cpu-sample 0 > "$OUT/${b}_$c.json" \
+        2>> "$OUT/bench.err" || exit 1
+      echo "$b $c ($a): $(head -c 160 "$OUT/${b}_$c.json")" ;;
+    envbench)  # envbench:<VAR=value>:<cfg>:<tag>  the bench with one extra environment variable
+      env "$a" timeout -k 10 300 python bench.py --config "$b" --cpu-sample 0 > "$OUT/${b}_$c.json" \
+        2>> "$OUT/bench.err" || exit 1
+      echo "$b $c ($a): $(head -c 160 "$OUT/${b}_$c.json")" ;;
     cpubench)
       timeout -k 10 400 python bench.py --config "$a" > "$OUT/${a}_cpu.json" 2>> "$OUT/bench.err" || exit 1
       echo "$a cpu: $(head -c 160 "$OUT/${a}_cpu.json")" ;;
@@ -47,7 +57,8 @@ for step in "$@"; do
       bash tools/profile_round.sh "$OUT/$a" --config "$a" || exit 1 ;;
     lab)
       tag=${b:-$(basename "$a")}
-      timeout -k 10 240 "$a" > "$OUT/lab_$tag.txt" 2>&1 || exit 1
+      IFS=, read -r -a X <<< "${c:-}"
+      timeout -k 10 240 "$a" "${X[@]}" > "$OUT/lab_$tag.txt" 2>&1 || exit 1
       tail -4 "$OUT/lab_$tag.txt" ;;
     *)
       echo "unknown step $step"; exit 2 ;;

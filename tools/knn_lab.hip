@@ -162,6 +162,20 @@ int main(int argc, char** argv) {
   n_fb = 0;
   for (int32_t c : cnt) n_fb += c;
 #endif
+#ifdef KCMC_STAMP
+  {
+    unsigned long long st[8];
+    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamp), sizeof(st)));
+    const double w = (double)st[4], tl = (double)st[5];
+    printf("stamps (s_memtime ticks, all launches): per wave and %s: %s %.1f, barrier %.1f, total %.1f; "
+           "waves %.0f %ss/wave %.2f\n",
+#ifdef KNN_F32
+           "tile", "vmcnt wait", st[0] / tl, st[1] / tl, st[2] / tl, w, "tile", tl / w);
+#else
+           "chunk", "staging (land_row)", st[0] / tl, st[1] / tl, st[2] / tl, w, "chunk", tl / w);
+#endif
+  }
+#endif
   printf("n_tpl %d D %d F %d nq %d: best %.4f ms mean %.4f ms (%.1f TOPs algorithmic) idx-hash %016llx fallback %ld\n",
          n_tpl, D, F, nq, best, sum / reps, ops / best * 1e-9, ck, n_fb);
   return 0;
