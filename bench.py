@@ -74,6 +74,8 @@ class BenchConfig:
     # CUs per shader engine of the analysis stream's fixed CU slice (OverlappedSlabs
     # ana_cus_per_se; 0: both streams share every CU)
     ana_cus_per_se: int = 0
+    # depth 2 + match beside: warp(k-1) queued before match(k) (OverlappedSlabs warp_first)
+    warp_first: bool = False
 
 
 # BASELINE.json configs.  c2 (configs[1]) is the headline line; the others are the
@@ -440,6 +442,13 @@ def main():
                          "ana_cus_per_se; default: the config's, 0 = no CU split)")
     ap.add_argument("--warp-shares", action="store_true",
                     help="with --ana-cus: the warp stream keeps every CU (only the analysis is confined)")
+    ap.add_argument("--warp-first", action="store_true", default=None,
+                    help="depth 2 + match beside: queue warp(k-1) before match(k) (OverlappedSlabs warp_first; "
+                         "default: the config's)")
+    ap.add_argument("--no-warp-first", dest="warp_first", action="store_false")
+    ap.add_argument("--no-device-merge", dest="device_merge", action="store_false",
+                    help="merge the consensus votes on the host (OverlappedSlabs device_merge=False; the "
+                         "round-3 schedule: votes D2H -> host merge -> pack H2D between vote and lookup)")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
@@ -448,6 +457,8 @@ def main():
         args.frames = bc.frames_per_gpu
     if args.pipeline_depth is None:
         args.pipeline_depth = bc.pipeline_depth
+    if args.warp_first is None:
+        args.warp_first = bc.warp_first
     if args.ana_cus is None:
         args.ana_cus = bc.ana_cus_per_se if not args.no_corun else 0
     if args.match_beside is None:
@@ -489,7 +500,9 @@ def main():
                                                             match_beside=args.match_beside,
                                                             fit_first=args.fit_first,
                                                             ana_cus_per_se=args.ana_cus,
-                                                            warp_exclusive=not args.warp_shares)
+                                                            warp_exclusive=not args.warp_shares,
+                                                            warp_first=args.warp_first,
+                                                            device_merge=args.device_merge)
 
     def step(timer):
         if ov is None:
@@ -560,6 +573,11 @@ def main():
                                     else "pipelined: match+vote(k) -> warp(k-2) -> lookup+RANSAC(k-1)") + (
                                         " on one stream" if args.no_corun else ", RANSAC on a second stream beside the warp"
                                     ) + ", host consensus merge under the warp"
+        stage_ms["schedule"] += ("; consensus merged on the device" if args.device_merge and
+                                 stages.merge_device_supported(bc.n_tpl, bc.n_kp_global) else
+                                 "; consensus merged on the host")
+        if args.warp_first and args.match_beside and args.pipeline_depth == 2:
+            stage_ms["schedule"] += "; warp(k-1) queued before match(k)"
         if args.ana_cus:
             stage_ms["schedule"] += (f"; analysis stream on {args.ana_cus} of 8 CUs per shader engine"
                                      + (", the warp on every CU" if args.warp_shares else ", the warp on the other "

@@ -197,6 +197,15 @@ int kcmc_consensus_vote_host(const uint32_t* keep_bits_host, int n_frames, int n
 int kcmc_consensus_merge(const int64_t* votes_host, int world, int n_tpl, int n_kp_global, int n_min,
                          int32_t* out_consensus_host, int32_t* out_votes_host, int* out_n_consensus,
                          int32_t* out_cons_pack_host);
+/* The same merge on the device (no host round trip in a pipelined step): votes_dev
+ * [world, 2, n_tpl]; out_consensus_dev / out_votes_dev [n_kp_global] (the first nc valid);
+ * out_meta_dev [2] = (nc, status: 0 ok, 1 fewer than n_min voted -- the caller raises
+ * VideoAligner.AlignmentError --, 2 invalid votes); out_pack_dev [n_kp_global + ceil(n_tpl/32)]:
+ * set(consensus) iteration order in [0, nc), the consensus bitmask from n_kp_global on.
+ * n_tpl <= 4096 and n_kp_global <= 1024 (KCMC_EUNSUPPORTED otherwise). */
+int kcmc_consensus_merge_device(kcmc_ctx* ctx, const int64_t* votes_dev, int world, int n_tpl, int n_kp_global,
+                                int n_min, int32_t* out_consensus_dev, int32_t* out_votes_dev, int32_t* out_meta_dev,
+                                int32_t* out_pack_dev, kcmc_stream_t stream);
 /* Device lookup: cons_pack_dev = kcmc_consensus_merge's pack (nc entries + bitmask words);
  * out_pt_off_dev [n_frames + 1], out_pt_idx_dev [n_frames * nc]; scratch_dev of at least
  * kcmc_consensus_lookup_scratch_bytes(n_frames, nc) bytes (the CPython set emulation tables
@@ -205,6 +214,13 @@ long long kcmc_consensus_lookup_scratch_bytes(int n_frames, int nc);
 int kcmc_consensus_lookup(kcmc_ctx* ctx, const uint32_t* keep_bits_dev, int n_frames, int n_tpl,
                           const int32_t* cons_pack_dev, int nc, int32_t* out_pt_off_dev,
                           int32_t* out_pt_idx_dev, void* scratch_dev, kcmc_stream_t stream);
+/* kcmc_consensus_lookup on kcmc_consensus_merge_device's outputs: the consensus size is read
+ * from meta_dev[0] on the device; out_pt_idx_dev [n_frames * min(n_kp_global, n_tpl)], scratch
+ * of kcmc_consensus_lookup_scratch_bytes(n_frames, min(n_kp_global, n_tpl)) bytes. */
+int kcmc_consensus_lookup_device(kcmc_ctx* ctx, const uint32_t* keep_bits_dev, int n_frames, int n_tpl,
+                                 const int32_t* cons_pack_dev, int n_kp_global, const int32_t* meta_dev,
+                                 int32_t* out_pt_off_dev, int32_t* out_pt_idx_dev, void* scratch_dev,
+                                 kcmc_stream_t stream);
 int kcmc_consensus_lookup_host(const uint32_t* keep_bits_host, int n_frames, int n_tpl,
                                const int32_t* cons_iter_host, int nc, int32_t* out_pt_off_host,
                                int32_t* out_pt_idx_host);

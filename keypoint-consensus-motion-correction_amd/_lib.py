@@ -40,8 +40,10 @@ EXPORTED_SYMBOLS = (
     "kcmc_consensus_vote",
     "kcmc_consensus_vote_host",
     "kcmc_consensus_merge",
+    "kcmc_consensus_merge_device",
     "kcmc_consensus_lookup_scratch_bytes",
     "kcmc_consensus_lookup",
+    "kcmc_consensus_lookup_device",
     "kcmc_consensus_lookup_host",
     "kcmc_params_boundary",
     "kcmc_hypothesis_table",
@@ -108,6 +110,8 @@ _SIGNATURES = {
     "kcmc_consensus_merge": ([P, I, I, I, I, P, P, P, P], I),
     "kcmc_consensus_lookup_scratch_bytes": ([I, I], LL),
     "kcmc_consensus_lookup": ([P, P, I, I, P, I, P, P, P, P], I),
+    "kcmc_consensus_merge_device": ([P, P, I, I, I, I, P, P, P, P, P], I),
+    "kcmc_consensus_lookup_device": ([P, P, I, I, P, I, P, P, P, P, P], I),
     "kcmc_consensus_lookup_host": ([P, I, I, P, I, P, P], I),
     "kcmc_params_boundary": ([P, P, I, I, P, P], I),
     "kcmc_hypothesis_table": ([I, I, U32, I, P], I),

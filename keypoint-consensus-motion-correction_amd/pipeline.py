@@ -202,7 +202,8 @@ def _check_point_counts(cons: stages.Consensus, cfg: AlignConfig) -> None:
 
 def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.Consensus,
                  cfg: AlignConfig, lists_dev: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                 stream: Optional[int] = None, max_workgroups: int = 0) -> stages.RansacResult:
+                 stream: Optional[int] = None, max_workgroups: int = 0,
+                 max_n: Optional[int] = None) -> stages.RansacResult:
     """VA:137-142: RANSAC of every frame's consensus points (src = the frame's matched
     keypoints, dst = template keypoints).  params [F, 2, 3] for the euclidean and
     affine models (model.params[:2], like VA:319), [F, 3, 3] for the projective one.
@@ -219,7 +220,8 @@ def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.C
         _check_point_counts(cons, cfg)
         prepare_ransac(dev, cfg)
         rr = stages.ransac_lists(cfg.ransac_model, src, kp_tpl, cons.pt_off_dev, cons.pt_idx_dev, n_tpl,
-                                 max_n=max(len(cons.order), 1), trials=cfg.ransac_trials,
+                                 max_n=max_n if max_n is not None else max(len(cons.order), 1),
+                                 trials=cfg.ransac_trials,
                                  residual_threshold=cfg.ransac_threshold, spatial_rate=cfg.spatial_rate,
                                  n_skip=cfg.effective_frame_skip, stream=stream, max_workgroups=max_workgroups)
     else:
@@ -356,6 +358,7 @@ class _SlabInFlight:
     aligned: Optional[torch.Tensor] = None
     fitted_ev: Optional[torch.cuda.Event] = None   # end of RANSAC(k) on the analysis stream (corun)
     n_bound: int = 0                               # elements of the gathered boundaries (sharded)
+    dchoice: Optional[stages.DeviceChoice] = None  # the consensus merged on the device (device_merge)
 
 
 class OverlappedSlabs:
@@ -404,7 +407,8 @@ class OverlappedSlabs:
     def __init__(self, device, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
                  counts: Optional[List[int]] = None, group=None, depth: int = 2, corun: bool = True,
                  ransac_grid: Optional[int] = None, match_beside: bool = False, fit_first: bool = False,
-                 ana_cus_per_se: int = 0, warp_exclusive: bool = True):
+                 ana_cus_per_se: int = 0, warp_exclusive: bool = True, warp_first: bool = False,
+                 device_merge: bool = True):
         if depth not in (2, 3):
             raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
         if match_beside and not corun:
@@ -419,6 +423,14 @@ class OverlappedSlabs:
         # so it starts beside match(k).  Measured slower at c3 (2.36 M vs 2.91 M frames/s,
         # same box: RANSAC then shares the CUs with the match and the warp), so off.
         self.fit_first = bool(fit_first)
+        # warp_first (depth 2, match_beside): warp(k-1) queued before match(k) (see submit)
+        self.warp_first = bool(warp_first)
+        # device_merge: Counter.most_common + set(consensus) (VA:240-248) on the device right
+        # behind the vote (kcmc_consensus_merge_device), so lookup + RANSAC are queued with no
+        # host round trip; the host checks N_KP_GLOBAL_MIN and reads the consensus when it
+        # collects the parameters (round 4; the host merge otherwise, and for shapes the
+        # device merge does not take: n_tpl > 4096 or n_kp_global > 1024)
+        self.device_merge = bool(device_merge)
         if counts is not None and len(counts) > 1 and cfg.frame_downsample_rate != 1:
             # the rank's first frame is counted in sample frames, the affines in full-rate
             # frames: the same restriction as distributed.align_sharded
@@ -535,10 +547,15 @@ class OverlappedSlabs:
                     t.record_stream(self.stream)
             if self.match_beside and self.depth == 2:
                 # kernel stream: warp(k-1); analysis stream: match(k) -> lookup + RANSAC(k),
-                # all of slab k beside warp(k-1); warp(k) (next submit) waits for RANSAC(k)
+                # all of slab k beside warp(k-1); warp(k) (next submit) waits for RANSAC(k).
+                # warp_first: the host queues warp(k-1) (it waits for RANSAC(k-1)) before
+                # match(k), so the warp's plan kernel does not queue behind the match's
+                # persistent workgroups (c3 trace: plan 10 -> 100 us, the warp 0.1 ms late)
                 fitted, self._fitted = self._fitted, None
+                if self.warp_first and fitted is not None and self._device_maps():
+                    self._warp_device_maps(fitted, mark)
                 new = self._match(inp, out, mark)
-                if fitted is not None and self._device_maps():
+                if not self.warp_first and fitted is not None and self._device_maps():
                     self._warp_device_maps(fitted, mark)
                 self._fitted = self._fit(new, mark)
                 return self._finish(fitted, mark) if fitted is not None else None
@@ -610,10 +627,19 @@ class OverlappedSlabs:
         if self._sharded():
             votes = self._gather(votes)  # the kernel stream waits for the collective
             self._queued()
-        ready = self._at_tail(mark)
         slot = self._slots.pop() if self._slots else _Slot()
+        if self._use_device_merge(n_tpl):
+            dch = stages.consensus_merge_device(votes, n_tpl, self.cfg.n_kp_global, self.cfg.n_kp_global_min,
+                                                stream=self._hs)
+            self._queued()
+            matched = self._at_tail(mark)
+            return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=matched, dchoice=dch)
+        ready = self._at_tail(mark)
         self._d2h(slot.buf("votes", votes.numel(), torch.int64), votes, ready, slot.votes_ev)
         return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=matched)
+
+    def _use_device_merge(self, n_tpl: int) -> bool:
+        return self.device_merge and stages.merge_device_supported(n_tpl, self.cfg.n_kp_global)
 
     def _match_beside(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
         """match(k) and its vote on the analysis stream (allocated there), ahead of the lookup +
@@ -634,14 +660,22 @@ class OverlappedSlabs:
             mark("m1", matched)
             if self._sharded():
                 votes = self._gather(votes)  # the analysis stream waits for the collective
+            dch = None
+            if self._use_device_merge(n_tpl):
+                dch = stages.consensus_merge_device(votes, n_tpl, self.cfg.n_kp_global, self.cfg.n_kp_global_min,
+                                                    stream=self._ha)
             ready = torch.cuda.Event()
             ready.record(self.ana)
         slot = self._slots.pop() if self._slots else _Slot()
+        if dch is not None:
+            return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=ready, dchoice=dch)
         self._d2h(slot.buf("votes", votes.numel(), torch.int64), votes, ready, slot.votes_ev)
         return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=matched)
 
     def _fit(self, p: _SlabInFlight, mark) -> _SlabInFlight:
         """The consensus merge (host) and the lookup + RANSAC (device) of a matched slab."""
+        if p.dchoice is not None:
+            return self._fit_merged(p, mark)
         cfg = self.cfg
         n_tpl = p.inp.des_tpl.shape[0]
         n_local = p.inp.q_off.numel() - 1
@@ -674,13 +708,40 @@ class OverlappedSlabs:
             self._queued()
         return p
 
-    def _fit_device(self, p: _SlabInFlight, choice: stages.ConsensusChoice, pack_dev: torch.Tensor, mark,
-                    hs: int) -> None:
+    def _fit_merged(self, p: _SlabInFlight, mark) -> _SlabInFlight:
+        """Lookup + RANSAC of a slab whose consensus was merged on the device: queued at once
+        (no host wait), on the analysis stream behind the match (corun) or on the kernel stream."""
+        d = p.dchoice
+        if self.corun:
+            with torch.cuda.stream(self.ana):
+                if not self.match_beside:
+                    self.ana.wait_event(p.matched)
+                for t in (p.match.kp_ordered, p.match.keep_bits, p.inp.kp_tpl, d.cons, d.votes, d.meta, d.pack):
+                    t.record_stream(self.ana)
+                self._fit_device(p, None, None, mark, self._ha)
+                for t in (p.rr.params, p.rr.inliers, p.rr.n_inliers, p.rr.best_trial):
+                    t.record_stream(self.stream)
+                p.fitted_ev = torch.cuda.Event()
+                p.fitted_ev.record(self.ana)
+        else:
+            self._fit_device(p, None, None, mark, self._hs)
+            self._queued()
+        return p
+
+    def _fit_device(self, p: _SlabInFlight, choice: Optional[stages.ConsensusChoice], pack_dev: Optional[torch.Tensor],
+                    mark, hs: int) -> None:
         """Lookup + RANSAC of a slab whose consensus is known, on the current stream (hs)."""
         n_tpl = p.inp.des_tpl.shape[0]
         mark("r0", None)
-        p.cons = lookup_stage(p.match, n_tpl, choice, pack_dev, stream=hs)
-        p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, stream=hs, max_workgroups=self.ransac_grid)
+        if p.dchoice is not None:
+            pt_off, pt_idx = stages.consensus_lookup_device(p.match.keep_bits, n_tpl, p.dchoice, stream=hs)
+            p.cons = stages.Consensus(np.zeros(0, np.int32), np.zeros(0, np.int32), pt_off_dev=pt_off,
+                                      pt_idx_dev=pt_idx)
+            p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, stream=hs, max_workgroups=self.ransac_grid,
+                                max_n=min(self.cfg.n_kp_global, n_tpl))
+        else:
+            p.cons = lookup_stage(p.match, n_tpl, choice, pack_dev, stream=hs)
+            p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, stream=hs, max_workgroups=self.ransac_grid)
         mark("r1", None)
         params = p.rr.params
         after = torch.cuda.Event()
@@ -697,6 +758,10 @@ class OverlappedSlabs:
             # analysis stream and break the overlap
             self._d2h(p.slot.buf("pt_off", p.cons.pt_off_dev.numel(), torch.int32), p.cons.pt_off_dev, after,
                       p.slot.params_ev)
+        if p.dchoice is not None:  # the device merge's status and consensus, for _finish
+            d = p.dchoice
+            for name, t in (("meta", d.meta), ("cons", d.cons), ("cvotes", d.votes)):
+                self._d2h(p.slot.buf(name, t.numel(), torch.int32), t, after, p.slot.params_ev)
         self._d2h(p.slot.buf("params", params.numel(), torch.float64), params, after, p.slot.params_ev)
 
     def _warp_device_maps(self, p: _SlabInFlight, mark) -> None:
@@ -715,6 +780,15 @@ class OverlappedSlabs:
         """Host post-processing of slab p (VA:143-145) and the warps that need its maps."""
         self._wait(p.slot.params_ev)  # after RANSAC(k): its parameters are on the host
         n = p.inp.frames.shape[0]
+        if p.dchoice is not None:
+            # the device merge: N_KP_GLOBAL_MIN (AlignmentError, VA:241-244) and the consensus
+            nc = stages.check_device_choice(p.slot.buf("meta", 2, torch.int32).numpy())
+            k = p.dchoice.n_kp_global
+            p.cons.order = p.slot.buf("cons", k, torch.int32).numpy()[:nc].copy()
+            p.cons.votes = p.slot.buf("cvotes", k, torch.int32).numpy()[:nc].copy()
+            if self._rank == 0:
+                n_all = sum(self.counts) if self._sharded() else p.inp.q_off.numel() - 1
+                _log_rates(self.logger, p.cons.votes, n_all)
         if logging_enabled(self.logger) and "pt_off" in p.slot.bufs:
             pt_off = p.slot.buf("pt_off", p.cons.pt_off_dev.numel(), torch.int32).numpy()
             _log_low_counts(self.logger, np.diff(pt_off), self.cfg, p.f0)

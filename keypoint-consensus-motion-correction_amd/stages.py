@@ -332,6 +332,82 @@ def consensus_merge(votes: np.ndarray, n_tpl: int, n_kp_global: int, n_min: int,
     return ConsensusChoice(order[:n].copy(), counts[:n].copy(), pack_out)
 
 
+@dataclass
+class DeviceChoice:
+    """kcmc_consensus_merge_device's outputs, on the device: the first meta[0] entries of
+    ``cons`` / ``votes`` are Counter.most_common(n_kp_global) (VA:240); meta[1] is 0, 1
+    (fewer than N_KP_GLOBAL_MIN voted: AlignmentError) or 2 (invalid votes); ``pack`` =
+    set(consensus) iteration order, then the consensus bitmask from n_kp_global on."""
+    cons: torch.Tensor
+    votes: torch.Tensor
+    meta: torch.Tensor
+    pack: torch.Tensor
+    n_kp_global: int
+
+
+def merge_device_supported(n_tpl: int, n_kp_global: int) -> bool:
+    return 1 <= n_tpl <= 4096 and 1 <= n_kp_global <= 1024
+
+
+def consensus_merge_device(votes: torch.Tensor, n_tpl: int, n_kp_global: int, n_min: int,
+                           stream: Optional[int] = None) -> DeviceChoice:
+    """consensus_merge on the device (no host round trip): votes [world, 2, n_tpl] or
+    [2, n_tpl] i64 device tensor.  The caller checks meta (check_device_choice) before it
+    uses the consensus on the host."""
+    dev = _device_of(votes)
+    _require(votes, "votes", torch.int64, dev)
+    world = votes.numel() // (2 * n_tpl) if n_tpl else 1
+    if not n_tpl or votes.numel() != world * 2 * n_tpl:
+        raise ValueError("votes must be [world, 2, n_tpl]")
+    words = (n_tpl + 31) // 32
+    ch = DeviceChoice(cons=torch.empty(n_kp_global, dtype=torch.int32, device=dev),
+                      votes=torch.empty(n_kp_global, dtype=torch.int32, device=dev),
+                      meta=torch.empty(2, dtype=torch.int32, device=dev),
+                      pack=torch.empty(n_kp_global + words, dtype=torch.int32, device=dev), n_kp_global=n_kp_global)
+    _lib.check(_lib.load().kcmc_consensus_merge_device(
+        _ctx(dev).handle, _ptr(votes), int(world), int(n_tpl), int(n_kp_global), int(n_min), _ptr(ch.cons),
+        _ptr(ch.votes), _ptr(ch.meta), _ptr(ch.pack), _stream(dev, stream)))
+    return ch
+
+
+ALIGNMENT_ERROR_TEXT = ("Too few keypoints found. Try a higher quality video, or decrease "
+                        "`VideoAligner.N_KP_GLOBAL_MIN`")
+
+
+def check_device_choice(meta: np.ndarray) -> int:
+    """The host side of a device merge: raises like kcmc_consensus_merge (AlignmentError below
+    N_KP_GLOBAL_MIN, VA:241-244; ValueError for invalid votes); returns nc."""
+    if int(meta[1]) == 1:
+        from .video_aligner import AlignmentError
+
+        raise AlignmentError(ALIGNMENT_ERROR_TEXT)
+    if int(meta[1]) != 0:
+        raise ValueError("consensus merge: invalid votes (a negative count or a voted template without a "
+                         "first-occurrence key)")
+    return int(meta[0])
+
+
+def consensus_lookup_device(keep_bits: torch.Tensor, n_tpl: int, ch: DeviceChoice,
+                            stream: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """consensus_lookup on a device merge: the consensus size is read on the device;
+    pt_idx is sized for min(n_kp_global, n_tpl) points per frame."""
+    dev = _device_of(keep_bits)
+    _require(keep_bits, "keep_bits", torch.int32, dev, 2)
+    F = keep_bits.shape[0]
+    if keep_bits.shape[1] != (n_tpl + 31) // 32:
+        raise ValueError("consensus_lookup_device: inconsistent shapes")
+    L = _lib.load()
+    ncap = min(ch.n_kp_global, n_tpl)
+    pt_off = torch.empty(F + 1, dtype=torch.int32, device=dev)
+    pt_idx = torch.empty(max(F * ncap, 1), dtype=torch.int32, device=dev)
+    sb = int(L.kcmc_consensus_lookup_scratch_bytes(F, ncap))
+    scratch = torch.empty(sb, dtype=torch.uint8, device=dev) if sb > 0 else None
+    _lib.check(L.kcmc_consensus_lookup_device(_ctx(dev).handle, _ptr(keep_bits), F, int(n_tpl), _ptr(ch.pack),
+                                              int(ch.n_kp_global), _ptr(ch.meta), _ptr(pt_off), _ptr(pt_idx),
+                                              _ptr(scratch), _stream(dev, stream)))
+    return pt_off, pt_idx
+
+
 def consensus_lookup(keep_bits: torch.Tensor, n_tpl: int, pack_dev: torch.Tensor, nc: int,
                      stream: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """The lookup part of the consensus (VA:274) on the device: every frame's

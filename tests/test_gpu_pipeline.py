@@ -148,6 +148,15 @@ def test_overlapped_slabs_equal_align_slab(dev, depth, corun, grid, beside, firs
     _check_overlapped(ov, slabs, ref, depth)
 
 
+def test_overlapped_slabs_warp_first(dev):
+    """warp(k-1) queued before match(k) (depth 2, match beside): same results."""
+    cfg = pipeline.AlignConfig(n_kp_global=60)
+    slabs = _gap_slabs(dev)
+    ref = [pipeline.align_slab(s, cfg) for s in slabs]
+    ov = pipeline.OverlappedSlabs(dev, cfg, match_beside=True, warp_first=True)
+    _check_overlapped(ov, slabs, ref, 2)
+
+
 @pytest.mark.parametrize("cus,exclusive,beside", [(1, True, True), (2, False, True), (3, True, False)])
 def test_overlapped_slabs_cu_split(dev, cus, exclusive, beside):
     """The analysis stream on a fixed CU slice (the first `cus` CUs of every shader engine;

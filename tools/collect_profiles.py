@@ -2,7 +2,7 @@
 measured on (the GPU box has no .git, so the sha is taken here: HEAD, which must be the
 tree that was sent; a dirty tree is recorded as such).
 
-    python tools/collect_profiles.py gpurun_out/<dir> <tag> [--config c2]
+    python tools/collect_profiles.py gpurun_out/<dir> <tag> [--config c2] [--commit <sha>]
 
 Writes profiles/<tag>_bench_<config>.json (the bench line), <tag>_<config>_kernel_stats.md
 (rocprofv3 summary of the same command), <tag>_warp_pmc_<config>.txt and the traffic file
@@ -29,7 +29,8 @@ def main():
     a = sys.argv[1:]
     src, tag = a[0], a[1]
     cfg = a[a.index("--config") + 1] if "--config" in a else "c2"
-    sha = commit()
+    # --commit <sha>: the tree the GPU run was sent from, when HEAD has moved on since
+    sha = a[a.index("--commit") + 1] if "--commit" in a else commit()
     prof = os.path.join(REPO, "profiles")
     line = open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1]
     d = json.loads(line)
