@@ -446,9 +446,11 @@ def main():
                     help="depth 2 + match beside: queue warp(k-1) before match(k) (OverlappedSlabs warp_first; "
                          "default: the config's)")
     ap.add_argument("--no-warp-first", dest="warp_first", action="store_false")
-    ap.add_argument("--no-device-merge", dest="device_merge", action="store_false",
-                    help="merge the consensus votes on the host (OverlappedSlabs device_merge=False; the "
-                         "round-3 schedule: votes D2H -> host merge -> pack H2D between vote and lookup)")
+    ap.add_argument("--device-merge", action="store_true",
+                    help="merge the consensus votes on the device (OverlappedSlabs device_merge=True: "
+                         "kcmc_consensus_merge_device behind the vote, no host round trip before the lookup; "
+                         "default: the host merge)")
+    ap.add_argument("--no-device-merge", dest="device_merge", action="store_false")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()

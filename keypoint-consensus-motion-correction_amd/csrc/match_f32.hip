@@ -29,12 +29,12 @@
 //   accumulation and the norms, bounded below at its use), so v~ orders a lane's frame
 //   rows like |a - b|^2 = 2 v + |a|^2 - K up to 2 beta, and v~ >= 0.  A distance costs a
 //   compare with the list's bound and, when some lane of the wave needs it, 9 VALU: the
-//   key (v~'s bits with the low bits replaced by the frame row: 2 ops), a sorted top-6
-//   insertion (v_med3_u32 x 5 + v_min_u32) and the new bound.  After the frame, the top-6 of
-//   the two lane halves are merged; when the 6th value exceeds v(2) (1 + 2T) + 2B the
+//   key (v~'s bits with the low bits replaced by the frame row: 1 op), a sorted top-8
+//   insertion (v_med3_u32 x 7 + v_min_u32).  After the frame, the top-8 of
+//   the two lane halves are merged; when the 8th value exceeds v(2) (1 + 2T) + 2B the
 //   exact top-2 lies among the listed rows below that bound (usually 2-3), which phase 2
 //   re-evaluates with the exact fp64 definition and orders by (dist, index).  Rows that
-//   cannot be certified (6+ rows within 2B of the second) are appended to their frame's
+//   cannot be certified (8+ rows within 2B of the second) are appended to their frame's
 //   list, which knn2_l2f32_fallback_kernel finishes by exact brute force.
 #include <cfloat>
 
@@ -58,7 +58,7 @@ constexpr int kImgC = kTile * kRowB * 2;  // byte offset of the per-row C' value
 constexpr int kImgBytes = 18 * 1024;      // tile image, whole 1 KiB LDS-DMA pieces
 constexpr int kPieces = kImgBytes / 1024;
 static_assert(kImgC + kTile * 4 <= kImgBytes, "tile image layout");
-constexpr int kTop = 6;                   // approximate top-K per lane
+constexpr int kTop = 8;                   // approximate top-K per lane
 constexpr int kImgThreads = 1024;         // frame_images_kernel
 
 // The build's exact distance (identical operation order in the oracle).
@@ -128,10 +128,10 @@ __device__ __forceinline__ void topk_key(uint32_t (&k)[kTop], uint32_t x) {
   k[0] = min(k[0], x);
 }
 
-// One distance of the tile loop: if its value bits x are below the list's last key k5
-// (some lane of the wave takes the branch), key = (x & kmask) | id enters the sorted top-6
-// in place (v_and_or_b32 + 5 v_med3_u32 + v_min_u32: 7 VALU).  Comparing the raw bits with
-// k5 keeps the bound the certification needs: a rejected x >= k5 truncates to >= the last
+// One distance of the tile loop: if its value bits x are below the list's last key k7
+// (some lane of the wave takes the branch), key = (x & kmask) | id enters the sorted top-8
+// in place (v_and_or_b32 + 7 v_med3_u32 + v_min_u32: 9 VALU).  Comparing the raw bits with
+// k7 keeps the bound the certification needs: a rejected x >= k7 truncates to >= the last
 // listed value, and so does every key the list pushes out.  Hand-written because the
 // backend gave the updated list fresh registers on every insertion and copied it back
 // (6-10 v_mov per insertion); id is wave-uniform (an SGPR), kmask a VGPR (a VOP3 reads
@@ -139,11 +139,13 @@ __device__ __forceinline__ void topk_key(uint32_t (&k)[kTop], uint32_t x) {
 // AFTER_MFMA: x was written by the MFMA just issued; hipcc pads nothing inside an asm
 // string, so the string opens with the 12 wait states an 8-pass XDL result needs before a
 // VALU reads it (the later values of the tile are read more than 12 states later).
-#define KCMC_TOPK_TRY6_BODY                            \
-  "v_cmp_lt_u32 vcc, %[x], %[k5]\n\t"                  \
+#define KCMC_TOPK_TRY_BODY                             \
+  "v_cmp_lt_u32 vcc, %[x], %[k7]\n\t"                  \
   "s_and_saveexec_b64 %[sv], vcc\n\t"                  \
   "s_cbranch_execz 1f\n\t"                             \
   "v_and_or_b32 %[x], %[x], %[km], %[id]\n\t"          \
+  "v_med3_u32 %[k7], %[k6], %[k7], %[x]\n\t"           \
+  "v_med3_u32 %[k6], %[k5], %[k6], %[x]\n\t"           \
   "v_med3_u32 %[k5], %[k4], %[k5], %[x]\n\t"           \
   "v_med3_u32 %[k4], %[k3], %[k4], %[x]\n\t"           \
   "v_med3_u32 %[k3], %[k2], %[k3], %[x]\n\t"           \
@@ -152,22 +154,22 @@ __device__ __forceinline__ void topk_key(uint32_t (&k)[kTop], uint32_t x) {
   "v_min_u32 %[k0], %[k0], %[x]\n"                      \
   "1:\n\t"                                             \
   "s_or_b64 exec, exec, %[sv]"
-#define KCMC_TOPK_TRY6_OPERANDS                                                                                 \
+#define KCMC_TOPK_TRY_OPERANDS                                                                                 \
   : [k0] "+v"(k[0]), [k1] "+v"(k[1]), [k2] "+v"(k[2]), [k3] "+v"(k[3]), [k4] "+v"(k[4]), [k5] "+v"(k[5]),      \
-    [x] "+v"(xb), [sv] "=&s"(saved)                                                                           \
+    [k6] "+v"(k[6]), [k7] "+v"(k[7]), [x] "+v"(xb), [sv] "=&s"(saved)                                         \
   : [km] "v"(kmask), [id] "s"(id)                                                                             \
   : "vcc"
 template <bool AFTER_MFMA>
-__device__ __forceinline__ void topk_try6(uint32_t (&k)[kTop], uint32_t xb, uint32_t kmask, uint32_t id) {
-  static_assert(kTop == 6, "topk_try6 keeps a top-6");
+__device__ __forceinline__ void topk_try(uint32_t (&k)[kTop], uint32_t xb, uint32_t kmask, uint32_t id) {
+  static_assert(kTop == 8, "topk_try keeps a top-8");
   uint64_t saved;
   if constexpr (AFTER_MFMA)
-    asm volatile("s_nop 11\n\t" KCMC_TOPK_TRY6_BODY KCMC_TOPK_TRY6_OPERANDS);
+    asm volatile("s_nop 11\n\t" KCMC_TOPK_TRY_BODY KCMC_TOPK_TRY_OPERANDS);
   else
-    asm volatile(KCMC_TOPK_TRY6_BODY KCMC_TOPK_TRY6_OPERANDS);
+    asm volatile(KCMC_TOPK_TRY_BODY KCMC_TOPK_TRY_OPERANDS);
 }
-#undef KCMC_TOPK_TRY6_BODY
-#undef KCMC_TOPK_TRY6_OPERANDS
+#undef KCMC_TOPK_TRY_BODY
+#undef KCMC_TOPK_TRY_OPERANDS
 
 // Sorted approximate top-kTop values with the frame rows of the first kTop - 1.
 struct TopK {
@@ -414,7 +416,7 @@ __device__ __forceinline__ void dma_tile(const uint8_t* __restrict__ src, uint8_
 }
 
 // 6 waves per SIMD (<= 80 VGPRs; the epilogue spills a few, the tile loop none): the
-// waits on LDS and the MFMA results hide behind the other waves' top-6 VALU work
+// waits on LDS and the MFMA results hide behind the other waves' top-K VALU work
 // (c5 lab 4.56 -> 4.38 ms against 4 waves per SIMD with three tile buffers)
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 6))) void knn2_l2f32_kernel(
     const float* __restrict__ des_tpl, int n_tpl, int D, const float* __restrict__ des_q,
@@ -495,10 +497,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 6))
       // few hundred rows most distances of a wave skip the insertion (the branch is per
       // wave): 1 + 7 P VALU per distance, P = the share of the wave's values some lane
       // inserts (0.31 on the c5 data, simulated; 0.34 from the round-3 PMC's INT32 count)
-      topk_try6<true>(ck, __float_as_uint(acc[0]), kmask, (uint32_t)(hh * 16) | tbase);
+      topk_try<true>(ck, __float_as_uint(acc[0]), kmask, (uint32_t)(hh * 16) | tbase);
 #pragma unroll
       for (int r = 1; r < 16; ++r)
-        topk_try6<false>(ck, __float_as_uint(acc[r]), kmask, (uint32_t)(hh * 16 + r) | tbase);
+        topk_try<false>(ck, __float_as_uint(acc[r]), kmask, (uint32_t)(hh * 16 + r) | tbase);
     }
   }
 

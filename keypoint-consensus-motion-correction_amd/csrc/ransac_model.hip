@@ -813,6 +813,7 @@ __global__ __launch_bounds__(kThreads) void ransac_model_score_kernel(
     const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, double tq, int n_skip,
     double* out_params, double* best_model, uint8_t* __restrict__ out_inl,
     int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
+  KCMC_ANA_PRIO_ENTER();
   for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
     ransac_model_score_frame<MODEL, LARGE>(f, src, dst, pt_idx, pt_off, src_stride, hyp, hyp_off, hyp_off_len, T,
                                            thresh, tq, n_skip, out_params, best_model, out_inl, out_nin, out_best);
@@ -826,6 +827,7 @@ __global__ __launch_bounds__(256) void ransac_model_refit_kernel(
     const int32_t* __restrict__ pt_off, int src_stride, const uint8_t* __restrict__ inl,
     const int32_t* __restrict__ nin, const double* best_model, int n_frames, double rate,
     double* out_params) {
+  KCMC_ANA_PRIO_ENTER();
   constexpr int n = MODEL == KCMC_MODEL_AFFINE ? 7 : 9;
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;

@@ -408,7 +408,7 @@ class OverlappedSlabs:
                  counts: Optional[List[int]] = None, group=None, depth: int = 2, corun: bool = True,
                  ransac_grid: Optional[int] = None, match_beside: bool = False, fit_first: bool = False,
                  ana_cus_per_se: int = 0, warp_exclusive: bool = True, warp_first: bool = False,
-                 device_merge: bool = True):
+                 device_merge: bool = False):
         if depth not in (2, 3):
             raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
         if match_beside and not corun:
@@ -429,7 +429,10 @@ class OverlappedSlabs:
         # behind the vote (kcmc_consensus_merge_device), so lookup + RANSAC are queued with no
         # host round trip; the host checks N_KP_GLOBAL_MIN and reads the consensus when it
         # collects the parameters (round 4; the host merge otherwise, and for shapes the
-        # device merge does not take: n_tpl > 4096 or n_kp_global > 1024)
+        # device merge does not take: n_tpl > 4096 or n_kp_global > 1024).  Off by default:
+        # in the beside-the-warp schedule the host merge of slab k-1 is already off the
+        # analysis stream's path (its votes were ready a step earlier), so the merge kernel
+        # only adds work there (c3 2.98-2.99 M vs 3.03-3.04 M frames/s, c2 607 k vs 622 k)
         self.device_merge = bool(device_merge)
         if counts is not None and len(counts) > 1 and cfg.frame_downsample_rate != 1:
             # the rank's first frame is counted in sample frames, the affines in full-rate

@@ -148,6 +148,18 @@ def test_overlapped_slabs_equal_align_slab(dev, depth, corun, grid, beside, firs
     _check_overlapped(ov, slabs, ref, depth)
 
 
+@pytest.mark.parametrize("depth,corun,beside", [(2, True, True), (3, True, True), (2, False, False),
+                                                (3, True, False)])
+def test_overlapped_slabs_device_merge(dev, depth, corun, beside):
+    """The consensus merged on the device (device_merge=True: lookup + RANSAC queued behind
+    the vote, no host round trip) gives the same results as align_slab."""
+    cfg = pipeline.AlignConfig(n_kp_global=60)
+    slabs = _gap_slabs(dev)
+    ref = [pipeline.align_slab(s, cfg) for s in slabs]
+    ov = pipeline.OverlappedSlabs(dev, cfg, depth=depth, corun=corun, match_beside=beside, device_merge=True)
+    _check_overlapped(ov, slabs, ref, depth)
+
+
 def test_overlapped_slabs_warp_first(dev):
     """warp(k-1) queued before match(k) (depth 2, match beside): same results."""
     cfg = pipeline.AlignConfig(n_kp_global=60)
@@ -247,15 +259,17 @@ def test_device_lists_follow_the_seed_after_host_list_ransac(dev, caplog):
         p, _, _, _ = oracle.ransac_rigid(kq[f][L], ks.kp_tpl[L], seed=7)
         np.testing.assert_allclose(a7.affines[f], p, rtol=1e-9, atol=1e-9)
     logger = logging.getLogger("test_seed_lists")
-    with caplog.at_level(logging.INFO, logger="test_seed_lists"):
-        ov = pipeline.OverlappedSlabs(dev, cfg42, logger=logger, match_beside=True)
-        got = [r for r in (ov.submit(inp), ov.submit(inp)) if r is not None] + ov.flush()
-        ov.synchronize()
-    low = [r.getMessage() for r in caplog.records if "low keypoint count" in r.getMessage()]
     n_low = int((np.diff(po) < cfg42.n_kp_frame_skip).sum())
-    assert len(got) == 2 and n_low >= 2 and len(low) == 2 * n_low
-    for g in got:
-        assert np.array_equal(g.affines, a42.affines, equal_nan=True)
+    for merge in (False, True):
+        caplog.clear()
+        with caplog.at_level(logging.INFO, logger="test_seed_lists"):
+            ov = pipeline.OverlappedSlabs(dev, cfg42, logger=logger, match_beside=True, device_merge=merge)
+            got = [r for r in (ov.submit(inp), ov.submit(inp)) if r is not None] + ov.flush()
+            ov.synchronize()
+        low = [r.getMessage() for r in caplog.records if "low keypoint count" in r.getMessage()]
+        assert len(got) == 2 and n_low >= 2 and len(low) == 2 * n_low
+        for g in got:
+            assert np.array_equal(g.affines, a42.affines, equal_nan=True)
 
 
 def test_euclidean_min_samples_other_than_two_raises(dev):

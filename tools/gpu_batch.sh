@@ -12,6 +12,9 @@
 #   envbench:<VAR=val>:<cfg>:<tag>  the same with one extra environment variable
 #   cpubench:<cfg>        bench.py --config <cfg> with its CPU baseline -> <out>/<cfg>_cpu.json
 #   profile:<cfg>         tools/profile_round.sh (bench + rocprofv3 summary + warp PMC) -> <out>/<cfg>/
+#   abpmc:<lib>:<cfg>:<tag>  the warp PMC passes (tools/pmc_warp.sh) against another build -> <out>/pmc_<tag>/
+#   trace:<cfg>:<tag>[:<args,comma>]  rocprofv3 --kernel-trace --memory-copy-trace of a short bench
+#                         -> <out>/trace_<tag>/ (read with tools/timeline.py)
 #   lab:<binary>[:<tag>][:<args,comma,separated>]  a lab binary (tools/ or ab/) -> <out>/lab_<tag>.txt
 set -u
 OUT=${1:?out dir}
@@ -55,6 +58,17 @@ for step in "$@"; do
       echo "$a cpu: $(head -c 160 "$OUT/${a}_cpu.json")" ;;
     profile)
       bash tools/profile_round.sh "$OUT/$a" --config "$a" || exit 1 ;;
+    abpmc)
+      KCMC_LIB_PATH="$a" bash tools/pmc_warp.sh "$OUT/pmc_$c" "warp_affine_u16|warp_perspective_u16" --config "$b" \
+        || exit 1 ;;
+    trace)
+      IFS=, read -r -a X <<< "${c:-}"
+      R=$PWD
+      (cd /tmp && export TMPDIR=/tmp && cd "$R" &&
+        timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$R/$OUT/trace_$b" \
+          -o run -- python bench.py --config "$a" --cpu-sample 0 --steps 12 --warmup 3 "${X[@]}" \
+          > "$OUT/trace_$b.json" 2> "$OUT/trace_$b.err") || exit 1
+      echo "trace $a $b: $(head -c 160 "$OUT/trace_$b.json")" ;;
     lab)
       tag=${b:-$(basename "$a")}
       IFS=, read -r -a X <<< "${c:-}"
