@@ -425,7 +425,9 @@ __global__ __launch_bounds__(64) void lookup_order_kernel(
 // replays the insertions).  Outputs: cons [n_kp_global] / votes [n_kp_global] (first nc),
 // meta [2] = (nc, 0 | 1: fewer than n_min voted (AlignmentError, VA:241-244) | 2: invalid
 // votes), pack = iteration order [0, n_kp_global) then the bitmask words.
-constexpr int kMergeThreads = 1024;
+// 256 threads: one wave per SIMD fits in the slot a full warp grid leaves free (7 x 4-wave
+// tiles per CU); a 1024-thread workgroup waited for the warp to drain (c3 trace: 0.42 ms)
+constexpr int kMergeThreads = 256;
 constexpr int kMergeMaxTpl = 4096;
 constexpr int kMergeMaxCons = 1024;
 

@@ -5,11 +5,12 @@
 # Steps (run in order; the batch stops at the first failing step):
 #   probe                 host CPU facts (cpu_count, affinity, cgroup quota) -> <out>/probe.txt
 #   tests[:<-k expr>]     pytest -m gpu (optionally -k) -> <out>/tests.log
+#   envtests:<VAR=val>:<-k expr>  the same -k subset with one extra environment variable
 #   smoke                 __graft_entry__.smoke() -> <out>/smoke.log
 #   bench:<cfg>[:<tag>][:<args,comma,separated>]
 #                         bench.py --config <cfg> --cpu-sample 0 [args] -> <out>/<cfg>_<tag>.json
 #   abbench:<lib>:<cfg>:<tag>  the same against KCMC_LIB_PATH=<lib> (tools/ab_build.py) -> <out>/<cfg>_<tag>.json
-#   envbench:<VAR=val>:<cfg>:<tag>  the same with one extra environment variable
+#   envbench:<VAR=val>:<cfg>:<tag>[:<args,comma>]  the same with one extra environment variable
 #   cpubench:<cfg>        bench.py --config <cfg> with its CPU baseline -> <out>/<cfg>_cpu.json
 #   profile:<cfg>         tools/profile_round.sh (bench + rocprofv3 summary + warp PMC) -> <out>/<cfg>/
 #   abpmc:<lib>:<cfg>:<tag>  the warp PMC passes (tools/pmc_warp.sh) against another build -> <out>/pmc_<tag>/
@@ -21,7 +22,7 @@ OUT=${1:?out dir}
 shift
 mkdir -p "$OUT"
 for step in "$@"; do
-  IFS=: read -r kind a b c <<< "$step"
+  IFS=: read -r kind a b c d <<< "$step"
   case "$kind" in
     probe)
       { python -c "import os; print('cpu_count', os.cpu_count()); print('affinity', len(os.sched_getaffinity(0)))"
@@ -36,6 +37,12 @@ for step in "$@"; do
       rc=$?
       echo "tests rc=$rc" >> "$OUT/tests.log"; tail -3 "$OUT/tests.log"
       [ $rc -eq 0 ] || exit 1 ;;
+    envtests)  # envtests:<VAR=value>:<-k expr>  pytest -m gpu -k <expr> with one extra environment variable
+      env "$a" timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$b" \
+        > "$OUT/tests_env.log" 2>&1
+      rc=$?
+      echo "envtests $a rc=$rc" >> "$OUT/tests_env.log"; tail -3 "$OUT/tests_env.log"
+      [ $rc -eq 0 ] || exit 1 ;;
     smoke)
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit 1
       tail -1 "$OUT/smoke.log" ;;
@@ -49,8 +56,9 @@ for step in "$@"; do
       KCMC_LIB_PATH="$a" timeout -k 10 300 python bench.py --config "$b" --cpu-sample 0 > "$OUT/${b}_$c.json" \
         2>> "$OUT/bench.err" || exit 1
       echo "$b $c ($a): $(head -c 160 "$OUT/${b}_$c.json")" ;;
-    envbench)  # envbench:<VAR=value>:<cfg>:<tag>  the bench with one extra environment variable
-      env "$a" timeout -k 10 300 python bench.py --config "$b" --cpu-sample 0 > "$OUT/${b}_$c.json" \
+    envbench)  # envbench:<VAR=value>:<cfg>:<tag>[:<args,comma>]  the bench with one extra environment variable
+      IFS=, read -r -a X <<< "${d:-}"
+      env "$a" timeout -k 10 300 python bench.py --config "$b" --cpu-sample 0 "${X[@]}" > "$OUT/${b}_$c.json" \
         2>> "$OUT/bench.err" || exit 1
       echo "$b $c ($a): $(head -c 160 "$OUT/${b}_$c.json")" ;;
     cpubench)
