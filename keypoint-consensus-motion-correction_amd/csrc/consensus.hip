@@ -131,7 +131,6 @@ __host__ __device__ inline uint32_t lookup_scratch_words(uint32_t cap) {
 __global__ __launch_bounds__(kVoteThreads) void vote_count_kernel(const uint32_t* __restrict__ keep, int F, int n_tpl,
                                                                   int W, int32_t* __restrict__ cnt,
                                                                   int32_t* __restrict__ first_enc) {
-  KCMC_ANA_PRIO_ENTER();
   const int t = blockIdx.x * kVoteThreads + threadIdx.x;
   if (t >= n_tpl) return;
   const int f0 = blockIdx.y * kVoteChunk, f1 = min(F, f0 + kVoteChunk);
@@ -156,7 +155,6 @@ __global__ __launch_bounds__(kVoteThreads) void vote_count_kernel(const uint32_t
 __global__ __launch_bounds__(kKeyThreads) void vote_key_kernel(const uint32_t* __restrict__ keep, int F, int n_tpl,
                                                                int W, long long frame_base, long long* __restrict__ out,
                                                                int32_t* __restrict__ scratch, uint32_t emu_cap) {
-  KCMC_ANA_PRIO_ENTER();
   extern __shared__ uint32_t lds[];
   int32_t* first = reinterpret_cast<int32_t*>(lds);  // [n_tpl]
   int32_t* count = first + n_tpl;                    // [n_tpl]
@@ -228,7 +226,6 @@ __global__ __launch_bounds__(kKeyThreads) void vote_key_kernel(const uint32_t* _
 __global__ __launch_bounds__(kCountThreads) void lookup_count_kernel(const uint32_t* __restrict__ keep, int F, int W,
                                                                      const uint32_t* __restrict__ cons_bits,
                                                                      int32_t* __restrict__ pt_off) {
-  KCMC_ANA_PRIO_ENTER();
   const int f = blockIdx.x * kCountThreads + threadIdx.x;
   if (f >= F) return;
   const uint32_t* row = keep + (size_t)f * W;
@@ -242,7 +239,6 @@ __global__ __launch_bounds__(kCountThreads) void lookup_count_kernel(const uint3
 // slot as soon as one tile retires, a 1024-thread one waited ~0.43 ms for 16 free slots on
 // one CU (c3 trace).
 __global__ __launch_bounds__(64) void lookup_scan_kernel(int F, int32_t* __restrict__ pt_off) {
-  KCMC_ANA_PRIO_ENTER();
   // 1024 frames per pass, 16 consecutive ones per lane: the 16 loads of a lane are in
   // flight together (a pass per 64 frames waited on one load at a time: ~40 us at F = 2500)
   constexpr int kPer = 16;
@@ -298,7 +294,6 @@ __global__ __launch_bounds__(64) void lookup_order_kernel(
     const uint32_t* __restrict__ keep, int F, int W, const int32_t* __restrict__ cons_iter, int nc_arg,
     const int32_t* __restrict__ nc_dev, const uint32_t* __restrict__ cons_bits, const int32_t* __restrict__ pt_off,
     int32_t* __restrict__ pt_idx, int32_t* __restrict__ scratch, uint32_t cap, int r_lds, int s_lds) {
-  KCMC_ANA_PRIO_ENTER();
   // nc_dev: the consensus size written by consensus_merge_kernel (the launch was sized for
   // nc_arg >= it); cap, r_lds and s_lds follow nc_arg (a table of cap entries holds any set
   // of up to nc_arg keys)
@@ -446,7 +441,6 @@ __global__ __launch_bounds__(kMergeThreads) void consensus_merge_kernel(
     const long long* __restrict__ votes, int world, int n_tpl, int n_kp_global, int n_min,
     int32_t* __restrict__ out_cons, int32_t* __restrict__ out_votes, int32_t* __restrict__ meta,
     int32_t* __restrict__ pack) {
-  KCMC_ANA_PRIO_ENTER();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int P = merge_sort_slots(n_tpl);
   long long* sc = reinterpret_cast<long long*>(smem);   // [P] counts (-1: padding)

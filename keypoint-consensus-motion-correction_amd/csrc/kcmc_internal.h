@@ -12,16 +12,6 @@
 
 #include "../../include/kcmc.h"
 
-// Wave priority of the analysis kernels (match, consensus, RANSAC) that run beside the warp
-// in the pipelined schedule: s_setprio(KCMC_ANA_PRIO) at kernel start (0: the default
-// arbitration by age).  A/B knob (tools/ab_build.py KCMC_AB_FLAGS=-DKCMC_ANA_PRIO=3).
-#ifndef KCMC_ANA_PRIO
-#define KCMC_ANA_PRIO 0
-#endif
-#define KCMC_ANA_PRIO_ENTER()                                      \
-  do {                                                             \
-    if constexpr (KCMC_ANA_PRIO > 0) __builtin_amdgcn_s_setprio(KCMC_ANA_PRIO); \
-  } while (0)
 
 // Hypothesis tables of the min_samples-point models (3: affine, 4: projective): per
 // point count n, `trials` samples packed as four 16-bit indices in a u64 (unused slots

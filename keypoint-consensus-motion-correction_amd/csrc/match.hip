@@ -204,7 +204,6 @@ __global__ __launch_bounds__(KnnShape<WAVES>::kThreads) void knn2_l2u8_kernel(
     const uint8_t* __restrict__ des_tpl, int n_tpl, int D, const uint8_t* __restrict__ des_q,
     const int32_t* __restrict__ q_off, int n_frames, int n_tg, int32_t* __restrict__ out_idx,
     float* __restrict__ out_dist) {
-  KCMC_ANA_PRIO_ENTER();
   constexpr int KSTEPS = DP / 32;
   constexpr int ROWB = DP + 16;  // padded LDS row stride (bytes)
   // double-buffered chunks: one barrier per chunk (a wave writes chunk c + 1 only after
@@ -366,7 +365,6 @@ __global__ __launch_bounds__(kFilterThreads) void match_filter_kernel(
     const double* __restrict__ kp_q, const int32_t* __restrict__ q_off, int n_tpl, double ratio,
     double d_lo, double d_hi, double* __restrict__ kp_ordered, uint32_t* __restrict__ keep_bits,
     int32_t* __restrict__ counts) {
-  KCMC_ANA_PRIO_ENTER();
   extern __shared__ __attribute__((aligned(16))) double sdisp[];  // [pow2 >= n_tpl]
   __shared__ int s_nratio;
   __shared__ int s_ndist;
@@ -478,7 +476,6 @@ __global__ __launch_bounds__(64 * kFilterWaveFrames) void match_filter_wave_kern
     const double* __restrict__ kp_q, const int32_t* __restrict__ q_off, int n_frames, int n_tpl, double ratio,
     double d_lo, double d_hi, double* __restrict__ kp_ordered, uint32_t* __restrict__ keep_bits,
     int32_t* __restrict__ counts) {
-  KCMC_ANA_PRIO_ENTER();
   const int lane = threadIdx.x & 63;
   const int f = blockIdx.x * kFilterWaveFrames + (threadIdx.x >> 6);
   if (f >= n_frames) return;  // the whole wave
@@ -586,7 +583,6 @@ __global__ __launch_bounds__(kFilterWgThreads) void match_filter_wg_kernel(
     const int32_t* __restrict__ idx, const float* __restrict__ dist, const double* __restrict__ kp_tpl,
     const double* __restrict__ kp_q, const int32_t* __restrict__ q_off, int n_tpl, double ratio, double d_lo,
     double d_hi, double* __restrict__ kp_ordered, uint32_t* __restrict__ keep_bits, int32_t* __restrict__ counts) {
-  KCMC_ANA_PRIO_ENTER();
   __shared__ double sx[kFilterWgThreads * 8];
   __shared__ int s_cnt[kFilterWgThreads / 64];
   __shared__ double s_med[2];

@@ -432,7 +432,6 @@ __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
     const int32_t* __restrict__ hyp_off, int hyp_off_len,
     int T, double thresh, double tq, double rate, int n_skip, double* __restrict__ out_params,
     uint8_t* __restrict__ out_inl, int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
-  KCMC_ANA_PRIO_ENTER();
   for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
     ransac_rigid_frame<LARGE>(f, src, dst, pt_idx, pt_off, src_stride, hyp, hyp_off, hyp_off_len, T, thresh, tq, rate,
                               n_skip, out_params, out_inl, out_nin, out_best);

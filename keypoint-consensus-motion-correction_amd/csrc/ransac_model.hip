@@ -806,14 +806,21 @@ __device__ __forceinline__ void smallest_eigvec(const double (&A)[n][n], double 
 }
 
 // Workgroup g scores frames g, g + grid, ... (kcmc_set_ransac_grid; default one per frame).
+// KCMC_RANSAC_WAVES (A/B knob): waves per SIMD the register budget must allow, e.g. 5
+// (<= 102 VGPRs) fits the 120 a CU full of warp tiles leaves (7 x 56 of 512), so the
+// scoring can start beside the warp instead of waiting for tiles to retire.
+#ifdef KCMC_RANSAC_WAVES
+#define KCMC_RANSAC_VGPR_ATTR __attribute__((amdgpu_waves_per_eu(KCMC_RANSAC_WAVES)))
+#else
+#define KCMC_RANSAC_VGPR_ATTR
+#endif
 template <int MODEL, bool LARGE>
-__global__ __launch_bounds__(kThreads) void ransac_model_score_kernel(
+__global__ __launch_bounds__(kThreads) KCMC_RANSAC_VGPR_ATTR void ransac_model_score_kernel(
     int n_frames, const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint64_t* __restrict__ hyp,
     const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, double tq, int n_skip,
     double* out_params, double* best_model, uint8_t* __restrict__ out_inl,
     int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
-  KCMC_ANA_PRIO_ENTER();
   for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
     ransac_model_score_frame<MODEL, LARGE>(f, src, dst, pt_idx, pt_off, src_stride, hyp, hyp_off, hyp_off_len, T,
                                            thresh, tq, n_skip, out_params, best_model, out_inl, out_nin, out_best);
@@ -827,7 +834,6 @@ __global__ __launch_bounds__(256) void ransac_model_refit_kernel(
     const int32_t* __restrict__ pt_off, int src_stride, const uint8_t* __restrict__ inl,
     const int32_t* __restrict__ nin, const double* best_model, int n_frames, double rate,
     double* out_params) {
-  KCMC_ANA_PRIO_ENTER();
   constexpr int n = MODEL == KCMC_MODEL_AFFINE ? 7 : 9;
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;

@@ -4,7 +4,7 @@
 #   bash tools/gpu_batch.sh <out_dir> <step> [<step> ...]
 # Steps (run in order; the batch stops at the first failing step):
 #   probe                 host CPU facts (cpu_count, affinity, cgroup quota) -> <out>/probe.txt
-#   tests[:<-k expr>]     pytest -m gpu (optionally -k) -> <out>/tests.log
+#   tests[:<-k expr>]     pytest -m gpu (optionally -k; "+" stands for " or ") -> <out>/tests.log
 #   envtests:<VAR=val>:<-k expr>  the same -k subset with one extra environment variable
 #   smoke                 __graft_entry__.smoke() -> <out>/smoke.log
 #   bench:<cfg>[:<tag>][:<args,comma,separated>]
@@ -31,14 +31,14 @@ for step in "$@"; do
       cat "$OUT/probe.txt" ;;
     tests)
       K=()
-      [ -n "${a:-}" ] && K=(-k "$a")
+      [ -n "${a:-}" ] && K=(-k "${a//+/ or }")  # tests:a+b = -k "a or b"
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread "${K[@]}" \
         > "$OUT/tests.log" 2>&1
       rc=$?
       echo "tests rc=$rc" >> "$OUT/tests.log"; tail -3 "$OUT/tests.log"
       [ $rc -eq 0 ] || exit 1 ;;
     envtests)  # envtests:<VAR=value>:<-k expr>  pytest -m gpu -k <expr> with one extra environment variable
-      env "$a" timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$b" \
+      env "$a" timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "${b//+/ or }" \
         > "$OUT/tests_env.log" 2>&1
       rc=$?
       echo "envtests $a rc=$rc" >> "$OUT/tests_env.log"; tail -3 "$OUT/tests_env.log"
