@@ -408,7 +408,7 @@ class OverlappedSlabs:
                  counts: Optional[List[int]] = None, group=None, depth: int = 2, corun: bool = True,
                  ransac_grid: Optional[int] = None, match_beside: bool = False, fit_first: bool = False,
                  ana_cus_per_se: int = 0, warp_exclusive: bool = True, warp_first: bool = False,
-                 device_merge: bool = False, early_match: bool = False):
+                 device_merge: bool = False):
         if depth not in (2, 3):
             raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
         if match_beside and not corun:
@@ -434,14 +434,6 @@ class OverlappedSlabs:
         # analysis stream's path (its votes were ready a step earlier), so the merge kernel
         # only adds work there (c3 2.98-2.99 M vs 3.03-3.04 M frames/s, c2 607 k vs 622 k)
         self.device_merge = bool(device_merge)
-        # early_match (depth 2, match_beside): match(k) + vote(k) on a third stream that
-        # waits for warp(k-2) to end instead of queueing behind lookup + RANSAC(k-1), so the
-        # next slab's persistent knn2 fills the CUs while RANSAC(k-1) finishes its tail and
-        # the host queues warp(k-1) (the default order runs knn2 alone between RANSAC and
-        # the warp: c3 trace, 0.13 ms of a 0.83 ms step)
-        self.early_match = bool(early_match)
-        if self.early_match and not (match_beside and depth == 2):
-            raise ValueError("early_match needs depth=2 and match_beside=True")
         if counts is not None and len(counts) > 1 and cfg.frame_downsample_rate != 1:
             # the rank's first frame is counted in sample frames, the affines in full-rate
             # frames: the same restriction as distributed.align_sharded
@@ -474,9 +466,6 @@ class OverlappedSlabs:
         self._hs = self.stream.cuda_stream
         self._hc = self.copy.cuda_stream
         self._ha = self.ana.cuda_stream if self.corun else self._hs
-        self.mstream = torch.cuda.Stream(self.dev) if self.early_match else self.ana  # the match's stream
-        self._hm = self.mstream.cuda_stream if self.mstream is not None else self._hs
-        self._warp_done: Optional[torch.cuda.Event] = None  # after the last warp queued (early_match)
         # RANSAC beside the warp on at most this many workgroups (each walks its share of
         # the frames; 0 / None = one per frame).  Same-box A/B at c2:
         # 128, 256 or 512 workgroups were no faster than one per frame, so the default
@@ -623,7 +612,7 @@ class OverlappedSlabs:
         ev.record(cur)
         self.stream.wait_event(ev)
         if self.match_beside:  # the analysis stream reads the slab's keypoints
-            self.mstream.wait_event(ev)
+            self.ana.wait_event(ev)
         self._queued()
 
     def _match(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
@@ -659,30 +648,27 @@ class OverlappedSlabs:
         """match(k) and its vote on the analysis stream (allocated there), ahead of the lookup +
         RANSAC of the previous slab; the (gathered) votes to the host."""
         n_tpl = inp.des_tpl.shape[0]
-        ms, hm = self.mstream, self._hm
-        with torch.cuda.stream(ms):
-            if self.early_match and self._warp_done is not None:
-                ms.wait_event(self._warp_done)  # start when warp(k-2) has left the CUs
+        with torch.cuda.stream(self.ana):
             # the match reads the slab's descriptors / keypoints on the analysis stream: keep
             # their memory from being reused by the caller's stream until it has
             for t in (inp.des_tpl, inp.kp_tpl, inp.des_q, inp.kp_q, inp.q_off):
-                t.record_stream(ms)
+                t.record_stream(self.ana)
             m0 = torch.cuda.Event(enable_timing=True)
-            m0.record(ms)
+            m0.record(self.ana)
             mark("m0", m0)
-            match = match_stage(inp, self.cfg, stream=hm)
-            votes = stages.consensus_vote(match.keep_bits, n_tpl, self._f0, stream=hm)
+            match = match_stage(inp, self.cfg, stream=self._ha)
+            votes = stages.consensus_vote(match.keep_bits, n_tpl, self._f0, stream=self._ha)
             matched = torch.cuda.Event(enable_timing=True)
-            matched.record(ms)
+            matched.record(self.ana)
             mark("m1", matched)
             if self._sharded():
                 votes = self._gather(votes)  # the analysis stream waits for the collective
             dch = None
             if self._use_device_merge(n_tpl):
                 dch = stages.consensus_merge_device(votes, n_tpl, self.cfg.n_kp_global, self.cfg.n_kp_global_min,
-                                                    stream=hm)
+                                                    stream=self._ha)
             ready = torch.cuda.Event()
-            ready.record(ms)
+            ready.record(self.ana)
         slot = self._slots.pop() if self._slots else _Slot()
         if dch is not None:
             return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=ready, dchoice=dch)
@@ -731,7 +717,7 @@ class OverlappedSlabs:
         d = p.dchoice
         if self.corun:
             with torch.cuda.stream(self.ana):
-                if not self.match_beside or self.early_match:
+                if not self.match_beside:
                     self.ana.wait_event(p.matched)
                 for t in (p.match.kp_ordered, p.match.keep_bits, p.inp.kp_tpl, d.cons, d.votes, d.meta, d.pack):
                     t.record_stream(self.ana)
@@ -791,7 +777,7 @@ class OverlappedSlabs:
         self._at_tail(mark, "w0")
         p.aligned = warp_frames(p.inp.frames, p.rr.params, out=p.out, stream=self._hs)
         self._queued()
-        self._warp_done = self._at_tail(mark, "w1")
+        self._at_tail(mark, "w1")
 
     def _finish(self, p: _SlabInFlight, mark) -> SlabResult:
         """Host post-processing of slab p (VA:143-145) and the warps that need its maps."""
@@ -869,8 +855,6 @@ class OverlappedSlabs:
         self.stream.synchronize()
         if self.ana is not None:
             self.ana.synchronize()
-        if self.mstream is not None:
-            self.mstream.synchronize()
         self.copy.synchronize()
 
 

@@ -160,23 +160,6 @@ def test_overlapped_slabs_device_merge(dev, depth, corun, beside):
     _check_overlapped(ov, slabs, ref, depth)
 
 
-@pytest.mark.parametrize("merge", [False, True])
-def test_overlapped_slabs_early_match(dev, merge):
-    """match(k) on a third stream gated by the end of warp(k-2) (depth 2, match beside),
-    with the host or the device consensus merge: same results as align_slab."""
-    cfg = pipeline.AlignConfig(n_kp_global=60)
-    slabs = _gap_slabs(dev)
-    ref = [pipeline.align_slab(s, cfg) for s in slabs]
-    ov = pipeline.OverlappedSlabs(dev, cfg, match_beside=True, early_match=True, device_merge=merge)
-    _check_overlapped(ov, slabs, ref, 2)
-
-
-def test_early_match_needs_depth_two_beside():
-    with pytest.raises(ValueError, match="early_match"):
-        pipeline.OverlappedSlabs("cpu", pipeline.AlignConfig(n_kp_global=60), depth=3, match_beside=True,
-                                  early_match=True)
-
-
 def test_overlapped_slabs_warp_first(dev):
     """warp(k-1) queued before match(k) (depth 2, match beside): same results."""
     cfg = pipeline.AlignConfig(n_kp_global=60)
