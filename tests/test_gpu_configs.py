@@ -105,7 +105,13 @@ def _check_slab(dev, *, F, H, W, C, n_tpl, D, model, n_kp_global, descriptor="u8
     out = res.aligned.cpu().numpy()
     warp = oracle.warp_perspective_u16 if model == "projective" else oracle.warp_affine_u16
     for f in (range(F) if warp_frames is None else warp_frames):
-        assert np.array_equal(out[f], warp(base, res.affines[f])), f
+        ref = warp(base, res.affines[f])
+        bad = np.argwhere(out[f] != ref)
+        # on a mismatch: where (the first positions, the values) and whether a second read
+        # of the device buffer agrees with the first
+        assert len(bad) == 0, (f, len(bad), bad[:16].tolist(), out[f][tuple(bad[:16].T)].tolist(),
+                               ref[tuple(bad[:16].T)].tolist(),
+                               bool(np.array_equal(res.aligned[f].cpu().numpy(), out[f])))
     return res, ks
 
 
