@@ -17,6 +17,7 @@
 #   trace:<cfg>:<tag>[:<args,comma>]  rocprofv3 --kernel-trace --memory-copy-trace of a short bench
 #                         -> <out>/trace_<tag>/ (read with tools/timeline.py)
 #   lab:<binary>[:<tag>][:<args,comma,separated>]  a lab binary (tools/ or ab/) -> <out>/lab_<tag>.txt
+#   envlab:<VAR=val>:<binary>:<tag>[:<args,comma>]  the same with one extra environment variable
 set -u
 OUT=${1:?out dir}
 shift
@@ -77,6 +78,10 @@ for step in "$@"; do
           -o run -- python bench.py --config "$a" --cpu-sample 0 --steps 12 --warmup 3 "${X[@]}" \
           > "$OUT/trace_$b.json" 2> "$OUT/trace_$b.err") || exit 1
       echo "trace $a $b: $(head -c 160 "$OUT/trace_$b.json")" ;;
+    envlab)  # envlab:<VAR=value>:<binary>:<tag>[:<args,comma>]  a lab with one extra environment variable
+      IFS=, read -r -a X <<< "${d:-}"
+      env "$a" timeout -k 10 240 "$b" "${X[@]}" > "$OUT/lab_$c.txt" 2>&1 || exit 1
+      tail -4 "$OUT/lab_$c.txt" ;;
     lab)
       tag=${b:-$(basename "$a")}
       IFS=, read -r -a X <<< "${c:-}"
