@@ -149,6 +149,24 @@ int kcmc_match_frames_f32(kcmc_ctx* ctx, const float* des_tpl_dev, const double*
                           double d_lo, double d_hi, int32_t* out_idx_dev, float* out_dist_dev,
                           double* out_kp_ordered_dev, uint32_t* out_keep_bits_dev,
                           int32_t* out_counts_dev, kcmc_stream_t stream);
+/* The same match in two parts, so the first can run on another stream ahead of the
+ * second (OverlappedSlabs early_prep: beside the previous slab's warp).
+ * kcmc_match_f32_prepare: the template statistics and the frames' fp16 tile images into
+ * prep_dev (device, 256-byte aligned, kcmc_match_f32_prep_bytes(n_tpl, n_frames, max_nq)
+ * bytes; -1 for negative sizes); kcmc_match_frames_f32_prepared: kcmc_match_frames_f32 on
+ * a prepared prep_dev (same des_tpl / des_q / q_off; ordered after the prepare by the
+ * caller).  Results identical to kcmc_match_frames_f32. */
+long long kcmc_match_f32_prep_bytes(int n_tpl, int n_frames, int max_nq);
+int kcmc_match_f32_prepare(kcmc_ctx* ctx, const float* des_tpl_dev, int n_tpl, int D, const float* des_q_dev,
+                           const int32_t* q_off_dev, int n_frames, int max_nq, void* prep_dev,
+                           long long prep_bytes, kcmc_stream_t stream);
+int kcmc_match_frames_f32_prepared(kcmc_ctx* ctx, const float* des_tpl_dev, const double* kp_tpl_dev,
+                                   int n_tpl, int D, const float* des_q_dev, const double* kp_q_dev,
+                                   const int32_t* q_off_dev, int n_frames, int max_nq, const void* prep_dev,
+                                   double ratio, double d_lo, double d_hi, int32_t* out_idx_dev,
+                                   float* out_dist_dev, double* out_kp_ordered_dev,
+                                   uint32_t* out_keep_bits_dev, int32_t* out_counts_dev,
+                                   kcmc_stream_t stream);
 
 /* ------------------------------------------------------- host: keypoint consensus
  * VA:224-286 on the host, reproducing CPython 3 set/Counter iteration order exactly:

@@ -33,6 +33,9 @@ EXPORTED_SYMBOLS = (
     "kcmc_match_frames",
     "kcmc_knn2_l2f32",
     "kcmc_match_frames_f32",
+    "kcmc_match_f32_prep_bytes",
+    "kcmc_match_f32_prepare",
+    "kcmc_match_frames_f32_prepared",
     "kcmc_knn2_hamming",
     "kcmc_match_frames_hamming",
     "kcmc_consensus",
@@ -101,6 +104,9 @@ _SIGNATURES = {
     "kcmc_match_frames": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
     "kcmc_knn2_l2f32": ([P, P, I, I, P, P, I, I, P, P, P], I),
     "kcmc_match_frames_f32": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
+    "kcmc_match_f32_prep_bytes": ([I, I, I], LL),
+    "kcmc_match_f32_prepare": ([P, P, I, I, P, P, I, I, P, LL, P], I),
+    "kcmc_match_frames_f32_prepared": ([P, P, P, I, I, P, P, P, I, I, P, D, D, D, P, P, P, P, P, P], I),
     "kcmc_knn2_hamming": ([P, P, I, I, P, P, I, I, P, P, P], I),
     "kcmc_match_frames_hamming": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
     "kcmc_consensus": ([P, I, I, I, I, P, P, P, P, P], I),

@@ -783,50 +783,75 @@ int check_f32_args(const void* des_tpl, int n_tpl, int D, const void* des_q, con
   return KCMC_OK;
 }
 
-int launch_knn_f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const float* des_q, const int32_t* q_off,
-                   int n_frames, int max_nq, int32_t* out_idx, float* out_dist, hipStream_t s) {
-  if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
-  // workspace: per-frame fallback counters, the listed frames (count + ids) and the lists
-  // (room for every template row), the template stats, the frames' max |b|^2 / max beta /
-  // bad flags, then the tile images (tpf = ceil(max_nq / 64) per frame; the CSR total is a
-  // device value) and the fallback merge keys (set by the matcher when it lists a row)
+// Layout of the two work areas of a float match.  The prepared part (template stats,
+// the frames' max |b|^2 / max beta / bad flags, then the tile images: tpf = ceil(max_nq /
+// 64) per frame; the CSR total is a device value) can be filled ahead of the match on
+// another stream (kcmc_match_f32_prepare); the run part holds the per-frame fallback
+// counters, the listed frames (count + ids) and lists (room for every template row) and
+// the fallback merge keys (set by the matcher when it lists a row).
+struct F32Layout {
+  int tpf = 0, key_bits = 0;
+  size_t stat_bytes = 0, img_bytes = 0, cnt_bytes = 0, fb_bytes = 0, key_bytes = 0;
+  size_t prep_bytes() const { return stat_bytes + img_bytes; }
+  size_t run_bytes() const { return cnt_bytes + fb_bytes + key_bytes; }
+};
+
+F32Layout f32_layout(int n_tpl, int n_frames, int max_nq) {
+  F32Layout L;
   const size_t rows = (size_t)n_frames * n_tpl;
-  const int tpf = ceil_div(max(max_nq, 0), kTile);
+  L.tpf = ceil_div(max(max_nq, 0), kTile);
   int tbits = 0;
-  while ((1 << tbits) < tpf) ++tbits;
-  const int key_bits = 5 + tbits;  // (tile << 5 | half << 4 | register)
-  if (key_bits > 20) return fail(KCMC_EUNSUPPORTED, "match_f32: more than 2^21 descriptors in one frame");
-  const size_t cnt_bytes = ((2 * (size_t)n_frames + 1) * sizeof(int32_t) + 255) & ~(size_t)255;
-  const size_t fb_bytes = (rows * sizeof(int32_t) + 255) & ~(size_t)255;
-  const size_t stat_bytes = (256 + 3 * (size_t)n_frames * sizeof(float) + 255) & ~(size_t)255;
-  const size_t img_bytes = (size_t)n_frames * tpf * kImgBytes;
-  const size_t key_bytes = rows * 2 * sizeof(unsigned long long);  // the fallback's merged top-2 keys
-  void* ws = nullptr;
-  KCMC_TRY(workspace_alloc(ctx, &ws, cnt_bytes + fb_bytes + stat_bytes + img_bytes + key_bytes, s));
-  char* w = static_cast<char*>(ws);
-  int32_t* fb_cnt = reinterpret_cast<int32_t*>(w);
-  int32_t* fb = reinterpret_cast<int32_t*>(w + cnt_bytes);
-  unsigned* Kst = reinterpret_cast<unsigned*>(w + cnt_bytes + fb_bytes);
-  unsigned* fmax = reinterpret_cast<unsigned*>(w + cnt_bytes + fb_bytes + 256);  // max |b|^2, max beta, bad flag
+  while ((1 << tbits) < L.tpf) ++tbits;
+  L.key_bits = 5 + tbits;  // (tile << 5 | half << 4 | register)
+  L.stat_bytes = (256 + 3 * (size_t)n_frames * sizeof(float) + 255) & ~(size_t)255;
+  L.img_bytes = (size_t)n_frames * L.tpf * kImgBytes;
+  L.cnt_bytes = ((2 * (size_t)n_frames + 1) * sizeof(int32_t) + 255) & ~(size_t)255;
+  L.fb_bytes = (rows * sizeof(int32_t) + 255) & ~(size_t)255;
+  L.key_bytes = rows * 2 * sizeof(unsigned long long);
+  return L;
+}
+
+// The prepared part: template stats, then the frames' tile images and stats.
+int launch_f32_prepare(const F32Layout& L, const float* des_tpl, int n_tpl, int D, const float* des_q,
+                       const int32_t* q_off, int n_frames, void* prep, hipStream_t s) {
+  char* w = static_cast<char*>(prep);
+  unsigned* Kst = reinterpret_cast<unsigned*>(w);
+  unsigned* fmax = reinterpret_cast<unsigned*>(w + 256);  // max |b|^2, max beta, bad flag
   unsigned* fbeta = fmax + n_frames;
   int32_t* fbad = reinterpret_cast<int32_t*>(fbeta + n_frames);
-  uint8_t* img = reinterpret_cast<uint8_t*>(w + cnt_bytes + fb_bytes + stat_bytes);
-  unsigned long long* fb_keys = reinterpret_cast<unsigned long long*>(w + cnt_bytes + fb_bytes + stat_bytes + img_bytes);
-  int32_t* fb_frames = fb_cnt + n_frames;
-  KCMC_TRY(hip_check(hipMemsetAsync(fb_cnt, 0, (size_t)(n_frames + 1) * sizeof(int32_t), s), "hipMemsetAsync"));
-  KCMC_TRY(hip_check(hipMemsetAsync(Kst, 0, stat_bytes, s), "hipMemsetAsync"));
+  uint8_t* img = reinterpret_cast<uint8_t*>(w + L.stat_bytes);
+  KCMC_TRY(hip_check(hipMemsetAsync(Kst, 0, L.stat_bytes, s), "hipMemsetAsync"));
   hipLaunchKernelGGL(tpl_stats_kernel, dim3(ceil_div(n_tpl, kTplRowsPerWG)), dim3(256), 0, s, des_tpl, n_tpl, D, Kst);
   KCMC_TRY(launch_check("tpl_stats_kernel"));
   hipLaunchKernelGGL(tpl_err_kernel, dim3(ceil_div(n_tpl, kTplRowsPerWG)), dim3(256), 0, s, des_tpl, n_tpl, D, Kst);
   KCMC_TRY(launch_check("tpl_err_kernel"));
-  if (tpf > 0) {
-    hipLaunchKernelGGL(frame_images_kernel, dim3(tpf, n_frames), dim3(kImgThreads), 0, s, des_q, D, q_off, tpf, Kst,
-                       img, fmax, fbeta, fbad);
+  if (L.tpf > 0) {
+    hipLaunchKernelGGL(frame_images_kernel, dim3(L.tpf, n_frames), dim3(kImgThreads), 0, s, des_q, D, q_off, L.tpf,
+                       Kst, img, fmax, fbeta, fbad);
     KCMC_TRY(launch_check("frame_images_kernel"));
   }
+  return KCMC_OK;
+}
+
+// The matcher and its exact fallback on a prepared part.
+int launch_f32_run(const F32Layout& L, const float* des_tpl, int n_tpl, int D, const float* des_q,
+                   const int32_t* q_off, int n_frames, const void* prep, void* run, int32_t* out_idx, float* out_dist,
+                   hipStream_t s) {
+  const char* w = static_cast<const char*>(prep);
+  const unsigned* Kst = reinterpret_cast<const unsigned*>(w);
+  const unsigned* fmax = reinterpret_cast<const unsigned*>(w + 256);
+  const unsigned* fbeta = fmax + n_frames;
+  const int32_t* fbad = reinterpret_cast<const int32_t*>(fbeta + n_frames);
+  const uint8_t* img = reinterpret_cast<const uint8_t*>(w + L.stat_bytes);
+  char* r = static_cast<char*>(run);
+  int32_t* fb_cnt = reinterpret_cast<int32_t*>(r);
+  int32_t* fb = reinterpret_cast<int32_t*>(r + L.cnt_bytes);
+  unsigned long long* fb_keys = reinterpret_cast<unsigned long long*>(r + L.cnt_bytes + L.fb_bytes);
+  int32_t* fb_frames = fb_cnt + n_frames;
+  KCMC_TRY(hip_check(hipMemsetAsync(fb_cnt, 0, (size_t)(n_frames + 1) * sizeof(int32_t), s), "hipMemsetAsync"));
   hipLaunchKernelGGL(knn2_l2f32_kernel, dim3(ceil_div(n_tpl, kTplPerWG), n_frames), dim3(kThreads), 0, s, des_tpl,
-                     n_tpl, D, des_q, q_off, img, tpf, Kst, reinterpret_cast<const float*>(fmax),
-                     reinterpret_cast<const float*>(fbeta), fbad, key_bits, out_idx, out_dist, fb, fb_cnt, fb_frames,
+                     n_tpl, D, des_q, q_off, img, L.tpf, Kst, reinterpret_cast<const float*>(fmax),
+                     reinterpret_cast<const float*>(fbeta), fbad, L.key_bits, out_idx, out_dist, fb, fb_cnt, fb_frames,
                      fb_keys);
   KCMC_TRY(launch_check("knn2_l2f32_kernel"));
   const int fb_grid = min(n_frames * kFbSplit * kFbLanes, 4 * device_cus());
@@ -835,8 +860,33 @@ int launch_knn_f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const 
   KCMC_TRY(launch_check("knn2_l2f32_fallback_kernel"));
   hipLaunchKernelGGL(knn2_l2f32_fallback_out_kernel, dim3(min(n_frames, 1024)), dim3(256), 0, s, n_tpl, fb, fb_cnt,
                      fb_frames, fb_keys, out_idx, out_dist);
-  KCMC_TRY(launch_check("knn2_l2f32_fallback_out_kernel"));
-  return workspace_free(ctx, ws, s);
+  return launch_check("knn2_l2f32_fallback_out_kernel");
+}
+
+int f32_layout_check(const F32Layout& L) {
+  if (L.key_bits > 20) return fail(KCMC_EUNSUPPORTED, "match_f32: more than 2^21 descriptors in one frame");
+  return KCMC_OK;
+}
+
+// prep: a prepared part (kcmc_match_f32_prepare) or nullptr (prepared here, in the same
+// stream-ordered workspace as the run part).
+int launch_knn_f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const float* des_q, const int32_t* q_off,
+                   int n_frames, int max_nq, const void* prep, int32_t* out_idx, float* out_dist, hipStream_t s) {
+  if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
+  const F32Layout L = f32_layout(n_tpl, n_frames, max_nq);
+  KCMC_TRY(f32_layout_check(L));
+  const size_t own = prep ? 0 : L.prep_bytes();
+  void* ws = nullptr;
+  KCMC_TRY(workspace_alloc(ctx, &ws, own + L.run_bytes(), s));
+  char* w = static_cast<char*>(ws);
+  int rc = KCMC_OK;
+  if (!prep) {
+    rc = launch_f32_prepare(L, des_tpl, n_tpl, D, des_q, q_off, n_frames, w, s);
+    prep = w;
+  }
+  if (rc == KCMC_OK) rc = launch_f32_run(L, des_tpl, n_tpl, D, des_q, q_off, n_frames, prep, w + own, out_idx, out_dist, s);
+  const int rf = workspace_free(ctx, ws, s);
+  return rc != KCMC_OK ? rc : rf;
 }
 
 }  // namespace
@@ -849,8 +899,28 @@ extern "C" int kcmc_knn2_l2f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, i
                                kcmc_stream_t stream) {
   if (!ctx) return fail(KCMC_EINVAL, "kcmc_knn2_l2f32: ctx is NULL");
   KCMC_TRY(check_f32_args(des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, out_idx, out_dist));
-  return launch_knn_f32(ctx, des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, out_idx, out_dist,
+  return launch_knn_f32(ctx, des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, nullptr, out_idx, out_dist,
                         (hipStream_t)stream);
+}
+
+extern "C" long long kcmc_match_f32_prep_bytes(int n_tpl, int n_frames, int max_nq) {
+  if (n_tpl < 0 || n_frames < 0 || max_nq < 0) return -1;
+  return (long long)f32_layout(n_tpl, n_frames, max_nq).prep_bytes();
+}
+
+extern "C" int kcmc_match_f32_prepare(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const float* des_q,
+                                      const int32_t* q_off, int n_frames, int max_nq, void* prep_dev,
+                                      long long prep_bytes, kcmc_stream_t stream) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_match_f32_prepare: ctx is NULL");
+  int32_t dummy_i = 0;
+  float dummy_f = 0.f;
+  KCMC_TRY(check_f32_args(des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, &dummy_i, &dummy_f));
+  if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
+  const F32Layout L = f32_layout(n_tpl, n_frames, max_nq);
+  KCMC_TRY(f32_layout_check(L));
+  if (!prep_dev || prep_bytes < (long long)L.prep_bytes())
+    return fail(KCMC_EINVAL, "kcmc_match_f32_prepare: prep_dev must hold kcmc_match_f32_prep_bytes bytes");
+  return launch_f32_prepare(L, des_tpl, n_tpl, D, des_q, q_off, n_frames, prep_dev, (hipStream_t)stream);
 }
 
 extern "C" int kcmc_match_frames_f32(kcmc_ctx* ctx, const float* des_tpl, const double* kp_tpl, int n_tpl, int D,
@@ -865,7 +935,26 @@ extern "C" int kcmc_match_frames_f32(kcmc_ctx* ctx, const float* des_tpl, const 
   if (n_tpl > 8192) return fail(KCMC_EUNSUPPORTED, "kcmc_match_frames_f32: n_tpl > 8192");
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
   hipStream_t s = (hipStream_t)stream;
-  KCMC_TRY(launch_knn_f32(ctx, des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, out_idx, out_dist, s));
+  KCMC_TRY(launch_knn_f32(ctx, des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, nullptr, out_idx, out_dist, s));
+  return launch_match_filter(out_idx, out_dist, kp_tpl, kp_q, q_off, n_frames, n_tpl, ratio, d_lo, d_hi,
+                             out_kp_ordered, out_keep_bits, out_counts, s);
+}
+
+extern "C" int kcmc_match_frames_f32_prepared(kcmc_ctx* ctx, const float* des_tpl, const double* kp_tpl, int n_tpl,
+                                              int D, const float* des_q, const double* kp_q, const int32_t* q_off,
+                                              int n_frames, int max_nq, const void* prep_dev, double ratio,
+                                              double d_lo, double d_hi, int32_t* out_idx, float* out_dist,
+                                              double* out_kp_ordered, uint32_t* out_keep_bits, int32_t* out_counts,
+                                              kcmc_stream_t stream) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_match_frames_f32_prepared: ctx is NULL");
+  KCMC_TRY(check_f32_args(des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, out_idx, out_dist));
+  if (n_frames > 0 && n_tpl > 0 && (!kp_tpl || !out_kp_ordered || !out_keep_bits || !out_counts || !prep_dev ||
+                                    (max_nq > 0 && !kp_q)))
+    return fail(KCMC_EINVAL, "kcmc_match_frames_f32_prepared: NULL pointer");
+  if (n_tpl > 8192) return fail(KCMC_EUNSUPPORTED, "kcmc_match_frames_f32_prepared: n_tpl > 8192");
+  if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
+  hipStream_t s = (hipStream_t)stream;
+  KCMC_TRY(launch_knn_f32(ctx, des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, prep_dev, out_idx, out_dist, s));
   return launch_match_filter(out_idx, out_dist, kp_tpl, kp_q, q_off, n_frames, n_tpl, ratio, d_lo, d_hi,
                              out_kp_ordered, out_keep_bits, out_counts, s);
 }

@@ -58,6 +58,13 @@ using BlockCfg = WarpCfg<56, 10240, 9>;  // 20 KB box, box rows <= 72 (7 workgro
 // to ~2.5 deg; larger rotations take the general staged path or the direct gather).
 using Block64Cfg = WarpCfg<64, 10240, 9>;
 
+// Extra LDS elements per one-channel affine workgroup (A/B knob): 20 KB boxes fit 8
+// workgroups = every wave slot of a CU; a pad of 512 (21 KB) caps them at 7 and leaves one
+// wave slot per SIMD to the kernels beside the warp.
+#ifndef KCMC_WARP_LDS_PAD
+#define KCMC_WARP_LDS_PAD 0
+#endif
+
 // one-channel tile height for a frame height (round 3)
 inline bool use_tile64(int H) { return H % 64 == 0 && H % 56 != 0; }
 // Multi-channel frames (RGB / RGBA, config 4): 3-4x the bytes per box pixel, so shorter
@@ -828,7 +835,7 @@ template <int C, class Cfg = BlockCfg, int VARIANT = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-access-mode"))) void warp_affine_u16_kernel(
     const uint16_t* __restrict__ src, uint16_t* __restrict__ dst, const TilePlan* __restrict__ plan,
     const double* __restrict__ minv, const int2* __restrict__ rowtab, int hq, int H, int W) {
-  __shared__ __attribute__((aligned(16))) uint16_t stile[Cfg::kLdsElems];
+  __shared__ __attribute__((aligned(16))) uint16_t stile[Cfg::kLdsElems + (C == 1 ? KCMC_WARP_LDS_PAD : 0)];
   const int ntx = gridDim.x, nty = gridDim.y;
   const int tile = xcd_remap(blockIdx.x + ntx * (blockIdx.y + nty * blockIdx.z), ntx * nty * gridDim.z);
   const int f = tile / (ntx * nty);

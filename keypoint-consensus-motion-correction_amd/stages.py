@@ -163,12 +163,14 @@ def match_frames(
     d_hi: float = 2.0,
     norm: str = "l2",
     stream: Optional[int] = None,
+    prep: Optional[torch.Tensor] = None,
 ) -> MatchResult:
     """VA:194-214 for every frame: knn k=2 + reorder + ratio + median filters.
     uint8 descriptors (the reference's) or float32 (SIFT-style extension; its distance is
     this build's fp64-accumulated L2, not OpenCV's float accumulation, so near-tie order
     against cv2 is unpinned -- see knn2_l2u8); ``norm`` "hamming" (uint8 only) is the
-    opt-in NORM_HAMMING matcher for binary descriptors."""
+    opt-in NORM_HAMMING matcher for binary descriptors.  ``prep`` (float32 only): the
+    output of match_f32_prepare for these descriptors, ordered before this call's stream."""
     if norm not in ("l2", "hamming"):
         raise ValueError(f"norm must be 'l2' or 'hamming' (got {norm!r})")
     dev = _device_of(des_tpl)
@@ -199,12 +201,48 @@ def match_frames(
         counts=torch.empty((F, 4), dtype=torch.int32, device=dev),
     )
     L = _lib.load()
+    max_nq = int(nq.max()) if F else 0
+    if prep is not None:
+        if not f32:
+            raise TypeError("prep: the prepared match is the float32 matcher's")
+        _require(prep, "prep", torch.uint8, dev, 1)
+        if prep.numel() < L.kcmc_match_f32_prep_bytes(n_tpl, F, max_nq):
+            raise ValueError("prep is smaller than kcmc_match_f32_prep_bytes")
+        _lib.check(L.kcmc_match_frames_f32_prepared(
+            _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F, max_nq,
+            _ptr(prep), float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist), _ptr(res.kp_ordered),
+            _ptr(res.keep_bits), _ptr(res.counts), _stream(dev, stream)))
+        return res
     fn = L.kcmc_match_frames_f32 if f32 else (L.kcmc_match_frames_hamming if norm == "hamming" else L.kcmc_match_frames)
     _lib.check(fn(
         _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F,
-        int(nq.max()) if F else 0, float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist),
+        max_nq, float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist),
         _ptr(res.kp_ordered), _ptr(res.keep_bits), _ptr(res.counts), _stream(dev, stream)))
     return res
+
+
+def match_f32_prepare(des_tpl: torch.Tensor, des_q: torch.Tensor, q_off: torch.Tensor, q_off_host: np.ndarray,
+                      stream: Optional[int] = None) -> torch.Tensor:
+    """The first part of the float32 match (template statistics, the frames' fp16 tile
+    images; kcmc_match_f32_prepare) into a fresh uint8 device buffer, on ``stream``; pass it
+    to match_frames(prep=...) on a stream ordered after this one."""
+    dev = _device_of(des_tpl)
+    _require(des_tpl, "des_tpl", torch.float32, dev, 2)
+    _require(des_q, "des_q", torch.float32, dev, 2)
+    _require(q_off, "q_off", torch.int32, dev, 1)
+    n_tpl, D = des_tpl.shape
+    F = q_off.numel() - 1
+    q_off_host = np.asarray(q_off_host)
+    _check_offsets(q_off_host, F)
+    max_nq = int(np.diff(q_off_host).max()) if F else 0
+    L = _lib.load()
+    nbytes = int(L.kcmc_match_f32_prep_bytes(n_tpl, F, max_nq))
+    if nbytes < 0:
+        raise ValueError("bad sizes")
+    prep = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    _lib.check(L.kcmc_match_f32_prepare(_ctx(dev).handle, _ptr(des_tpl), n_tpl, D, _ptr(des_q), _ptr(q_off), F, max_nq,
+                                        _ptr(prep), nbytes, _stream(dev, stream)))
+    return prep
 
 
 # ------------------------------------------------------------------ consensus
