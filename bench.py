@@ -76,9 +76,6 @@ class BenchConfig:
     ana_cus_per_se: int = 0
     # depth 2 + match beside: warp(k-1) queued before match(k) (OverlappedSlabs warp_first)
     warp_first: bool = False
-    # float descriptors, match on the kernel stream: the match's tile images of slab k+1 on
-    # a side stream beside warp(k-1) (OverlappedSlabs early_prep)
-    early_prep: bool = False
 
 
 # BASELINE.json configs.  c2 (configs[1]) is the headline line; the others are the
@@ -449,10 +446,6 @@ def main():
                     help="depth 2 + match beside: queue warp(k-1) before match(k) (OverlappedSlabs warp_first; "
                          "default: the config's)")
     ap.add_argument("--no-warp-first", dest="warp_first", action="store_false")
-    ap.add_argument("--early-prep", action="store_true", default=None,
-                    help="float descriptors: the match's tile images of the next slab on a side stream beside "
-                         "the warp (OverlappedSlabs early_prep; default: the config's)")
-    ap.add_argument("--no-early-prep", dest="early_prep", action="store_false")
     ap.add_argument("--device-merge", action="store_true",
                     help="merge the consensus votes on the device (OverlappedSlabs device_merge=True: "
                          "kcmc_consensus_merge_device behind the vote, no host round trip before the lookup; "
@@ -468,8 +461,6 @@ def main():
         args.pipeline_depth = bc.pipeline_depth
     if args.warp_first is None:
         args.warp_first = bc.warp_first
-    if args.early_prep is None:
-        args.early_prep = bc.early_prep
     if args.ana_cus is None:
         args.ana_cus = bc.ana_cus_per_se if not args.no_corun else 0
     if args.match_beside is None:
@@ -513,8 +504,7 @@ def main():
                                                             ana_cus_per_se=args.ana_cus,
                                                             warp_exclusive=not args.warp_shares,
                                                             warp_first=args.warp_first,
-                                                            device_merge=args.device_merge,
-                                                            early_prep=args.early_prep)
+                                                            device_merge=args.device_merge)
 
     def step(timer):
         if ov is None:
@@ -590,8 +580,6 @@ def main():
                                  "; consensus merged on the host")
         if args.warp_first and args.match_beside and args.pipeline_depth == 2:
             stage_ms["schedule"] += "; warp(k-1) queued before match(k)"
-        if args.early_prep and bc.descriptor == "f32" and not args.match_beside:
-            stage_ms["schedule"] += "; the next slab's tile images on a side stream beside the warp"
         if args.ana_cus:
             stage_ms["schedule"] += (f"; analysis stream on {args.ana_cus} of 8 CUs per shader engine"
                                      + (", the warp on every CU" if args.warp_shares else ", the warp on the other "

@@ -149,8 +149,8 @@ int kcmc_match_frames_f32(kcmc_ctx* ctx, const float* des_tpl_dev, const double*
                           double d_lo, double d_hi, int32_t* out_idx_dev, float* out_dist_dev,
                           double* out_kp_ordered_dev, uint32_t* out_keep_bits_dev,
                           int32_t* out_counts_dev, kcmc_stream_t stream);
-/* The same match in two parts, so the first can run on another stream ahead of the
- * second (OverlappedSlabs early_prep: beside the previous slab's warp).
+/* The same match in two parts, so that an integrator can run the first on another stream
+ * ahead of the second (measured at c5 beside the previous slab's warp: no gain).
  * kcmc_match_f32_prepare: the template statistics and the frames' fp16 tile images into
  * prep_dev (device, 256-byte aligned, kcmc_match_f32_prep_bytes(n_tpl, n_frames, max_nq)
  * bytes; -1 for negative sizes); kcmc_match_frames_f32_prepared: kcmc_match_frames_f32 on

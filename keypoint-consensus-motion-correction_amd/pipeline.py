@@ -101,6 +101,7 @@ def _nomark(name, ev=None):
 
 def match_stage(inp: SlabInputs, cfg: AlignConfig, stream: Optional[int] = None,
                 prep: Optional[torch.Tensor] = None) -> stages.MatchResult:
+    """VA:194-214 for the slab; ``prep``: the float match's first part (stages.match_f32_prepare)."""
     return stages.match_frames(inp.des_tpl, inp.kp_tpl, inp.des_q, inp.kp_q, inp.q_off, inp.q_off_host,
                                ratio=cfg.ratio, d_lo=cfg.d_lo, d_hi=cfg.d_hi, norm=cfg.match_norm, stream=stream,
                                prep=prep)
@@ -410,7 +411,7 @@ class OverlappedSlabs:
                  counts: Optional[List[int]] = None, group=None, depth: int = 2, corun: bool = True,
                  ransac_grid: Optional[int] = None, match_beside: bool = False, fit_first: bool = False,
                  ana_cus_per_se: int = 0, warp_exclusive: bool = True, warp_first: bool = False,
-                 device_merge: bool = False, early_prep: bool = False):
+                 device_merge: bool = False):
         if depth not in (2, 3):
             raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
         if match_beside and not corun:
@@ -436,12 +437,6 @@ class OverlappedSlabs:
         # analysis stream's path (its votes were ready a step earlier), so the merge kernel
         # only adds work there (c3 2.98-2.99 M vs 3.03-3.04 M frames/s, c2 607 k vs 622 k)
         self.device_merge = bool(device_merge)
-        # early_prep (float descriptors, the match on the kernel stream): the float match's
-        # first part (template stats + the frames' fp16 tile images, kcmc_match_f32_prepare)
-        # of slab k+1 on a side stream as soon as it is submitted, i.e. beside warp(k-1)
-        # (memory-bound beside a compute-bound warpPerspective), instead of on the kernel
-        # stream after it (c5 trace: frame_images 0.36-0.55 ms of a 5.5 ms step)
-        self.early_prep = bool(early_prep)
         if counts is not None and len(counts) > 1 and cfg.frame_downsample_rate != 1:
             # the rank's first frame is counted in sample frames, the affines in full-rate
             # frames: the same restriction as distributed.align_sharded
@@ -473,7 +468,6 @@ class OverlappedSlabs:
             self.ana = torch.cuda.Stream(self.dev) if self.corun else None
         self._hs = self.stream.cuda_stream
         self._hc = self.copy.cuda_stream
-        self.prep_stream = torch.cuda.Stream(self.dev) if self.early_prep else None
         self._ha = self.ana.cuda_stream if self.corun else self._hs
         # RANSAC beside the warp on at most this many workgroups (each walks its share of
         # the frames; 0 / None = one per frame).  Same-box A/B at c2:
@@ -628,28 +622,10 @@ class OverlappedSlabs:
         """match(k) and its vote on the kernel stream; the (gathered) votes to the host."""
         if self.match_beside:
             return self._match_beside(inp, out, mark)
-        prep = None
-        if self.early_prep and inp.des_tpl.dtype == torch.float32:
-            ps = self.prep_stream
-            cur = torch.cuda.current_stream(self.dev)
-            if cur != ps and not cur.query():  # the slab's inputs may still be in flight
-                ev = torch.cuda.Event()
-                ev.record(cur)
-                ps.wait_event(ev)
-            for t in (inp.des_tpl, inp.des_q, inp.q_off):
-                t.record_stream(ps)
-            with torch.cuda.stream(ps):
-                prep = stages.match_f32_prepare(inp.des_tpl, inp.des_q, inp.q_off, inp.q_off_host,
-                                                stream=ps.cuda_stream)
-            prepared = torch.cuda.Event()
-            prepared.record(ps)
-            prep.record_stream(self.stream)
-            self.stream.wait_event(prepared)
-            self._queued()
         self._at_tail(mark, "m0")
         for t in (inp.des_tpl, inp.kp_tpl, inp.des_q, inp.kp_q, inp.q_off):
             t.record_stream(self.stream)
-        match = match_stage(inp, self.cfg, stream=self._hs, prep=prep)
+        match = match_stage(inp, self.cfg, stream=self._hs)
         n_tpl = inp.des_tpl.shape[0]
         votes = stages.consensus_vote(match.keep_bits, n_tpl, self._f0, stream=self._hs)
         self._queued()
@@ -882,8 +858,6 @@ class OverlappedSlabs:
         self.stream.synchronize()
         if self.ana is not None:
             self.ana.synchronize()
-        if self.prep_stream is not None:
-            self.prep_stream.synchronize()
         self.copy.synchronize()
 
 

@@ -160,33 +160,6 @@ def test_overlapped_slabs_device_merge(dev, depth, corun, beside):
     _check_overlapped(ov, slabs, ref, depth)
 
 
-@pytest.mark.parametrize("depth", [2, 3])
-def test_overlapped_slabs_early_prep_float(dev, depth):
-    """Float descriptors with the match's first part (tile images) on a side stream as soon
-    as a slab is submitted (early_prep): same affines and frames as align_slab."""
-    cfg = pipeline.AlignConfig(n_kp_global=60, ransac_model="projective")
-    F, H, W = 10, 270, 480
-    slabs, ref = [], []
-    for seed in (31, 32, 33):
-        ks = synthetic.make_keypoints(F, 300, 128, (H, W), seed=seed, model="projective", descriptor="f32")
-        base = synthetic.make_texture((H, W), seed=seed)
-        frames = torch.from_numpy(np.broadcast_to(base, (F, H, W)).copy()).to(dev)
-        s = pipeline.SlabInputs(frames, torch.from_numpy(ks.des_tpl).to(dev), torch.from_numpy(ks.kp_tpl).to(dev),
-                                torch.from_numpy(ks.des_q).to(dev), torch.from_numpy(ks.kp_q).to(dev),
-                                torch.from_numpy(ks.q_off).to(dev), ks.q_off)
-        slabs.append(s)
-        ref.append(pipeline.align_slab(s, cfg))
-    ov = pipeline.OverlappedSlabs(dev, cfg, depth=depth, early_prep=True)
-    got = [ov.submit(s) for s in slabs]
-    got = [g for g in got if g is not None] + ov.flush()
-    ov.synchronize()
-    assert len(got) == 3
-    for r, g in zip(ref, got):
-        assert np.array_equal(r.affines, g.affines, equal_nan=True)
-        assert r.skipped == g.skipped and r.interpolated == g.interpolated
-        assert torch.equal(r.aligned, g.aligned)
-
-
 def test_overlapped_slabs_warp_first(dev):
     """warp(k-1) queued before match(k) (depth 2, match beside): same results."""
     cfg = pipeline.AlignConfig(n_kp_global=60)
