@@ -57,7 +57,7 @@ def _inputs(ks_list, dev):
 
 
 def _rank_main(rank: int, port: int, out_dir: str, model: str, depth: int, world: int, blind: bool,
-               beside: bool = False) -> None:
+               beside: bool = False, merge: bool = False) -> None:
     import torch.distributed as dist
 
     from kcmc_amd import distributed as kdist
@@ -82,7 +82,8 @@ def _rank_main(rank: int, port: int, out_dir: str, model: str, depth: int, world
     out["sharded_skipped"] = np.asarray(res.skipped, np.int64)
     out["sharded_interpolated"] = np.asarray(res.interpolated, np.int64)
     # 2. the pipelined schedule with the two exchanges, `depth` slabs in flight
-    ov = pipeline.OverlappedSlabs(dev, cfg, counts=list(COUNTS[world]), depth=depth, match_beside=beside)
+    ov = pipeline.OverlappedSlabs(dev, cfg, counts=list(COUNTS[world]), depth=depth, match_beside=beside,
+                                  device_merge=merge)
     r = [ov.submit(s) for s in slabs]
     rest = ov.flush()
     ov.synchronize()
@@ -107,16 +108,20 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("model,depth,world,blind,beside", [("euclidean", 2, 2, False, False),
-                                                            ("affine", 3, 2, False, False),
-                                                            ("euclidean", 2, 3, True, False),
-                                                            ("euclidean", 2, 2, False, True),
-                                                            ("affine", 2, 3, True, True)])
-def test_sharded_hip_path_equals_single_device(tmp_path, model, depth, world, blind, beside):
+@pytest.mark.parametrize("model,depth,world,blind,beside,merge", [("euclidean", 2, 2, False, False, False),
+                                                                  ("affine", 3, 2, False, False, False),
+                                                                  ("euclidean", 2, 3, True, False, False),
+                                                                  ("euclidean", 2, 2, False, True, False),
+                                                                  ("affine", 2, 3, True, True, False),
+                                                                  ("euclidean", 2, 2, False, True, True),
+                                                                  ("affine", 3, 3, True, False, True)])
+def test_sharded_hip_path_equals_single_device(tmp_path, model, depth, world, blind, beside, merge):
+    """merge: the consensus merged on the device from the all-gathered votes (device_merge)."""
     port = _free_port()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), str(r), str(port), str(tmp_path), model,
-                               str(depth), str(world), str(int(blind)), str(int(beside))], env=env, cwd=REPO)
+                               str(depth), str(world), str(int(blind)), str(int(beside)), str(int(merge))],
+                              env=env, cwd=REPO)
              for r in range(world)]
     try:
         rcs = [p.wait(timeout=200) for p in procs]
@@ -151,4 +156,4 @@ def test_sharded_hip_path_equals_single_device(tmp_path, model, depth, world, bl
 
 if __name__ == "__main__":
     _rank_main(int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5]), int(sys.argv[6]),
-               bool(int(sys.argv[7])), bool(int(sys.argv[8])))
+               bool(int(sys.argv[7])), bool(int(sys.argv[8])), bool(int(sys.argv[9])))
