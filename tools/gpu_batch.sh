@@ -16,6 +16,7 @@
 #   abpmc:<lib>:<cfg>:<tag>  the warp PMC passes (tools/pmc_warp.sh) against another build -> <out>/pmc_<tag>/
 #   trace:<cfg>:<tag>[:<args,comma>]  rocprofv3 --kernel-trace --memory-copy-trace of a short bench
 #                         -> <out>/trace_<tag>/ (read with tools/timeline.py)
+#   rehearse:<cfg>:<ranks>  bench.py over gloo ranks that share cuda:0 (the multi-rank path on one GPU)
 #   lab:<binary>[:<tag>][:<args,comma,separated>]  a lab binary (tools/ or ab/) -> <out>/lab_<tag>.txt
 #   envlab:<VAR=val>:<binary>:<tag>[:<args,comma>]  the same with one extra environment variable
 set -u
@@ -82,6 +83,11 @@ for step in "$@"; do
       IFS=, read -r -a X <<< "${d:-}"
       env "$a" timeout -k 10 240 "$b" "${X[@]}" > "$OUT/lab_$c.txt" 2>&1 || exit 1
       tail -4 "$OUT/lab_$c.txt" ;;
+    rehearse)  # rehearse:<cfg>:<ranks>  bench.py over <ranks> gloo ranks sharing cuda:0 (the N>1 code path)
+      KCMC_BENCH_BACKEND=gloo KCMC_BENCH_ONE_DEVICE=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node "$b" --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus "$b" --steps 5 --warmup 2 \
+        --config "$a" --cpu-sample 0 > "$OUT/rehearse_${a}_$b.json" 2>> "$OUT/rehearse.err" || exit 1
+      echo "rehearse $a x$b: $(tail -1 "$OUT/rehearse_${a}_$b.json" | head -c 200)" ;;
     lab)
       tag=${b:-$(basename "$a")}
       IFS=, read -r -a X <<< "${c:-}"
