@@ -492,6 +492,7 @@ class OverlappedSlabs:
         self._matched: Optional[_SlabInFlight] = None  # match queued, consensus pending
         self._fitted: Optional[_SlabInFlight] = None   # RANSAC queued, warp pending
         self._tail: Optional[torch.cuda.Event] = None   # an event at the kernel stream's tail
+        self._ana_tail: Optional[torch.cuda.Event] = None  # the same for the analysis stream
 
     def _at_tail(self, mark, *names) -> torch.cuda.Event:
         """One (timing) event at the kernel stream's current tail, shared by every wait,
@@ -507,6 +508,27 @@ class OverlappedSlabs:
     def _queued(self) -> None:
         """Work was queued on the kernel stream: the tail event moves."""
         self._tail = None
+
+    def _tail_on(self, stream: torch.cuda.Stream, mark, *names) -> torch.cuda.Event:
+        """_at_tail for any of the pipeline's streams: the analysis stream's RANSAC end, the
+        parameter transfer's dependency, the warp's wait and the next match's start mark
+        share one marker packet (c3 trace: four markers between RANSAC and the next knn2
+        cost ~20 us of idle device per step)."""
+        if stream is self.stream:
+            return self._at_tail(mark, *names)
+        ev = self._ana_tail
+        if ev is None:
+            ev = self._ana_tail = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+        for n in names:
+            mark(n, ev)
+        return ev
+
+    def _queued_on(self, stream: torch.cuda.Stream) -> None:
+        if stream is self.stream:
+            self._queued()
+        else:
+            self._ana_tail = None
 
     def _sharded(self) -> bool:
         return self.counts is not None and len(self.counts) > 1
@@ -616,6 +638,7 @@ class OverlappedSlabs:
         self.stream.wait_event(ev)
         if self.match_beside:  # the analysis stream reads the slab's keypoints
             self.ana.wait_event(ev)
+            self._queued_on(self.ana)
         self._queued()
 
     def _match(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
@@ -656,22 +679,20 @@ class OverlappedSlabs:
             # their memory from being reused by the caller's stream until it has
             for t in (inp.des_tpl, inp.kp_tpl, inp.des_q, inp.kp_q, inp.q_off):
                 t.record_stream(self.ana)
-            m0 = torch.cuda.Event(enable_timing=True)
-            m0.record(self.ana)
-            mark("m0", m0)
+            self._tail_on(self.ana, mark, "m0")  # usually the previous slab's RANSAC end
             match = match_stage(inp, self.cfg, stream=self._ha)
             votes = stages.consensus_vote(match.keep_bits, n_tpl, self._f0, stream=self._ha)
-            matched = torch.cuda.Event(enable_timing=True)
-            matched.record(self.ana)
-            mark("m1", matched)
+            self._queued_on(self.ana)
+            matched = self._tail_on(self.ana, mark, "m1")
             if self._sharded():
                 votes = self._gather(votes)  # the analysis stream waits for the collective
+                self._queued_on(self.ana)
             dch = None
             if self._use_device_merge(n_tpl):
                 dch = stages.consensus_merge_device(votes, n_tpl, self.cfg.n_kp_global, self.cfg.n_kp_global_min,
                                                     stream=self._ha)
-            ready = torch.cuda.Event()
-            ready.record(self.ana)
+                self._queued_on(self.ana)
+            ready = self._tail_on(self.ana, _nomark)
         slot = self._slots.pop() if self._slots else _Slot()
         if dch is not None:
             return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=ready, dchoice=dch)
@@ -701,15 +722,16 @@ class OverlappedSlabs:
             with torch.cuda.stream(self.ana):
                 self.ana.wait_event(p.matched)
                 self.ana.wait_event(p.slot.pack_ev)
+                self._queued_on(self.ana)
                 for t in (p.match.kp_ordered, p.match.keep_bits, p.inp.kp_tpl, pack_dev):
                     t.record_stream(self.ana)
                 self._fit_device(p, choice, pack_dev, mark, self._ha)
                 for t in (p.rr.params, p.rr.inliers, p.rr.n_inliers, p.rr.best_trial):
                     t.record_stream(self.stream)
-                p.fitted_ev = torch.cuda.Event()
-                p.fitted_ev.record(self.ana)
+                p.fitted_ev = self._tail_on(self.ana, _nomark)  # = the parameters' transfer event
         else:
             self.stream.wait_event(p.slot.pack_ev)
+            self._queued()
             self._fit_device(p, choice, pack_dev, mark, self._hs)
             self._queued()
         return p
@@ -722,13 +744,13 @@ class OverlappedSlabs:
             with torch.cuda.stream(self.ana):
                 if not self.match_beside:
                     self.ana.wait_event(p.matched)
+                    self._queued_on(self.ana)
                 for t in (p.match.kp_ordered, p.match.keep_bits, p.inp.kp_tpl, d.cons, d.votes, d.meta, d.pack):
                     t.record_stream(self.ana)
                 self._fit_device(p, None, None, mark, self._ha)
                 for t in (p.rr.params, p.rr.inliers, p.rr.n_inliers, p.rr.best_trial):
                     t.record_stream(self.stream)
-                p.fitted_ev = torch.cuda.Event()
-                p.fitted_ev.record(self.ana)
+                p.fitted_ev = self._tail_on(self.ana, _nomark)
         else:
             self._fit_device(p, None, None, mark, self._hs)
             self._queued()
@@ -736,9 +758,11 @@ class OverlappedSlabs:
 
     def _fit_device(self, p: _SlabInFlight, choice: Optional[stages.ConsensusChoice], pack_dev: Optional[torch.Tensor],
                     mark, hs: int) -> None:
-        """Lookup + RANSAC of a slab whose consensus is known, on the current stream (hs)."""
+        """Lookup + RANSAC of a slab whose consensus is known, on the current stream (hs): the
+        analysis stream (corun) or the kernel stream."""
         n_tpl = p.inp.des_tpl.shape[0]
-        mark("r0", None)
+        st = self.ana if self.corun and hs == self._ha else self.stream
+        self._tail_on(st, mark, "r0")
         if p.dchoice is not None:
             pt_off, pt_idx = stages.consensus_lookup_device(p.match.keep_bits, n_tpl, p.dchoice, stream=hs)
             p.cons = stages.Consensus(np.zeros(0, np.int32), np.zeros(0, np.int32), pt_off_dev=pt_off,
@@ -748,16 +772,15 @@ class OverlappedSlabs:
         else:
             p.cons = lookup_stage(p.match, n_tpl, choice, pack_dev, stream=hs)
             p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, stream=hs, max_workgroups=self.ransac_grid)
-        mark("r1", None)
+        self._queued_on(st)
+        after = self._tail_on(st, mark, "r1")
         params = p.rr.params
-        after = torch.cuda.Event()
         if self._sharded():
             bound = self._gather(stages.params_boundary(params, stream=hs))
+            self._queued_on(st)
+            after = self._tail_on(st, _nomark)
             p.n_bound = bound.numel()
-            after.record()
             self._d2h(p.slot.buf("bound", bound.numel(), torch.float64), bound, after, p.slot.params_ev)
-        else:
-            after.record()
         if logging_enabled(self.logger):
             # the point counts for VA:279-283's log lines travel with the parameters (the
             # lines are written in _finish): reading pt_off here would block the host on the
