@@ -468,9 +468,6 @@ __device__ __forceinline__ void fast_rows(const uint16_t* stile, const int2* __r
 #ifndef KCMC_FASTC_PITCH
 #define KCMC_FASTC_PITCH 144
 #endif
-#ifndef KCMC_FASTC_STORE_AUX
-#define KCMC_FASTC_STORE_AUX 2  // cache policy of the row stores (2: nontemporal)
-#endif
 template <class Cfg, int C>
 struct FastC {
   static constexpr int kPitch = KCMC_FASTC_PITCH;                        // plane row pitch (pixels)
@@ -625,14 +622,14 @@ __device__ __forceinline__ void fastc_rows(const uint16_t* stile, const int2* __
       const u32x3 o = {__builtin_amdgcn_perm(KCMC_Q(0, 1), KCMC_Q(0, 0), 0x05040100u),
                        __builtin_amdgcn_perm(KCMC_Q(1, 0), KCMC_Q(0, 2), 0x05040100u),
                        __builtin_amdgcn_perm(KCMC_Q(1, 2), KCMC_Q(1, 1), 0x05040100u)};
-      if (store_ok) __builtin_amdgcn_raw_buffer_store_b96(o, dst_rsrc, xoff, 2 * C * y * W, KCMC_FASTC_STORE_AUX);
+      if (store_ok) __builtin_amdgcn_raw_buffer_store_b96(o, dst_rsrc, xoff, 2 * C * y * W, 2);
     } else {
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
       const u32x4 o = {__builtin_amdgcn_perm(KCMC_Q(0, 1), KCMC_Q(0, 0), 0x05040100u),
                        __builtin_amdgcn_perm(KCMC_Q(0, 3), KCMC_Q(0, 2), 0x05040100u),
                        __builtin_amdgcn_perm(KCMC_Q(1, 1), KCMC_Q(1, 0), 0x05040100u),
                        __builtin_amdgcn_perm(KCMC_Q(1, 3), KCMC_Q(1, 2), 0x05040100u)};
-      if (store_ok) __builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, xoff, 2 * C * y * W, KCMC_FASTC_STORE_AUX);
+      if (store_ok) __builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, xoff, 2 * C * y * W, 2);
     }
 #undef KCMC_Q
   }
