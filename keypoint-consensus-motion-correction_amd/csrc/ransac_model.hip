@@ -24,7 +24,7 @@
 //     S = sum r^2 in numpy's pairwise order;
 //   * selection (count desc, S asc, trial asc) with skimage's S <= 0 early exit, then
 //     the winner's inlier mask and model.
-// ransac_model_refit_kernel -- one wave per frame: the final total-least-squares fit on
+// refit_frame (fused at the end of each scoring workgroup) -- one wave per frame: the final total-least-squares fit on
 //   the inliers (fit.py:871-875 -> ProjectiveTransform.estimate): Hartley
 //   normalisation, A^T A of the 2N x 7 (affine) / 2N x 9 (projective) system in fp64
 //   (its smallest eigenvector is the last right singular vector of A that skimage
@@ -477,6 +477,16 @@ __device__ __forceinline__ void gather_point(const double* __restrict__ src, con
   v = dst[2 * di + 1];
 }
 
+// The scoring kernel ends each frame with its refit for the homography (kFusedRefit); the
+// affine model runs ransac_model_refit_kernel after the scoring.
+template <int MODEL>
+constexpr bool kFusedRefit = MODEL == KCMC_MODEL_PROJECTIVE;
+
+// The final total-least-squares fit of one frame by one wave (defined with the refit below).
+template <int MODEL, class PointFn, class InlierFn>
+__device__ __forceinline__ void refit_frame(int N, int lane, PointFn point, InlierFn inlier, const double (&hyp)[9],
+                                            double rate, double* o);
+
 // ---------------------------------------------------------------------- scoring
 // LARGE = false: frames with N <= 128 (one pairwise leaf) and the NaN frames;
 // LARGE = true: 128 < N <= kMaxN through the split plan.
@@ -484,9 +494,8 @@ template <int MODEL, bool LARGE>
 __device__ __forceinline__ void ransac_model_score_frame(
     int f, const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint64_t* __restrict__ hyp,
-    const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, double tq, int n_skip,
-    double* out_params, double* best_model, uint8_t* __restrict__ out_inl,
-    int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
+    const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, double tq, int n_skip, double rate,
+    double* out_params, uint8_t* __restrict__ out_inl, int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
   constexpr int K = MODEL == KCMC_MODEL_AFFINE ? 3 : 4;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int s_cnt[kThreads / 64];
@@ -518,7 +527,7 @@ __device__ __forceinline__ void ransac_model_score_frame(
   }
 
   // LDS: sx, sy, dx, dy [N] f64 | trial S [T] f64 | [LARGE: stack [kMaxStack][256] f64]
-  //      | per-wave leaf values [4][128] f64 | trial count [T] i32
+  //      | per-wave leaf values [4][128] f64 | trial count [T] i32 | the winner's inlier mask [N] u8
   double* sx = smem;
   double* sy = sx + N;
   double* dxs = sy + N;
@@ -529,6 +538,7 @@ __device__ __forceinline__ void ransac_model_score_frame(
   double* stk = tS + T;
   double* wvals = stk + (LARGE ? kMaxStack * kThreads : 0);
   int* tC = reinterpret_cast<int*>(wvals + kThreads / 64 * 128);
+  uint8_t* sinl = reinterpret_cast<uint8_t*>(tC + T);
   if (LARGE && tid == 0) {
     s_plan.n = 0;
     plan_gen<kPwDepth>(s_plan, 0, N);
@@ -727,15 +737,34 @@ __device__ __forceinline__ void ransac_model_score_frame(
     int c = 0;
     if (has_model) resid2<MODEL>(bm.h, P, k, thresh, c);
     out_inl[p0 + k] = (uint8_t)c;
+    if constexpr (kFusedRefit<MODEL>) sinl[k] = (uint8_t)c;
   }
   if (tid == 0) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      best_model[9 * (size_t)f + k] = has_model ? bm.h[k] : NAN;
-      if (!has_model) out_params[9 * (size_t)f + k] = NAN;  // skimage: model None (fit.py:876-879)
-    }
+    for (int k = 0; k < 9; ++k)  // skimage: model None (fit.py:876-879); else the separate refit's input
+      if (!has_model || !kFusedRefit<MODEL>) out_params[9 * (size_t)f + k] = has_model ? bm.h[k] : NAN;
     out_nin[f] = has_model ? best_c : 0;
     out_best[f] = best_t;
+  }
+  // the final fit on the inliers (fit.py:871-875), fused for the homography: one wave, the
+  // points and the mask from LDS (c5: the separate refit launch ran after every frame's
+  // scoring, beside the next slab's match; 92.5-94.1 k -> 97.6 k frames/s).  The affine
+  // model keeps the separate launch: fused, its 7 x 7 system takes the kernel from 124 to
+  // 157 VGPRs (3 waves per SIMD) or, held to 128, 108 B of spills (c3 even or slower)
+  if constexpr (kFusedRefit<MODEL>) {
+    if (has_model) {  // workgroup-uniform
+    __syncthreads();  // the mask in LDS
+    if (wave == 0)
+      refit_frame<MODEL>(
+          N, lane,
+          [&](int k, double& x, double& y, double& u, double& v) {
+            x = sx[k];
+            y = sy[k];
+            u = dxs[k];
+            v = dys[k];
+          },
+          [&](int k) { return sinl[k] != 0; }, bm.h, rate, out_params + 9 * (size_t)f);
+    }
   }
 }
 
@@ -813,39 +842,60 @@ __device__ __forceinline__ void smallest_eigvec(const double (&A)[n][n], double 
 #else
 #define KCMC_RANSAC_VGPR_ATTR
 #endif
+// (projective: 2 waves per SIMD, its scoring alone needs 231 VGPRs)
 template <int MODEL, bool LARGE>
-__global__ __launch_bounds__(kThreads) KCMC_RANSAC_VGPR_ATTR void ransac_model_score_kernel(
+__global__ __launch_bounds__(kThreads, MODEL == KCMC_MODEL_AFFINE ? 1 : 2) KCMC_RANSAC_VGPR_ATTR void
+ransac_model_score_kernel(
     int n_frames, const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint64_t* __restrict__ hyp,
-    const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, double tq, int n_skip,
-    double* out_params, double* best_model, uint8_t* __restrict__ out_inl,
-    int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
+    const int32_t* __restrict__ hyp_off, int hyp_off_len, int T, double thresh, double tq, int n_skip, double rate,
+    double* out_params, uint8_t* __restrict__ out_inl, int32_t* __restrict__ out_nin,
+    int32_t* __restrict__ out_best) {
   for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
     ransac_model_score_frame<MODEL, LARGE>(f, src, dst, pt_idx, pt_off, src_stride, hyp, hyp_off, hyp_off_len, T,
-                                           thresh, tq, n_skip, out_params, best_model, out_inl, out_nin, out_best);
+                                           thresh, tq, n_skip, rate, out_params, out_inl, out_nin, out_best);
     __syncthreads();  // the frame's LDS is free for the next one
   }
 }
 
+// The affine model's refit after the scoring: one wave per frame, the points through pt_idx
+// and the mask from global memory; the hypothesis model is the scoring's out_params entry,
+// overwritten here.
 template <int MODEL>
 __global__ __launch_bounds__(256) void ransac_model_refit_kernel(
     const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint8_t* __restrict__ inl,
-    const int32_t* __restrict__ nin, const double* best_model, int n_frames, double rate,
-    double* out_params) {
-  constexpr int n = MODEL == KCMC_MODEL_AFFINE ? 7 : 9;
+    const int32_t* __restrict__ nin, int n_frames, double rate, double* out_params) {
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (f >= n_frames || nin[f] <= 0) return;  // NaN params already written by the scoring kernel
   const int p0 = pt_off[f], N = pt_off[f + 1] - p0;
   double* o = out_params + 9 * (size_t)f;
+  double hyp[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) hyp[k] = o[k];
+  refit_frame<MODEL>(
+      N, lane,
+      [&](int k, double& x, double& y, double& u, double& v) {
+        gather_point(src, dst, pt_idx, src_stride, f, p0 + k, x, y, u, v);
+      },
+      [&](int k) { return inl[p0 + k] != 0; }, hyp, rate, o);
+}
+
+// The final fit of one frame by one wave (lane = its lane): point(k, x, y, u, v) gives
+// point pair k of the frame's N, inlier(k) its mask entry, hyp the scoring's model (kept
+// when the refit is degenerate); the result, scaled by the spatial rate, goes to o[0..8].
+template <int MODEL, class PointFn, class InlierFn>
+__device__ __forceinline__ void refit_frame(int N, int lane, PointFn point, InlierFn inlier, const double (&hyp)[9],
+                                            double rate, double* o) {
+  constexpr int n = MODEL == KCMC_MODEL_AFFINE ? 7 : 9;
 
   // centroids (np.mean(points, axis=0) of the inliers)
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, sc = 0.0;
   for (int k = lane; k < N; k += 64)
-    if (inl[p0 + k]) {
+    if (inlier(k)) {
       double x, y, u, v;
-      gather_point(src, dst, pt_idx, src_stride, f, p0 + k, x, y, u, v);
+      point(k, x, y, u, v);
       s0 += x;
       s1 += y;
       s2 += u;
@@ -857,9 +907,9 @@ __global__ __launch_bounds__(256) void ransac_model_refit_kernel(
   const double cdx = wave_sum(s2) / cnt, cdy = wave_sum(s3) / cnt;
   double q0 = 0.0, q1 = 0.0;
   for (int k = lane; k < N; k += 64)
-    if (inl[p0 + k]) {
+    if (inlier(k)) {
       double x, y, u, v;
-      gather_point(src, dst, pt_idx, src_stride, f, p0 + k, x, y, u, v);
+      point(k, x, y, u, v);
       q0 += (x - csx) * (x - csx) + (y - csy) * (y - csy);
       q1 += (u - cdx) * (u - cdx) + (v - cdy) * (v - cdy);
     }
@@ -880,9 +930,9 @@ __global__ __launch_bounds__(256) void ransac_model_refit_kernel(
 #pragma unroll
   for (int a = 0; a < NA; ++a) acc[a] = 0.0;
   for (int k = lane; k < N; k += 64)
-    if (inl[p0 + k]) {
+    if (inlier(k)) {
       double x, y, u, v;
-      gather_point(src, dst, pt_idx, src_stride, f, p0 + k, x, y, u, v);
+      point(k, x, y, u, v);
       const double xs = (x - csx) * nfs, ys = (y - csy) * nfs;
       const double e = (u - cdx) * nfd, g = (v - cdy) * nfd;
       const double q = e * e + g * g;
@@ -967,7 +1017,7 @@ __global__ __launch_bounds__(256) void ransac_model_refit_kernel(
   if (fabs(v[n - 1]) <= 1e-8) {
     // np.isclose(V[-1, -1], 0): estimate() returns False and keeps the hypothesis model
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Hm[k] = best_model[9 * (size_t)f + k];
+    for (int k = 0; k < 9; ++k) Hm[k] = hyp[k];
   } else {
     double h[8];
 #pragma unroll
@@ -988,6 +1038,7 @@ __global__ __launch_bounds__(256) void ransac_model_refit_kernel(
     o[8] = Hm[8];
   }
 }
+
 
 }  // namespace
 }  // namespace kcmc
@@ -1019,42 +1070,39 @@ static int ransac_model_impl(kcmc_ctx* ctx, int model, const double* src, const 
   const int need = max_n < ms + 1 ? ms + 1 : max_n;
   const int n_small = need < 128 ? need : 128;
   const size_t wvals = (size_t)kThreads / 64 * 128 * sizeof(double);
+  // + the winner's inlier mask (N bytes) for the fused refit
   const size_t lds_small = (size_t)(n_small + 1) * 4 * sizeof(double) + (size_t)n_small * 4 * sizeof(double) +
-                           (size_t)trials * (sizeof(double) + sizeof(int)) + wvals + 16;
+                           (size_t)trials * (sizeof(double) + sizeof(int)) + wvals + 16 + (((size_t)n_small + 15) & ~15);
   const size_t lds_large = (size_t)need * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) + wvals +
-                           (size_t)kMaxStack * kThreads * sizeof(double) + 16;
+                           (size_t)kMaxStack * kThreads * sizeof(double) + 16 + (((size_t)need + 15) & ~15);
   if ((max_n > 128 ? lds_large : lds_small) > 150 * 1024)
     return fail(KCMC_EUNSUPPORTED, "kcmc_ransac_model: max_n/trials exceed the LDS budget");
   const double tq = inlier_bound(thresh);
   hipStream_t s = (hipStream_t)stream;
-  // The scoring kernel's best hypothesis model goes straight into out_params: the refit
-  // reads a frame's entries before it overwrites them (one wave per frame), and frames
-  // without a model get NaN in both roles.  No workspace: a stream-ordered pool
-  // allocation cost ~0.2 ms of host time per call.
-  double* best_model = out_params;
-  const dim3 refit_grid((unsigned)ceil_div(n_frames, 4));
+  // The scoring kernel writes out_params: the homography's refit is fused into it (one wave
+  // per frame, points and mask from LDS); the affine model's hypothesis model goes there
+  // first and ransac_model_refit_kernel overwrites it with the refit.  No workspace: a stream-ordered pool allocation cost
+  // ~0.2 ms of host time per call.
   const unsigned grid = (unsigned)(max_workgroups > 0 && max_workgroups < n_frames ? max_workgroups : n_frames);
   if (model == KCMC_MODEL_AFFINE) {
     hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, false>), dim3(grid), dim3(kThreads),
                        lds_small, s, n_frames, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
-                       trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
+                       trials, thresh, tq, n_skip, rate, out_params, out_inliers, out_n_inliers, out_best_trial);
     if (max_n > 128)
       hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_AFFINE, true>), dim3(grid), dim3(kThreads),
                          lds_large, s, n_frames, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
-                         trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
-    hipLaunchKernelGGL((ransac_model_refit_kernel<KCMC_MODEL_AFFINE>), refit_grid, dim3(256), 0, s, src, dst, pt_idx,
-                       pt_off, src_frame_stride, out_inliers, out_n_inliers, best_model, n_frames, rate, out_params);
+                         trials, thresh, tq, n_skip, rate, out_params, out_inliers, out_n_inliers, out_best_trial);
+    hipLaunchKernelGGL((ransac_model_refit_kernel<KCMC_MODEL_AFFINE>), dim3((unsigned)ceil_div(n_frames, 4)), dim3(256),
+                       0, s, src, dst, pt_idx, pt_off, src_frame_stride, out_inliers, out_n_inliers, n_frames, rate,
+                       out_params);
   } else {
     hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_PROJECTIVE, false>), dim3(grid), dim3(kThreads),
                        lds_small, s, n_frames, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
-                       trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
+                       trials, thresh, tq, n_skip, rate, out_params, out_inliers, out_n_inliers, out_best_trial);
     if (max_n > 128)
       hipLaunchKernelGGL((ransac_model_score_kernel<KCMC_MODEL_PROJECTIVE, true>), dim3(grid), dim3(kThreads),
                          lds_large, s, n_frames, src, dst, pt_idx, pt_off, src_frame_stride, tab.dev, tab.off, tab.off_len,
-                         trials, thresh, tq, n_skip, out_params, best_model, out_inliers, out_n_inliers, out_best_trial);
-    hipLaunchKernelGGL((ransac_model_refit_kernel<KCMC_MODEL_PROJECTIVE>), refit_grid, dim3(256), 0, s, src, dst,
-                       pt_idx, pt_off, src_frame_stride, out_inliers, out_n_inliers, best_model, n_frames, rate,
-                       out_params);
+                         trials, thresh, tq, n_skip, rate, out_params, out_inliers, out_n_inliers, out_best_trial);
   }
   return launch_check("ransac_model kernels");
 }
