@@ -59,7 +59,11 @@ constexpr int kImgBytes = 18 * 1024;      // tile image, whole 1 KiB LDS-DMA pie
 constexpr int kPieces = kImgBytes / 1024;
 static_assert(kImgC + kTile * 4 <= kImgBytes, "tile image layout");
 constexpr int kTop = 8;                   // approximate top-K per lane
-constexpr int kImgThreads = 1024;         // frame_images_kernel
+#ifndef KCMC_IMG_ROWS
+#define KCMC_IMG_ROWS 1  // 4 (256-thread workgroups): faster alone, slower in the c5 step
+#endif
+constexpr int kImgRows = KCMC_IMG_ROWS;            // frame_images_kernel: rows per 16-lane group
+constexpr int kImgThreads = kTile * 16 / kImgRows;  // threads per 64-row tile
 
 // The build's exact distance (identical operation order in the oracle).
 __device__ __forceinline__ float exact_dist(const float* __restrict__ a, const float* __restrict__ b, int D) {
@@ -286,7 +290,8 @@ __global__ __launch_bounds__(256) void tpl_err_kernel(const float* __restrict__ 
 // keep 11 bits down to 2^-14 and the subnormal rest is in |db|), per row C'; and the
 // frame's max |b|^2 / max beta_j (fmax / fbeta, zeroed before the launch).  A value
 // beyond fp16's range flags the frame (fbad), whose rows are then all certified nowhere
-// (exact fallback).  One workgroup per tile: 16 lanes per row, 8 elements each.
+// (exact fallback).  One workgroup per tile: 16 lanes per row, 8 elements each, kImgRows rows
+// per lane group with all their loads issued before the first conversion.
 __device__ __forceinline__ float frame_scale(const unsigned* __restrict__ Kst) {
   return pow2_scale(__uint_as_float(Kst[1])) * 0.00390625f;
 }
@@ -298,6 +303,7 @@ __global__ __launch_bounds__(kImgThreads) void frame_images_kernel(const float* 
                                                                    unsigned* __restrict__ fmax,
                                                                    unsigned* __restrict__ fbeta,
                                                                    int32_t* __restrict__ fbad) {
+  constexpr int kGroups = kImgThreads / 16;  // 16-lane row groups; group g owns rows g, g + kGroups, ...
   const int t = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
   const int q_begin = q_off[f];
   const int n_q = min(q_off[f + 1] - q_begin, tpf * kTile);
@@ -311,58 +317,67 @@ __global__ __launch_bounds__(kImgThreads) void frame_images_kernel(const float* 
   const float isf = 1.f / sf;  // exact: s_f is a power of 2 in [2^-68, 2^52]
   const float sc = sT * sf;
   const float dA = __uint_as_float(Kst[2]);
-  const int rr = tid >> 4, col = (tid & 15) * 8;
+  const int g = tid >> 4, col = (tid & 15) * 8;
   uint8_t* tile = img + ((size_t)f * tpf + t) * kImgBytes;
-  const int r = t * kTile + rr;
-  const bool real = r < n_q;
-  float x[8];
+  // every row's loads first (kImgRows rows per lane in flight), then the conversions
+  float x[kImgRows][8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) x[k] = 0.f;
-  if (real) {
-    const float* src = base + (size_t)r * D;
-    if (v4) {
-      if (col < D) {
-        const float4 p = *reinterpret_cast<const float4*>(src + col);
-        x[0] = p.x; x[1] = p.y; x[2] = p.z; x[3] = p.w;
-      }
-      if (col + 4 < D) {
-        const float4 p = *reinterpret_cast<const float4*>(src + col + 4);
-        x[4] = p.x; x[5] = p.y; x[6] = p.z; x[7] = p.w;
-      }
-    } else {
+  for (int i = 0; i < kImgRows; ++i) {
+    const int r = t * kTile + g + i * kGroups;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) x[k] = col + k < D ? src[col + k] : 0.f;
+    for (int k = 0; k < 8; ++k) x[i][k] = 0.f;
+    if (r < n_q) {
+      const float* src = base + (size_t)r * D;
+      if (v4) {
+        if (col < D) {
+          const float4 p = *reinterpret_cast<const float4*>(src + col);
+          x[i][0] = p.x; x[i][1] = p.y; x[i][2] = p.z; x[i][3] = p.w;
+        }
+        if (col + 4 < D) {
+          const float4 p = *reinterpret_cast<const float4*>(src + col + 4);
+          x[i][4] = p.x; x[i][5] = p.y; x[i][6] = p.z; x[i][7] = p.w;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[i][k] = col + k < D ? src[col + k] : 0.f;
+      }
     }
   }
-  float ss = 0.f, e2 = 0.f;
-  bool big = false;
-  f16x8 h;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    ss = fmaf(x[k], x[k], ss);
-    const float y = x[k] * sf;
-    big |= !(fabsf(y) <= 65504.f);  // also NaN
-    h[k] = (_Float16)y;
-    const float d = x[k] - (float)h[k] * isf;  // the rounding error, exact (isf = 1 / s_f, a power of 2)
-    e2 = fmaf(d, d, e2);
-  }
-#pragma unroll
-  for (int off = 8; off > 0; off >>= 1) {
-    ss += __shfl_xor(ss, off);
-    e2 += __shfl_xor(e2, off);
-  }
-  *reinterpret_cast<f16x8*>(tile + (rr * kRowB + col) * 2) = h;
-  if ((tid & 15) == 15)  // the row's 16 bytes of padding: every image line is written whole
-    *reinterpret_cast<uint4*>(tile + (rr * kRowB + kDP) * 2) = make_uint4(0u, 0u, 0u, 0u);
   float nmax = 0.f, bmax = 0.f;
-  if ((tid & 15) == 0) {
-    const float beta = beta_of(sK, sqrtf(ss), dA, sqrtf(e2), D);
-    *reinterpret_cast<float*>(tile + kImgC + 4 * rr) = real ? (0.5f * (ss + K) + beta) * sc : INFINITY;
-    if (real) {
-      nmax = ss;
-      bmax = beta;
+  bool big = false;
+#pragma unroll
+  for (int i = 0; i < kImgRows; ++i) {
+    const int rr = g + i * kGroups;
+    const bool real = t * kTile + rr < n_q;
+    float ss = 0.f, e2 = 0.f;
+    f16x8 h;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ss = fmaf(x[i][k], x[i][k], ss);
+      const float y = x[i][k] * sf;
+      big |= !(fabsf(y) <= 65504.f);  // also NaN
+      h[k] = (_Float16)y;
+      const float d = x[i][k] - (float)h[k] * isf;  // the rounding error, exact (isf = 1 / s_f, a power of 2)
+      e2 = fmaf(d, d, e2);
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+      ss += __shfl_xor(ss, off);
+      e2 += __shfl_xor(e2, off);
+    }
+    *reinterpret_cast<f16x8*>(tile + (rr * kRowB + col) * 2) = h;
+    if ((tid & 15) == 15)  // the row's 16 bytes of padding: every image line is written whole
+      *reinterpret_cast<uint4*>(tile + (rr * kRowB + kDP) * 2) = make_uint4(0u, 0u, 0u, 0u);
+    if ((tid & 15) == 0) {
+      const float beta = beta_of(sK, sqrtf(ss), dA, sqrtf(e2), D);
+      *reinterpret_cast<float*>(tile + kImgC + 4 * rr) = real ? (0.5f * (ss + K) + beta) * sc : INFINITY;
+      if (real) {
+        nmax = fmaxf(nmax, ss);
+        bmax = fmaxf(bmax, beta);
+      }
     }
   }
+  static_assert((kImgBytes - kImgC - kTile * 4) / 16 <= kImgThreads, "image tail");
   if (tid < (kImgBytes - kImgC - kTile * 4) / 16)  // the image's tail after the C' values
     *reinterpret_cast<uint4*>(tile + kImgC + kTile * 4 + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
   if (__any(big) && (tid & 63) == 0) atomicOr(&fbad[f], 1);

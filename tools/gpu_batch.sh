@@ -19,6 +19,7 @@
 #   rehearse:<cfg>:<ranks>  bench.py over gloo ranks that share cuda:0 (the multi-rank path on one GPU)
 #   lab:<binary>[:<tag>][:<args,comma,separated>]  a lab binary (tools/ or ab/) -> <out>/lab_<tag>.txt
 #   envlab:<VAR=val>:<binary>:<tag>[:<args,comma>]  the same with one extra environment variable
+#   labprof:<binary>:<tag>  a lab under rocprofv3 --kernel-trace --stats -> <out>/labprof_<tag>/
 set -u
 OUT=${1:?out dir}
 shift
@@ -88,6 +89,12 @@ for step in "$@"; do
         --nproc-per-node "$b" --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus "$b" --steps 5 --warmup 2 \
         --config "$a" --cpu-sample 0 > "$OUT/rehearse_${a}_$b.json" 2>> "$OUT/rehearse.err" || exit 1
       echo "rehearse $a x$b: $(tail -1 "$OUT/rehearse_${a}_$b.json" | head -c 200)" ;;
+    labprof)  # labprof:<binary>:<tag>  a lab under rocprofv3 --kernel-trace --stats -> <out>/labprof_<tag>/
+      R=$PWD
+      (cd /tmp && export TMPDIR=/tmp && cd "$R" &&
+        timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/labprof_$b" -o run \
+          -- "$a" > "$OUT/labprof_$b.txt" 2>&1) || exit 1
+      tail -2 "$OUT/labprof_$b.txt" ;;
     lab)
       tag=${b:-$(basename "$a")}
       IFS=, read -r -a X <<< "${c:-}"

@@ -62,7 +62,7 @@ typedef uint8_t Desc;
 static int launch(const Desc* t, int n_tpl, int D, const Desc* q, const int32_t* off, int F, int nq, int32_t* idx,
                   float* dist) {
 #ifdef KNN_F32
-  return kcmc::launch_knn_f32(nullptr, t, n_tpl, D, q, off, F, nq, idx, dist, 0);
+  return kcmc::launch_knn_f32(nullptr, t, n_tpl, D, q, off, F, nq, nullptr, idx, dist, 0);
 #else
   return kcmc::launch_knn(t, n_tpl, D, q, off, F, nq, idx, dist, 0);
 #endif
