@@ -46,10 +46,18 @@ namespace {
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int kThreads = 512;
+#ifndef KCMC_F32_BLOCKS
+#define KCMC_F32_BLOCKS 1
+#endif
+constexpr int kBlk = KCMC_F32_BLOCKS;     // 32-row template blocks per wave (each lane: kBlk rows)
+constexpr int kThreads = 512 / kBlk;
 constexpr int kWaves = kThreads / 64;
+#ifndef KCMC_F32_WPE
+#define KCMC_F32_WPE (6 / KCMC_F32_BLOCKS)
+#endif
+constexpr int kWavesPerEU = KCMC_F32_WPE;  // occupancy target (register budget 512 / it)
 constexpr int kNBuf = 2;                  // tile buffers: one tile in flight ahead of the one in use
-constexpr int kTplPerWG = kWaves * 32;    // 256 template rows per workgroup
+constexpr int kTplPerWG = kWaves * 32 * kBlk;  // 256 template rows per workgroup
 constexpr int kDP = 128;                  // padded descriptor length
 constexpr int kKSteps = kDP / 16;         // k-steps of v_mfma_f32_32x32x16_f16
 constexpr int kTile = 64;                 // frame rows per tile image (two MFMA row blocks)
@@ -430,95 +438,16 @@ __device__ __forceinline__ void dma_tile(const uint8_t* __restrict__ src, uint8_
   }
 }
 
-// 6 waves per SIMD (<= 80 VGPRs; the epilogue spills a few, the tile loop none): the
-// waits on LDS and the MFMA results hide behind the other waves' top-K VALU work
-// (c5 lab 4.56 -> 4.38 ms against 4 waves per SIMD with three tile buffers)
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 6))) void knn2_l2f32_kernel(
-    const float* __restrict__ des_tpl, int n_tpl, int D, const float* __restrict__ des_q,
-    const int32_t* __restrict__ q_off, const uint8_t* __restrict__ img, int tpf,
-    const unsigned* __restrict__ Kst, const float* __restrict__ fmax, const float* __restrict__ fbeta,
-    const int32_t* __restrict__ fbad, int key_bits, int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
-    int32_t* __restrict__ fallback, int32_t* __restrict__ fb_cnt, int32_t* __restrict__ fb_frames,
-    unsigned long long* __restrict__ fb_keys) {
-  __shared__ __attribute__((aligned(16))) uint8_t tbuf[kNBuf][kImgBytes];
-
-  // XCD-aware order: the workgroups of one frame get consecutive ids of one XCD's run
-  // (dispatch is round-robin over the 8 XCDs), so the frame's tile images stay in that
-  // XCD's L2 for all of its template blocks
-  const int ntb = gridDim.x;
-  const int wg = xcd_remap(blockIdx.x + ntb * blockIdx.y, ntb * gridDim.y);
-  const int f = wg / ntb, tb = wg - f * ntb;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int c = lane & 31;  // MFMA column = template row within the wave's block
-  const int h = lane >> 5;  // k-half of the fragments / row group of the output
-  const int q_begin = q_off[f];
-  const int n_q = q_off[f + 1] - q_begin;
-  const int n_tiles = min((n_q + kTile - 1) / kTile, tpf);
-  const uint8_t* fimg = img + (size_t)f * tpf * kImgBytes;
-  if (n_tiles > 0) dma_tile(fimg, tbuf[0], wave, lane);
-
-  // ---- template fragment (B operand, fp16(-s_T a)) kept in registers: lane (c, h) holds
-  // row i's elements k = 16 s + 8 h + j of k-step s
+// Decode, merge, certify and re-rank one template row i of the wave (the lane's list ck).
+__device__ __forceinline__ void finish_row(const uint32_t (&ck)[kTop], int i, int c, int h, int f, int n_tpl, int D,
+                                           const float* __restrict__ des_tpl, const float* __restrict__ des_q,
+                                           int q_begin, int n_q, const unsigned* __restrict__ Kst,
+                                           const float* __restrict__ fmax, const float* __restrict__ fbeta,
+                                           const int32_t* __restrict__ fbad, int key_bits, uint32_t kmask,
+                                           int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
+                                           int32_t* __restrict__ fallback, int32_t* __restrict__ fb_cnt,
+                                           int32_t* __restrict__ fb_frames, unsigned long long* __restrict__ fb_keys) {
   const float sT = pow2_scale(__uint_as_float(Kst[1]));
-  const int i = tb * kTplPerWG + wave * 32 + c;
-  f16x8 btpl[kKSteps];
-#pragma unroll
-  for (int st = 0; st < kKSteps; ++st)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 16 * st + 8 * h + j;
-      const float v = (i < n_tpl && k < D) ? des_tpl[(size_t)i * D + k] : 0.f;
-      btpl[st][j] = (_Float16)(-v * sT);
-    }
-
-  // keys: v~'s bits with the low key_bits bits replaced by (tile << 5 | half << 4 | r)
-  const uint32_t kmask = ~((1u << key_bits) - 1u);
-  uint32_t ck[kTop];
-#pragma unroll
-  for (int k = 0; k < kTop; ++k) ck[k] = 0xffffffffu;
-  int cur = 0;  // t % kNBuf
-  for (int t = 0; t < n_tiles; ++t) {
-    // tile t has landed (this wave's pieces: vmcnt; the others': the barrier) and every
-    // wave is done with tile t - 1, whose buffer the copy of tile t + 1 overwrites.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + 1 < n_tiles) dma_tile(fimg + (size_t)(t + 1) * kImgBytes, tbuf[cur ^ 1], wave, lane);
-    const uint8_t* tbp = tbuf[cur];
-    cur ^= 1;
-    // accumulators start at the rows' C': half hh, lane's 16 rows 32 hh + (r & 3) + 8 (r >> 2) + 4h
-    const float* cq = reinterpret_cast<const float*>(tbp + kImgC);
-    const uint32_t tbase = (uint32_t)t << 5;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      v16f acc;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 q4 = *reinterpret_cast<const float4*>(cq + 32 * hh + 8 * g + 4 * h);
-        acc[4 * g] = q4.x;
-        acc[4 * g + 1] = q4.y;
-        acc[4 * g + 2] = q4.z;
-        acc[4 * g + 3] = q4.w;
-      }
-      const _Float16* ap = reinterpret_cast<const _Float16*>(tbp) + (32 * hh + c) * kRowB + 8 * h;
-#pragma unroll
-      for (int st = 0; st < kKSteps; ++st)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*reinterpret_cast<const f16x8*>(ap + 16 * st), btpl[st], acc, 0,
-                                                     0, 0);
-      // a value whose bits are >= the last key cannot enter the list (its truncation is >=
-      // the last listed value, which already bounds every unlisted row).  After the first
-      // few hundred rows most distances of a wave skip the insertion (the branch is per
-      // wave): 1 + 7 P VALU per distance, P = the share of the wave's values some lane
-      // inserts (0.31 on the c5 data, simulated; 0.34 from the round-3 PMC's INT32 count)
-      topk_try<true>(ck, __float_as_uint(acc[0]), kmask, (uint32_t)(hh * 16) | tbase);
-#pragma unroll
-      for (int r = 1; r < 16; ++r)
-        topk_try<false>(ck, __float_as_uint(acc[r]), kmask, (uint32_t)(hh * 16 + r) | tbase);
-    }
-  }
-
   // ---- decode (value truncated to the key, frame row) and merge the two row halves
   // (lanes c and c + 32 own the same template row)
   TopK best;
@@ -614,6 +543,118 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 6))
   out_dist[o] = d0;
   out_dist[o + 1] = d1;
 }
+
+// 6 waves per SIMD (<= 80 VGPRs; the epilogue spills a few, the tile loop none): the
+// waits on LDS and the MFMA results hide behind the other waves' top-K VALU work
+// (c5 lab 4.56 -> 4.38 ms against 4 waves per SIMD with three tile buffers)
+// (kBlk = 1; with kBlk = 2 a wave holds two template blocks, one LDS fragment read feeds two
+// MFMAs, at 3 waves per SIMD)
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kWavesPerEU, kWavesPerEU)))
+void knn2_l2f32_kernel(
+    const float* __restrict__ des_tpl, int n_tpl, int D, const float* __restrict__ des_q,
+    const int32_t* __restrict__ q_off, const uint8_t* __restrict__ img, int tpf,
+    const unsigned* __restrict__ Kst, const float* __restrict__ fmax, const float* __restrict__ fbeta,
+    const int32_t* __restrict__ fbad, int key_bits, int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
+    int32_t* __restrict__ fallback, int32_t* __restrict__ fb_cnt, int32_t* __restrict__ fb_frames,
+    unsigned long long* __restrict__ fb_keys) {
+  __shared__ __attribute__((aligned(16))) uint8_t tbuf[kNBuf][kImgBytes];
+
+  // XCD-aware order: the workgroups of one frame get consecutive ids of one XCD's run
+  // (dispatch is round-robin over the 8 XCDs), so the frame's tile images stay in that
+  // XCD's L2 for all of its template blocks
+  const int ntb = gridDim.x;
+  const int wg = xcd_remap(blockIdx.x + ntb * blockIdx.y, ntb * gridDim.y);
+  const int f = wg / ntb, tb = wg - f * ntb;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 31;  // MFMA column = template row within the wave's block
+  const int h = lane >> 5;  // k-half of the fragments / row group of the output
+  const int q_begin = q_off[f];
+  const int n_q = q_off[f + 1] - q_begin;
+  const int n_tiles = min((n_q + kTile - 1) / kTile, tpf);
+  const uint8_t* fimg = img + (size_t)f * tpf * kImgBytes;
+  if (n_tiles > 0) dma_tile(fimg, tbuf[0], wave, lane);
+
+  // ---- template fragment (B operand, fp16(-s_T a)) kept in registers: lane (c, h) holds
+  // row i's elements k = 16 s + 8 h + j of k-step s
+  const float sT = pow2_scale(__uint_as_float(Kst[1]));
+  const int i0 = tb * kTplPerWG + wave * 32 * kBlk + c;  // block b: row i0 + 32 b
+  f16x8 btpl[kBlk][kKSteps];
+#pragma unroll
+  for (int b = 0; b < kBlk; ++b)
+#pragma unroll
+    for (int st = 0; st < kKSteps; ++st)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + 32 * b, k = 16 * st + 8 * h + j;
+        const float v = (i < n_tpl && k < D) ? des_tpl[(size_t)i * D + k] : 0.f;
+        btpl[b][st][j] = (_Float16)(-v * sT);
+      }
+
+  // keys: v~'s bits with the low key_bits bits replaced by (tile << 5 | half << 4 | r)
+  const uint32_t kmask = ~((1u << key_bits) - 1u);
+  uint32_t ck[kBlk][kTop];
+#pragma unroll
+  for (int b = 0; b < kBlk; ++b)
+#pragma unroll
+    for (int k = 0; k < kTop; ++k) ck[b][k] = 0xffffffffu;
+  int cur = 0;  // t % kNBuf
+  for (int t = 0; t < n_tiles; ++t) {
+    // tile t has landed (this wave's pieces: vmcnt; the others': the barrier) and every
+    // wave is done with tile t - 1, whose buffer the copy of tile t + 1 overwrites.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 1 < n_tiles) dma_tile(fimg + (size_t)(t + 1) * kImgBytes, tbuf[cur ^ 1], wave, lane);
+    const uint8_t* tbp = tbuf[cur];
+    cur ^= 1;
+    // accumulators start at the rows' C': half hh, lane's 16 rows 32 hh + (r & 3) + 8 (r >> 2) + 4h
+    const float* cq = reinterpret_cast<const float*>(tbp + kImgC);
+    const uint32_t tbase = (uint32_t)t << 5;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      v16f acc[kBlk];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 q4 = *reinterpret_cast<const float4*>(cq + 32 * hh + 8 * g + 4 * h);
+#pragma unroll
+        for (int b = 0; b < kBlk; ++b) {
+          acc[b][4 * g] = q4.x;
+          acc[b][4 * g + 1] = q4.y;
+          acc[b][4 * g + 2] = q4.z;
+          acc[b][4 * g + 3] = q4.w;
+        }
+      }
+      const _Float16* ap = reinterpret_cast<const _Float16*>(tbp) + (32 * hh + c) * kRowB + 8 * h;
+      // one LDS fragment read feeds every block's MFMA
+#pragma unroll
+      for (int st = 0; st < kKSteps; ++st) {
+        const f16x8 av = *reinterpret_cast<const f16x8*>(ap + 16 * st);
+#pragma unroll
+        for (int b = 0; b < kBlk; ++b)
+          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, btpl[b][st], acc[b], 0, 0, 0);
+      }
+      // a value whose bits are >= the last key cannot enter the list (its truncation is >=
+      // the last listed value, which already bounds every unlisted row).  After the first
+      // few hundred rows most distances of a wave skip the insertion (the branch is per
+      // wave): 1 + 7 P VALU per distance, P = the share of the wave's values some lane
+      // inserts (0.31 on the c5 data, simulated; 0.34 from the round-3 PMC's INT32 count)
+#pragma unroll
+      for (int b = 0; b < kBlk; ++b) {
+        topk_try<true>(ck[b], __float_as_uint(acc[b][0]), kmask, (uint32_t)(hh * 16) | tbase);
+#pragma unroll
+        for (int r = 1; r < 16; ++r)
+          topk_try<false>(ck[b], __float_as_uint(acc[b][r]), kmask, (uint32_t)(hh * 16 + r) | tbase);
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < kBlk; ++b)
+    finish_row(ck[b], i0 + 32 * b, c, h, f, n_tpl, D, des_tpl, des_q, q_begin, n_q, Kst, fmax, fbeta, fbad, key_bits,
+               kmask, out_idx, out_dist, fallback, fb_cnt, fb_frames, fb_keys);
+}
+
 
 // Exact brute force for the rows phase 1 could not certify: frame f's listed template
 // rows (fb[f * n_tpl + k], k < fb_cnt[f]) in batches of up to kFbBatch.  Workgroup
