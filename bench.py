@@ -9,11 +9,10 @@ Detection is not part of the path (no detector exists in this image; keypoints a
 synthetic, see kcmc_amd/synthetic.py).
 
 Steps are issued through pipeline.OverlappedSlabs, a software pipeline (kernel stream:
-match(k) -> warp(k-1); RANSAC(k) on a second stream beside warp(k-1), --no-corun queues
-it behind the warp instead; depth 3, the default for c3, orders match(k) -> warp(k-2)
--> RANSAC(k-1)): the host consensus of step k runs while step k-1's frames are warped;
-every step still runs every stage, and the pipeline is drained inside the timed region.
---serial runs the steps strictly one after another.
+warp(k-1); analysis stream: match(k) -> lookup + RANSAC(k) beside it, or for c5 the match
+on the kernel stream ahead of the warp): the host consensus of step k runs while step
+k-1's frames are warped; every step still runs every stage, and the pipeline is drained
+inside the timed region.  --serial runs the steps strictly one after another.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
@@ -64,18 +63,11 @@ class BenchConfig:
     frames_per_gpu: int
     cpu_sample: int
     descriptor: str = "u8"
-    # slabs in flight (pipeline.OverlappedSlabs depth)
-    pipeline_depth: int = 2
     # the match + vote on the analysis stream beside the warp (OverlappedSlabs match_beside):
     # c2 / c3 / c4 at depth 2 (match(k), lookup + RANSAC(k) beside warp(k-1): +0.9 % / +3.9 %
     # / +3.5 %, profiles/r03_b9_*, r03_b10_*); c5's
     # 4 ms float match beside its 1.6 ms warp is 12 % slower
     match_beside: bool = False
-    # CUs per shader engine of the analysis stream's fixed CU slice (OverlappedSlabs
-    # ana_cus_per_se; 0: both streams share every CU)
-    ana_cus_per_se: int = 0
-    # depth 2 + match beside: warp(k-1) queued before match(k) (OverlappedSlabs warp_first)
-    warp_first: bool = False
 
 
 # BASELINE.json configs.  c2 (configs[1]) is the headline line; the others are the
@@ -422,49 +414,12 @@ def main():
     ap.add_argument("--detect", action="store_true",
                     help="also time align from raw uint16 frames on the device: normalisation + ORB-style "
                          "detection + the hot path (pipeline.align_frames); reported as `with_detection`")
-    ap.add_argument("--pipeline-depth", type=int, default=None, choices=(2, 3),
-                    help="slabs in flight in the pipelined schedule (pipeline.OverlappedSlabs depth; "
-                         "default: the config's, 2)")
-    ap.add_argument("--no-corun", action="store_true",
-                    help="RANSAC behind the warp on the one kernel stream (OverlappedSlabs corun=False)")
-    ap.add_argument("--ransac-grid", type=int, default=None,
-                    help="workgroups of the RANSAC launches beside the warp (default 0: one per frame)")
-    ap.add_argument("--match-beside", action="store_true", default=None,
-                    help="the match + vote also on the analysis stream, beside the warp (OverlappedSlabs "
-                         "match_beside=True); default: the config's (c4)")
-    ap.add_argument("--no-match-beside", dest="match_beside", action="store_false",
-                    help="the match + vote on the kernel stream ahead of the warp")
-    ap.add_argument("--fit-first", action="store_true",
-                    help="depth 3: queue lookup + RANSAC(k-1) before warp(k-2) (OverlappedSlabs fit_first=True; "
-                         "measured slower at c3)")
-    ap.add_argument("--ana-cus", type=int, default=None,
-                    help="CUs per shader engine (of 8) reserved for the analysis stream (OverlappedSlabs "
-                         "ana_cus_per_se; default: the config's, 0 = no CU split)")
-    ap.add_argument("--warp-shares", action="store_true",
-                    help="with --ana-cus: the warp stream keeps every CU (only the analysis is confined)")
-    ap.add_argument("--warp-first", action="store_true", default=None,
-                    help="depth 2 + match beside: queue warp(k-1) before match(k) (OverlappedSlabs warp_first; "
-                         "default: the config's)")
-    ap.add_argument("--no-warp-first", dest="warp_first", action="store_false")
-    ap.add_argument("--device-merge", action="store_true",
-                    help="merge the consensus votes on the device (OverlappedSlabs device_merge=True: "
-                         "kcmc_consensus_merge_device behind the vote, no host round trip before the lookup; "
-                         "default: the host merge)")
-    ap.add_argument("--no-device-merge", dest="device_merge", action="store_false")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
     bc = CONFIGS[args.config]
     if args.frames is None:
         args.frames = bc.frames_per_gpu
-    if args.pipeline_depth is None:
-        args.pipeline_depth = bc.pipeline_depth
-    if args.warp_first is None:
-        args.warp_first = bc.warp_first
-    if args.ana_cus is None:
-        args.ana_cus = bc.ana_cus_per_se if not args.no_corun else 0
-    if args.match_beside is None:
-        args.match_beside = bc.match_beside and not args.no_corun
     if args.cpu_procs is None:
         args.cpu_procs = host_cpus()[0]
     if args.cpu_sample is None:
@@ -497,14 +452,7 @@ def main():
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s; {args.frames} frames {bc.H}x{bc.W}x{bc.C} on {dev}")
 
     ov = None if args.serial else pipeline.OverlappedSlabs(dev, cfg, counts=counts if world > 1 else None,
-                                                            depth=args.pipeline_depth, corun=not args.no_corun,
-                                                            ransac_grid=args.ransac_grid,
-                                                            match_beside=args.match_beside,
-                                                            fit_first=args.fit_first,
-                                                            ana_cus_per_se=args.ana_cus,
-                                                            warp_exclusive=not args.warp_shares,
-                                                            warp_first=args.warp_first,
-                                                            device_merge=args.device_merge)
+                                                            match_beside=bc.match_beside)
 
     def step(timer):
         if ov is None:
@@ -565,25 +513,12 @@ def main():
     if ov is None:
         stage_ms["host_and_transfers"] = round(ms_step - match_ms - ransac_ms - warp_ms, 3)
     else:  # step k+1's match/consensus/RANSAC/post-processing overlap step k's warp
-        if args.match_beside:
-            stage_ms["schedule"] = (("pipelined: kernel stream warp(k-1); analysis stream match+vote(k) -> "
-                                     "lookup+RANSAC(k) beside it" if args.pipeline_depth == 2 else
-                                     "pipelined: kernel stream warp(k-2); analysis stream match+vote(k) -> "
-                                     "lookup+RANSAC(k-1) beside it") + "; host consensus merge under the warp")
+        if bc.match_beside:
+            stage_ms["schedule"] = ("pipelined: kernel stream warp(k-1); analysis stream match+vote(k) -> "
+                                    "lookup+RANSAC(k) beside it; host consensus merge under the warp")
         else:
-            stage_ms["schedule"] = ("pipelined: match+vote(k) -> warp(k-1) -> lookup+RANSAC(k)" if args.pipeline_depth == 2
-                                    else "pipelined: match+vote(k) -> warp(k-2) -> lookup+RANSAC(k-1)") + (
-                                        " on one stream" if args.no_corun else ", RANSAC on a second stream beside the warp"
-                                    ) + ", host consensus merge under the warp"
-        stage_ms["schedule"] += ("; consensus merged on the device" if args.device_merge and
-                                 stages.merge_device_supported(bc.n_tpl, bc.n_kp_global) else
-                                 "; consensus merged on the host")
-        if args.warp_first and args.match_beside and args.pipeline_depth == 2:
-            stage_ms["schedule"] += "; warp(k-1) queued before match(k)"
-        if args.ana_cus:
-            stage_ms["schedule"] += (f"; analysis stream on {args.ana_cus} of 8 CUs per shader engine"
-                                     + (", the warp on every CU" if args.warp_shares else ", the warp on the other "
-                                        f"{8 - args.ana_cus}"))
+            stage_ms["schedule"] = ("pipelined: match+vote(k) -> warp(k-1) on the kernel stream, lookup+RANSAC(k) "
+                                    "on a second stream beside the warp; host consensus merge under the warp")
         stage_ms["step_minus_warp"] = round(ms_step - warp_ms, 3)
         # rank 0's host seconds per step blocked in event waits / inside the all-gathers, and
         # its consensus merge / post-processing (OverlappedSlabs.stats)

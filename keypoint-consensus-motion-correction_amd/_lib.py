@@ -137,10 +137,21 @@ _SIGNATURES = {
 }
 
 
+def _alt_lib() -> str:
+    """KCMC_LIB_PATH: another build of the same library (same-box A/B runs of tools/ and the
+    debug sentinel build), honoured only together with the explicit test-only switch
+    KCMC_TEST_ONLY_ALT_LIB=1; set alone it is an error, not a silent swap of the product."""
+    alt = os.environ.get("KCMC_LIB_PATH")
+    if not alt:
+        return ""
+    if os.environ.get("KCMC_TEST_ONLY_ALT_LIB") != "1":
+        raise KcmcLibraryError("KCMC_LIB_PATH is a test-only override: set KCMC_TEST_ONLY_ALT_LIB=1 as well to "
+                               "load an alternative build")
+    return alt
+
+
 def lib_path() -> str:
-    # KCMC_LIB_PATH: an alternative build of the same library (same-box A/B runs of
-    # tools/*_rates.py); the package's own in-tree libkcmc.so otherwise
-    return os.environ.get("KCMC_LIB_PATH") or _build.LIB_PATH
+    return _alt_lib() or _build.LIB_PATH
 
 
 def load(auto_build: bool = True) -> ctypes.CDLL:
@@ -149,13 +160,14 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
-        path = lib_path()
-        if os.environ.get("KCMC_LIB_PATH"):
+        alt = _alt_lib()
+        path = alt or _build.LIB_PATH
+        if alt:
             import warnings
 
             warnings.warn(f"KCMC_LIB_PATH set: loading {path} (an A/B build; no auto-build, entry points it lacks "
                           "stay unbound and fail when called)", RuntimeWarning, stacklevel=2)
-        if auto_build and os.environ.get("KCMC_NO_BUILD", "0") != "1" and not os.environ.get("KCMC_LIB_PATH"):
+        if auto_build and os.environ.get("KCMC_NO_BUILD", "0") != "1" and not alt:
             try:
                 if not _build.up_to_date():
                     _build.build()
@@ -174,7 +186,7 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         for name, (args, res) in _SIGNATURES.items():
             fn = getattr(L, name, None)
             if fn is None:
-                if os.environ.get("KCMC_LIB_PATH"):  # an older A/B build: its missing entries stay unbound
+                if alt:  # an older A/B build: its missing entries stay unbound
                     continue
                 raise KcmcLibraryError(f"{path}: missing symbol {name} (stale build?)")
             fn.argtypes = args

@@ -135,17 +135,11 @@ extern "C" int kcmc_destroy(kcmc_ctx* ctx) {
 
 namespace kcmc {
 
-// KCMC_NO_STREAM_WS (A/B knob) is read once, for both workspace_alloc and workspace_free.
-static bool ws_cache_enabled() {
-  static const bool on = getenv("KCMC_NO_STREAM_WS") == nullptr;
-  return on;
-}
-
 // The per-stream cache is used only on a stream that names one ordered queue and is not
 // being captured: a block baked into a hipGraph must never be swapped or freed by later
 // eager calls, and hipStreamPerThread is one handle shared by every thread's stream.
 static bool cacheable_stream(hipStream_t s) {
-  if (!ws_cache_enabled() || s == hipStreamPerThread) return false;
+  if (s == hipStreamPerThread) return false;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &st) != hipSuccess) {
     hipGetLastError();

@@ -46,16 +46,10 @@ namespace {
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-#ifndef KCMC_F32_BLOCKS
-#define KCMC_F32_BLOCKS 1
-#endif
-constexpr int kBlk = KCMC_F32_BLOCKS;     // 32-row template blocks per wave (each lane: kBlk rows)
+constexpr int kBlk = 1;                   // 32-row template blocks per wave (2 measured slower)
 constexpr int kThreads = 512 / kBlk;
 constexpr int kWaves = kThreads / 64;
-#ifndef KCMC_F32_WPE
-#define KCMC_F32_WPE (6 / KCMC_F32_BLOCKS)
-#endif
-constexpr int kWavesPerEU = KCMC_F32_WPE;  // occupancy target (register budget 512 / it)
+constexpr int kWavesPerEU = 6;            // occupancy target (register budget 512 / it)
 constexpr int kNBuf = 2;                  // tile buffers: one tile in flight ahead of the one in use
 constexpr int kTplPerWG = kWaves * 32 * kBlk;  // 256 template rows per workgroup
 constexpr int kDP = 128;                  // padded descriptor length
@@ -67,10 +61,9 @@ constexpr int kImgBytes = 18 * 1024;      // tile image, whole 1 KiB LDS-DMA pie
 constexpr int kPieces = kImgBytes / 1024;
 static_assert(kImgC + kTile * 4 <= kImgBytes, "tile image layout");
 constexpr int kTop = 8;                   // approximate top-K per lane
-#ifndef KCMC_IMG_ROWS
-#define KCMC_IMG_ROWS 1  // 4 (256-thread workgroups): faster alone, slower in the c5 step
-#endif
-constexpr int kImgRows = KCMC_IMG_ROWS;            // frame_images_kernel: rows per 16-lane group
+// frame_images_kernel: rows per 16-lane group (4, 256-thread workgroups: faster alone,
+// slower in the c5 step)
+constexpr int kImgRows = 1;
 constexpr int kImgThreads = kTile * 16 / kImgRows;  // threads per 64-row tile
 
 // The build's exact distance (identical operation order in the oracle).

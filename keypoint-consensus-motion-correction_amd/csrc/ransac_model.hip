@@ -835,16 +835,9 @@ __device__ __forceinline__ void smallest_eigvec(const double (&A)[n][n], double 
 }
 
 // Workgroup g scores frames g, g + grid, ... (kcmc_set_ransac_grid; default one per frame).
-// KCMC_RANSAC_WAVES (A/B knob, off): waves per SIMD the register budget must allow, e.g. 5
-// (<= 96 VGPRs, some spills) so a wave fits the VGPRs a CU of warp tiles leaves.
-#ifdef KCMC_RANSAC_WAVES
-#define KCMC_RANSAC_VGPR_ATTR __attribute__((amdgpu_waves_per_eu(KCMC_RANSAC_WAVES)))
-#else
-#define KCMC_RANSAC_VGPR_ATTR
-#endif
 // (projective: 2 waves per SIMD, its scoring alone needs 231 VGPRs)
 template <int MODEL, bool LARGE>
-__global__ __launch_bounds__(kThreads, MODEL == KCMC_MODEL_AFFINE ? 1 : 2) KCMC_RANSAC_VGPR_ATTR void
+__global__ __launch_bounds__(kThreads, MODEL == KCMC_MODEL_AFFINE ? 1 : 2) void
 ransac_model_score_kernel(
     int n_frames, const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint64_t* __restrict__ hyp,

@@ -58,13 +58,6 @@ using BlockCfg = WarpCfg<56, 10240, 9>;  // 20 KB box, box rows <= 72 (7 workgro
 // to ~2.5 deg; larger rotations take the general staged path or the direct gather).
 using Block64Cfg = WarpCfg<64, 10240, 9>;
 
-// Extra LDS elements per one-channel affine workgroup (A/B knob): 20 KB boxes fit 8
-// workgroups = every wave slot of a CU; a pad of 512 (21 KB) caps them at 7 and leaves one
-// wave slot per SIMD to the kernels beside the warp.
-#ifndef KCMC_WARP_LDS_PAD
-#define KCMC_WARP_LDS_PAD 0
-#endif
-
 // one-channel tile height for a frame height (round 3)
 inline bool use_tile64(int H) { return H % 64 == 0 && H % 56 != 0; }
 // Multi-channel frames (RGB / RGBA, config 4): 3-4x the bytes per box pixel, so shorter
@@ -89,10 +82,7 @@ struct CfgFor<4> {
 // immediate offset of the upper one, and the per-row source origins come from a per-frame
 // table through scalar loads.  Boxes wider than kFastPitch or taller than kFastRows take
 // the general staged path (mode 0).
-#ifndef KCMC_FAST_PITCH
-#define KCMC_FAST_PITCH 144
-#endif
-constexpr int kFastPitch = KCMC_FAST_PITCH;  // pixels: 128-px tile + up to ~8 deg / 6 % zoom
+constexpr int kFastPitch = 144;  // pixels: 128-px tile + up to ~8 deg / 6 % zoom
 constexpr int kFastChunks = kFastPitch / 8;  // 16-byte chunks per staged row
 template <class Cfg>
 struct Fast {
@@ -465,12 +455,9 @@ __device__ __forceinline__ void fast_rows(const uint16_t* stile, const int2* __r
 // 1024 contiguous bytes of the row.  The general multi-channel path (mode 0) reads
 // interleaved taps with per-channel addressing and stores C separate dwords per lane at a
 // 12-byte lane stride (round 3: 148 VALU, 49 SALU, 25 LDS instructions per wave row at c4).
-#ifndef KCMC_FASTC_PITCH
-#define KCMC_FASTC_PITCH 144
-#endif
 template <class Cfg, int C>
 struct FastC {
-  static constexpr int kPitch = KCMC_FASTC_PITCH;                        // plane row pitch (pixels)
+  static constexpr int kPitch = 144;  // plane row pitch in pixels (192: fewer bank conflicts, same time)
   static constexpr int kRows = (Cfg::kLdsElems - 8) / (C * kPitch);      // the last 16 bytes: flags
   static constexpr int kPlane = kRows * kPitch;                          // elements per channel plane
   static constexpr int kFlagWord = Cfg::kLdsElems / 2 - 4;
@@ -634,6 +621,21 @@ __device__ __forceinline__ void fastc_rows(const uint16_t* stile, const int2* __
 #undef KCMC_Q
   }
 }
+
+// Debug instrument (tools/debug/warp_sentinel.sh builds it; never the product library): the
+// whole LDS array is filled with 0xFFFF before a tile stages its box, so that a tap read
+// outside the staged rows / columns returns a deterministic wrong value (65535) instead of
+// whatever an earlier workgroup left in that LDS, and the bit-exact tests catch it.
+#ifdef KCMC_WARP_SENTINEL
+template <int ELEMS>
+__device__ __forceinline__ void lds_sentinel(uint16_t* stile, int tid) {
+  for (int i = tid; i < ELEMS / 2; i += kThreads) reinterpret_cast<uint32_t*>(stile)[i] = 0xffffffffu;
+  __syncthreads();
+}
+#define KCMC_LDS_SENTINEL(stile, elems, tid) lds_sentinel<elems>(stile, tid)
+#else
+#define KCMC_LDS_SENTINEL(stile, elems, tid) ((void)0)
+#endif
 
 // Per-tile plan made by warp_plan_kernel.
 struct TilePlan {
@@ -823,16 +825,14 @@ __global__ __launch_bounds__(256) void warp_plan_kernel(const double* __restrict
 }
 
 // ------------------------------------------------------------ one tile per workgroup
-// VARIANT != 0 builds are ablations for tools/warp_lab.hip only (1: zeros instead of the
-// per-pixel work, 2: skip the staging loads); the library launches VARIANT 0.
 // no-unaligned-access-mode: keeps the two adjacent 16-bit tap reads from being fused
 // into one 4-byte LDS read at a 2-byte-aligned address, which the LDS replays (1.75x
 // slower kernel, measured in tools/warp_lab).
-template <int C, class Cfg = BlockCfg, int VARIANT = 0>
+template <int C, class Cfg = BlockCfg>
 __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-access-mode"))) void warp_affine_u16_kernel(
     const uint16_t* __restrict__ src, uint16_t* __restrict__ dst, const TilePlan* __restrict__ plan,
     const double* __restrict__ minv, const int2* __restrict__ rowtab, int hq, int H, int W) {
-  __shared__ __attribute__((aligned(16))) uint16_t stile[Cfg::kLdsElems + (C == 1 ? KCMC_WARP_LDS_PAD : 0)];
+  __shared__ __attribute__((aligned(16))) uint16_t stile[Cfg::kLdsElems];
   const int ntx = gridDim.x, nty = gridDim.y;
   const int tile = xcd_remap(blockIdx.x + ntx * (blockIdx.y + nty * blockIdx.z), ntx * nty * gridDim.z);
   const int f = tile / (ntx * nty);
@@ -844,7 +844,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
   uint16_t* Dst = dst + (size_t)f * H * W * C;
 
   Box box = unpack(plan[tile]);
-  if constexpr (C == 1 && VARIANT == 0) {
+  KCMC_LDS_SENTINEL(stile, Cfg::kLdsElems, tid);
+  if constexpr (C == 1) {
     if (box.mode == 3) {
       const int cpr = box.pitch >> 3;
       uint4 fchunk[Fast<Cfg>::kPasses];
@@ -882,7 +883,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
       return;
     }
   }
-  if constexpr ((C == 3 || C == 4) && VARIANT == 0) {
+  if constexpr (C == 3 || C == 4) {
     if (box.mode == 3) {
       const int gpr = box.pitch >> 3;
       uint4 g[FastC<Cfg, C>::kPasses][C];
@@ -914,11 +915,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
       return;
     }
   }
-  if (box.mode == 3) box.mode = 0;  // lab ablations: the general staged path
   const bool vec_stage = (C == 1) && ((W & 7) == 0);
   uint4 chunk[Cfg::kRowPasses];
   uint4 cchunk[C > 1 ? VecC<Cfg, C>::kPasses : 1];
-  if (box.mode == 0 && vec_stage && VARIANT != 2) stage_issue<Cfg>(S, box, H, W, tid, chunk);  // loads first
+  if (box.mode == 0 && vec_stage) stage_issue<Cfg>(S, box, H, W, tid, chunk);  // loads first
   if constexpr (C > 1) {
     if (box.mode == 0 && (W & 7) == 0) stage_vec_c_issue<Cfg, C>(S, box, H, W, tid, cchunk);
   }
@@ -927,7 +927,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
                    box.mode == 0 ? box.sy0 : 0, ad, bd, X0v, Y0v);
   if (box.mode == 0) {
     if (vec_stage) {
-      if (VARIANT != 2) stage_land<Cfg>(stile, box, tid, chunk);
+      stage_land<Cfg>(stile, box, tid, chunk);
     } else if (C > 1 && (W & 7) == 0) {
       if constexpr (C > 1) stage_vec_c_land<Cfg, C>(stile, box, tid, cchunk);
     } else {
@@ -935,7 +935,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((target("no-unaligned-acces
     }
   }
   __syncthreads();
-  output_tile<Cfg, C>(VARIANT == 1 ? 1 : box.mode, stile, box, S, Dst, H, W, xb, yb, wave, lane, ad, bd, X0v, Y0v);
+  output_tile<Cfg, C>(box.mode, stile, box, S, Dst, H, W, xb, yb, wave, lane, ad, bd, X0v, Y0v);
 }
 
 // Row-origin table entries per (frame, y & 3): padded so that a wave's scalar loads of
@@ -950,7 +950,7 @@ size_t warp_workspace_bytes(int n_frames, int H, int W) {
 }
 
 // Plan + tile launches on `s`; ws holds warp_workspace_bytes<Cfg>(n_frames, H, W) bytes.
-template <int C, class Cfg = typename CfgFor<C>::type, int VARIANT = 0>
+template <int C, class Cfg = typename CfgFor<C>::type>
 void launch_warp(const uint16_t* src, uint16_t* dst, const double* M, int n_frames, int H, int W, int inverse_map,
                  void* ws, hipStream_t s) {
   const int ntx = ceil_div(W, kTileW), nty = ceil_div(H, Cfg::kTileH);
@@ -961,7 +961,7 @@ void launch_warp(const uint16_t* src, uint16_t* dst, const double* M, int n_fram
   TilePlan* plan = reinterpret_cast<TilePlan*>(rowtab + (size_t)n_frames * 4 * hq);
   hipLaunchKernelGGL((warp_plan_kernel<C, Cfg>), dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, s, M, n_frames,
                      H, W, inverse_map, ntx, nty, plan, minv, rowtab, hq);
-  hipLaunchKernelGGL((warp_affine_u16_kernel<C, Cfg, VARIANT>), dim3(ntx, nty, n_frames), dim3(kThreads), 0, s, src,
+  hipLaunchKernelGGL((warp_affine_u16_kernel<C, Cfg>), dim3(ntx, nty, n_frames), dim3(kThreads), 0, s, src,
                      dst, plan, minv, rowtab, hq, H, W);
 }
 
@@ -1245,6 +1245,7 @@ warp_perspective_u16_kernel(const uint16_t* __restrict__ src, uint16_t* __restri
   uint16_t* Dst = dst + (size_t)f * H * W * C;
 
   const Box box = unpack(plan[tile]);
+  KCMC_LDS_SENTINEL(stile, Cfg::kLdsElems, tid);
   const bool vec_stage = (C == 1) && ((W & 7) == 0);
   uint4 chunk[Cfg::kRowPasses];
   uint4 cchunk[C > 1 ? VecC<Cfg, C>::kPasses : 1];

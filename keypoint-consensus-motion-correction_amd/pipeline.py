@@ -220,7 +220,8 @@ def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.C
     F, n_tpl = match.kp_ordered.shape[:2]
     src = match.kp_ordered.view(F * n_tpl, 2)
     if lists_dev is None and cons.pt_off_dev is not None:
-        _check_point_counts(cons, cfg)
+        with stages.on_stream(dev, stream):  # pt_off is read after the lookup that wrote it
+            _check_point_counts(cons, cfg)
         prepare_ransac(dev, cfg)
         rr = stages.ransac_lists(cfg.ransac_model, src, kp_tpl, cons.pt_off_dev, cons.pt_idx_dev, n_tpl,
                                  max_n=max_n if max_n is not None else max(len(cons.order), 1),
@@ -355,44 +356,46 @@ class _SlabInFlight:
     match: stages.MatchResult
     slot: _Slot
     n_votes: int                                   # elements of the (gathered) votes
-    matched: Optional[torch.cuda.Event] = None     # end of match(k) + vote on the kernel stream
+    matched: Optional[torch.cuda.Event] = None     # end of match(k) + vote
     cons: Optional[stages.Consensus] = None
     rr: Optional[stages.RansacResult] = None
     aligned: Optional[torch.Tensor] = None
-    fitted_ev: Optional[torch.cuda.Event] = None   # end of RANSAC(k) on the analysis stream (corun)
+    fitted_ev: Optional[torch.cuda.Event] = None   # end of RANSAC(k) on the analysis stream
     n_bound: int = 0                               # elements of the gathered boundaries (sharded)
-    dchoice: Optional[stages.DeviceChoice] = None  # the consensus merged on the device (device_merge)
 
 
 class OverlappedSlabs:
     """Streams slabs through the hot path as a software pipeline.
 
-    submit(slab k) queues, in this device order (``depth=2``, the default),
+    submit(slab k) queues, in this device order,
 
-        kernel stream:    match(k) -> vote(k) -> warp(k-1) -> [waits RANSAC(k)] -> warp(k) ...
-        analysis stream:                         lookup(k) -> RANSAC(k)   (beside warp(k-1))
+        kernel stream:    [match(k) -> vote(k)] -> warp(k-1) -> [waits RANSAC(k)] -> warp(k) ...
+        analysis stream:  [match(k) -> vote(k)] -> lookup(k) -> RANSAC(k)   (beside warp(k-1))
 
-    with every transfer on a side stream.  The consensus (VA:224-286) runs in three parts:
+    with every transfer on a side stream; the match + vote run on the analysis stream with
+    ``match_beside`` (c2 / c3 / c4: the kernel stream then carries only the warps) and on
+    the kernel stream ahead of the warp otherwise (c5: its 4 ms float match beside the
+    1.4 ms warp starves it).  The consensus (VA:224-286) runs in three parts:
     the vote (per template count + first occurrence, VA:239) on the device right behind the
     match, the merge (Counter.most_common, set(consensus), VA:240-248) on the host from the
     O(n_tpl) votes, and the per-frame lookup (VA:274) on the device in front of RANSAC, so
     only the votes, the consensus set and the parameters cross PCIe.  RANSAC(k) shares the
-    CUs with warp(k-1) (``corun``, the default: the warp is bound by HBM at the speed of a
-    plain copy and leaves VALU slots free); ``corun=False`` queues lookup/RANSAC(k) behind
-    warp(k-1) on the one kernel stream.  ``depth=3`` queues match(k) -> warp(k-2) ->
-    lookup/RANSAC(k-1) instead, so the host merge uses votes that were ready a whole step
-    earlier.  The warp of a slab reads its RANSAC parameters where RANSAC left them: with
+    CUs with warp(k-1) (the warp is bound by HBM at the speed of a plain copy and leaves VALU
+    slots free).  The warp of a slab reads its RANSAC parameters where RANSAC left them: with
     frame_downsample_rate == 1 the reference's post-processing (VA:143-145) hands a frame
     with a model its own parameters, so only frames without a model need the host (NaN-gap
     interpolation); the warp writes zeros for those and they are warped again, with the
     filled maps, once the host has them.  With frame_downsample_rate > 1 every full-rate
     frame's map comes from the host interpolation, and the warp of slab k waits for it.
-    Every slab runs every stage and its results equal ``align_slab``'s.
+    Every slab runs every stage and its results equal ``align_slab``'s.  (Measured and
+    retired schedules -- depth 3, RANSAC behind the warp, a fixed CU slice for the
+    analysis, a narrow RANSAC grid, the device-side merge in the pipeline, warp-first
+    queueing -- are recorded in DESIGN 6b-6d.)
 
-    submit returns the SlabResult of the slab ``depth - 1`` submissions back (None
-    before that); flush() finishes the slabs still in flight and returns their results
-    in order.  ``res.extras["done"]`` is an event after the slab's last warp; ``aligned`` is
-    ready once it has passed (or after synchronize()).
+    submit returns the SlabResult of the previous submission (None for the first);
+    flush() finishes the slab still in flight and returns its result.
+    ``res.extras["done"]`` is an event after the slab's last warp; ``aligned`` is ready once
+    it has passed (or after synchronize()).
 
     With ``counts`` (frames per rank) the slabs are one rank's share of a frame-sharded
     job (frame_downsample_rate 1): the votes [2, n_tpl] and each slab's parameter boundary
@@ -408,35 +411,8 @@ class OverlappedSlabs:
     """
 
     def __init__(self, device, cfg: AlignConfig, logger: Optional[logging.Logger] = None,
-                 counts: Optional[List[int]] = None, group=None, depth: int = 2, corun: bool = True,
-                 ransac_grid: Optional[int] = None, match_beside: bool = False, fit_first: bool = False,
-                 ana_cus_per_se: int = 0, warp_exclusive: bool = True, warp_first: bool = False,
-                 device_merge: bool = False):
-        if depth not in (2, 3):
-            raise ValueError("depth must be 2 (match(k) -> warp(k-1) -> RANSAC(k)) or 3")
-        if match_beside and not corun:
-            raise ValueError("match_beside needs corun=True")
-        self.depth = depth
-        # match_beside: the match + vote of slab k also run on the analysis stream, so the
-        # kernel stream carries only the warps: depth 3 queues match(k) ahead of lookup +
-        # RANSAC(k-1) beside warp(k-2); depth 2 runs match(k), then lookup + RANSAC(k),
-        # beside warp(k-1)
+                 counts: Optional[List[int]] = None, group=None, match_beside: bool = False):
         self.match_beside = bool(match_beside)
-        # fit_first (depth 3, corun): queue lookup + RANSAC(k-1) before waiting for RANSAC(k-2),
-        # so it starts beside match(k).  Measured slower at c3 (2.36 M vs 2.91 M frames/s,
-        # same box: RANSAC then shares the CUs with the match and the warp), so off.
-        self.fit_first = bool(fit_first)
-        # warp_first (depth 2, match_beside): warp(k-1) queued before match(k) (see submit)
-        self.warp_first = bool(warp_first)
-        # device_merge: Counter.most_common + set(consensus) (VA:240-248) on the device right
-        # behind the vote (kcmc_consensus_merge_device), so lookup + RANSAC are queued with no
-        # host round trip; the host checks N_KP_GLOBAL_MIN and reads the consensus when it
-        # collects the parameters (round 4; the host merge otherwise, and for shapes the
-        # device merge does not take: n_tpl > 4096 or n_kp_global > 1024).  Off by default:
-        # in the beside-the-warp schedule the host merge of slab k-1 is already off the
-        # analysis stream's path (its votes were ready a step earlier), so the merge kernel
-        # only adds work there (c3 2.98-2.99 M vs 3.03-3.04 M frames/s, c2 607 k vs 622 k)
-        self.device_merge = bool(device_merge)
         if counts is not None and len(counts) > 1 and cfg.frame_downsample_rate != 1:
             # the rank's first frame is counted in sample frames, the affines in full-rate
             # frames: the same restriction as distributed.align_sharded
@@ -447,33 +423,12 @@ class OverlappedSlabs:
         self.logger = logger
         self.counts = counts
         self.group = group
-        # ana_cus_per_se: the analysis stream's kernels run on the first n CUs of every
-        # shader engine (a fixed CU slice, stages.cu_split_stream), and with warp_exclusive
-        # the kernel stream's on the other 8 - n; 0 = both streams on every CU
-        self.ana_cus_per_se = int(ana_cus_per_se or 0)
-        if self.ana_cus_per_se and not corun:
-            raise ValueError("ana_cus_per_se needs corun=True (an analysis stream)")
-        if self.ana_cus_per_se and warp_exclusive:
-            self.stream = stages.cu_split_stream(self.dev, self.ana_cus_per_se, complement=True)
-        else:
-            self.stream = torch.cuda.Stream(self.dev)
-        self.copy = torch.cuda.Stream(self.dev)  # vote / consensus / params / map transfers
-        # corun: lookup + RANSAC(k) on an analysis stream, beside warp(k-1) instead of behind
-        # it (the warp of slab k waits for it).  Same-box A/B: faster at
-        # c2, c3 and c5; the match stays on the kernel stream (beside the warp it starves).
-        self.corun = bool(corun)
-        if self.ana_cus_per_se:
-            self.ana = stages.cu_split_stream(self.dev, self.ana_cus_per_se)
-        else:
-            self.ana = torch.cuda.Stream(self.dev) if self.corun else None
+        self.stream = torch.cuda.Stream(self.dev)  # match (unless beside) and warps
+        self.copy = torch.cuda.Stream(self.dev)    # vote / consensus / params / map transfers
+        self.ana = torch.cuda.Stream(self.dev)     # [match], lookup and RANSAC beside the warp
         self._hs = self.stream.cuda_stream
         self._hc = self.copy.cuda_stream
-        self._ha = self.ana.cuda_stream if self.corun else self._hs
-        # RANSAC beside the warp on at most this many workgroups (each walks its share of
-        # the frames; 0 / None = one per frame).  Same-box A/B at c2:
-        # 128, 256 or 512 workgroups were no faster than one per frame, so the default
-        # stays one per frame.
-        self.ransac_grid = int(ransac_grid or 0) if self.corun else 0
+        self._ha = self.ana.cuda_stream
         self._rank = 0
         self._world = 1
         self._f0 = 0
@@ -489,7 +444,6 @@ class OverlappedSlabs:
         # host seconds spent blocked in event waits / inside the all-gathers (the rest of a
         # submit is the host's own work; tools/host_scaling.py)
         self.stats = {"wait_s": 0.0, "gather_s": 0.0, "merge_s": 0.0, "post_s": 0.0}
-        self._matched: Optional[_SlabInFlight] = None  # match queued, consensus pending
         self._fitted: Optional[_SlabInFlight] = None   # RANSAC queued, warp pending
         self._tail: Optional[torch.cuda.Event] = None   # an event at the kernel stream's tail
         self._ana_tail: Optional[torch.cuda.Event] = None  # the same for the analysis stream
@@ -564,72 +518,27 @@ class OverlappedSlabs:
 
     def submit(self, inp: SlabInputs, out: Optional[torch.Tensor] = None,
                mark: Optional[Callable[[str, Optional[torch.cuda.Event]], None]] = None) -> Optional[SlabResult]:
-        """``mark(name, event)``: stage marks m0/m1 (match + vote), w0/w1 (warp) with an event
-        the pipeline recorded on the kernel stream at that position, r0/r1 (lookup + RANSAC)
-        with None (record one on the current stream if needed)."""
+        """``mark(name, event)``: stage marks m0/m1 (match + vote), w0/w1 (warp), r0/r1
+        (lookup + RANSAC) with an event the pipeline recorded at that position."""
         mark = mark or _nomark
         self._wait_current()
         with torch.cuda.stream(self.stream):
             for t in (inp.frames, out):
                 if t is not None:
                     t.record_stream(self.stream)
-            if self.match_beside and self.depth == 2:
-                # kernel stream: warp(k-1); analysis stream: match(k) -> lookup + RANSAC(k),
-                # all of slab k beside warp(k-1); warp(k) (next submit) waits for RANSAC(k).
-                # warp_first: the host queues warp(k-1) (it waits for RANSAC(k-1)) before
-                # match(k), so the warp's plan kernel does not queue behind the match's
-                # persistent workgroups (c3 trace: plan 10 -> 100 us, the warp 0.1 ms late)
-                fitted, self._fitted = self._fitted, None
-                if self.warp_first and fitted is not None and self._device_maps():
-                    self._warp_device_maps(fitted, mark)
-                new = self._match(inp, out, mark)
-                if not self.warp_first and fitted is not None and self._device_maps():
-                    self._warp_device_maps(fitted, mark)
-                self._fitted = self._fit(new, mark)
-                return self._finish(fitted, mark) if fitted is not None else None
-            if self.match_beside:
-                # kernel stream: warp(k-2); analysis stream: match(k) -> lookup + RANSAC(k-1).
-                # The merge of slab k-1 uses votes that were ready a step earlier, so the
-                # analysis stream never waits on the host; warp(k-1) (next submit) waits for
-                # RANSAC(k-1) only.  (RANSAC(k-1) first and match(k) behind it put the
-                # votes -> host merge -> RANSAC round trip of one slab on the warp's path:
-                # c3 0.83 ms per step.)
-                fitted, self._fitted = self._fitted, None
-                if fitted is not None and self._device_maps():
-                    self._warp_device_maps(fitted, mark)
-                new = self._match(inp, out, mark)
-                if self._matched is not None:
-                    self._fitted = self._fit(self._matched, mark)
-                self._matched = new
-                return self._finish(fitted, mark) if fitted is not None else None
-            new = self._match(inp, out, mark)
             fitted, self._fitted = self._fitted, None
-            if self.depth == 3 and self.corun and self.fit_first:
-                # lookup + RANSAC(k-1) go to the analysis stream before the host waits for
-                # RANSAC(k-2): they start beside match(k) (meant to end inside warp(k-2); the
-                # c3 trace had RANSAC queued after the warp started spill 0.15 ms past it)
-                nxt = self._fit(self._matched, mark) if self._matched is not None else None
-                if fitted is not None and self._device_maps():
-                    self._warp_device_maps(fitted, mark)
-                self._fitted = nxt
-                self._matched = new
-                return self._finish(fitted, mark) if fitted is not None else None
+            new = self._match(inp, out, mark)  # match(k): analysis stream (beside) or kernel stream
             if fitted is not None and self._device_maps():
-                self._warp_device_maps(fitted, mark)  # warp(k-depth+1) queued behind match(k)
-            if self.depth == 2:
-                self._fitted = self._fit(new, mark)  # RANSAC(k) after warp(k-1)
-            else:
-                if self._matched is not None:
-                    self._fitted = self._fit(self._matched, mark)  # RANSAC(k-1) after warp(k-2)
-                self._matched = new
+                self._warp_device_maps(fitted, mark)  # warp(k-1)
+            self._fitted = self._fit(new, mark)  # lookup + RANSAC(k) beside warp(k-1)
             return self._finish(fitted, mark) if fitted is not None else None
 
     def _wait_current(self) -> None:
-        """Order the kernel stream after the caller's stream (the slab's inputs), but only
-        when the caller's stream still has work queued: a cross-stream wait that is already
-        satisfied still costs the device tens of microseconds.  The stream itself is asked
-        (hipStreamQuery): recording a probe event on it every submit delayed the next match
-        by ~11 us after the warp (`tools/gap_probe.py`: 41.5 -> 30.4 us)."""
+        """Order the pipeline's streams after the caller's stream (the slab's inputs), but
+        only when the caller's stream still has work queued: a cross-stream wait that is
+        already satisfied still costs the device tens of microseconds.  The stream itself is
+        asked (hipStreamQuery): recording a probe event on it every submit delayed the next
+        match by ~11 us after the warp (`tools/gap_probe.py`: 41.5 -> 30.4 us)."""
         cur = torch.cuda.current_stream(self.dev)
         if cur == self.stream or cur.query():
             return
@@ -642,7 +551,7 @@ class OverlappedSlabs:
         self._queued()
 
     def _match(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
-        """match(k) and its vote on the kernel stream; the (gathered) votes to the host."""
+        """match(k) and its vote; the (gathered) votes to the host."""
         if self.match_beside:
             return self._match_beside(inp, out, mark)
         self._at_tail(mark, "m0")
@@ -657,21 +566,12 @@ class OverlappedSlabs:
             votes = self._gather(votes)  # the kernel stream waits for the collective
             self._queued()
         slot = self._slots.pop() if self._slots else _Slot()
-        if self._use_device_merge(n_tpl):
-            dch = stages.consensus_merge_device(votes, n_tpl, self.cfg.n_kp_global, self.cfg.n_kp_global_min,
-                                                stream=self._hs)
-            self._queued()
-            matched = self._at_tail(mark)
-            return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=matched, dchoice=dch)
         ready = self._at_tail(mark)
         self._d2h(slot.buf("votes", votes.numel(), torch.int64), votes, ready, slot.votes_ev)
         return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=matched)
 
-    def _use_device_merge(self, n_tpl: int) -> bool:
-        return self.device_merge and stages.merge_device_supported(n_tpl, self.cfg.n_kp_global)
-
     def _match_beside(self, inp: SlabInputs, out: Optional[torch.Tensor], mark) -> _SlabInFlight:
-        """match(k) and its vote on the analysis stream (allocated there), ahead of the lookup +
+        """match(k) and its vote on the analysis stream (allocated there), behind the lookup +
         RANSAC of the previous slab; the (gathered) votes to the host."""
         n_tpl = inp.des_tpl.shape[0]
         with torch.cuda.stream(self.ana):
@@ -687,22 +587,14 @@ class OverlappedSlabs:
             if self._sharded():
                 votes = self._gather(votes)  # the analysis stream waits for the collective
                 self._queued_on(self.ana)
-            dch = None
-            if self._use_device_merge(n_tpl):
-                dch = stages.consensus_merge_device(votes, n_tpl, self.cfg.n_kp_global, self.cfg.n_kp_global_min,
-                                                    stream=self._ha)
-                self._queued_on(self.ana)
             ready = self._tail_on(self.ana, _nomark)
         slot = self._slots.pop() if self._slots else _Slot()
-        if dch is not None:
-            return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=ready, dchoice=dch)
         self._d2h(slot.buf("votes", votes.numel(), torch.int64), votes, ready, slot.votes_ev)
         return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=matched)
 
     def _fit(self, p: _SlabInFlight, mark) -> _SlabInFlight:
-        """The consensus merge (host) and the lookup + RANSAC (device) of a matched slab."""
-        if p.dchoice is not None:
-            return self._fit_merged(p, mark)
+        """The consensus merge (host) and the lookup + RANSAC (analysis stream) of a matched
+        slab."""
         cfg = self.cfg
         n_tpl = p.inp.des_tpl.shape[0]
         n_local = p.inp.q_off.numel() - 1
@@ -715,63 +607,29 @@ class OverlappedSlabs:
         choice = choose_consensus(votes, n_tpl, n_all, cfg, self.logger if self._rank == 0 else None,
                                   pack_out=pack_h.numpy())
         self.stats["merge_s"] += time.perf_counter() - t0
-        pack_dev = torch.empty(pack_h.numel(), dtype=torch.int32, device=self.dev)
-        stages.memcpy_async(pack_dev.data_ptr(), pack_h.data_ptr(), pack_h.numel() * 4, self._hc)
-        p.slot.pack_ev.record(self.copy)
-        if self.corun:
-            with torch.cuda.stream(self.ana):
-                self.ana.wait_event(p.matched)
-                self.ana.wait_event(p.slot.pack_ev)
-                self._queued_on(self.ana)
-                for t in (p.match.kp_ordered, p.match.keep_bits, p.inp.kp_tpl, pack_dev):
-                    t.record_stream(self.ana)
-                self._fit_device(p, choice, pack_dev, mark, self._ha)
-                for t in (p.rr.params, p.rr.inliers, p.rr.n_inliers, p.rr.best_trial):
-                    t.record_stream(self.stream)
-                p.fitted_ev = self._tail_on(self.ana, _nomark)  # = the parameters' transfer event
-        else:
-            self.stream.wait_event(p.slot.pack_ev)
-            self._queued()
-            self._fit_device(p, choice, pack_dev, mark, self._hs)
-            self._queued()
+        with torch.cuda.stream(self.ana):
+            pack_dev = torch.empty(pack_h.numel(), dtype=torch.int32, device=self.dev)
+            stages.memcpy_async(pack_dev.data_ptr(), pack_h.data_ptr(), pack_h.numel() * 4, self._hc)
+            p.slot.pack_ev.record(self.copy)
+            self.ana.wait_event(p.matched)
+            self.ana.wait_event(p.slot.pack_ev)
+            self._queued_on(self.ana)
+            for t in (p.match.kp_ordered, p.match.keep_bits, p.inp.kp_tpl):
+                t.record_stream(self.ana)
+            self._fit_device(p, choice, pack_dev, mark)
+            for t in (p.rr.params, p.rr.inliers, p.rr.n_inliers, p.rr.best_trial):
+                t.record_stream(self.stream)
+            p.fitted_ev = self._tail_on(self.ana, _nomark)  # = the parameters' transfer event
         return p
 
-    def _fit_merged(self, p: _SlabInFlight, mark) -> _SlabInFlight:
-        """Lookup + RANSAC of a slab whose consensus was merged on the device: queued at once
-        (no host wait), on the analysis stream behind the match (corun) or on the kernel stream."""
-        d = p.dchoice
-        if self.corun:
-            with torch.cuda.stream(self.ana):
-                if not self.match_beside:
-                    self.ana.wait_event(p.matched)
-                    self._queued_on(self.ana)
-                for t in (p.match.kp_ordered, p.match.keep_bits, p.inp.kp_tpl, d.cons, d.votes, d.meta, d.pack):
-                    t.record_stream(self.ana)
-                self._fit_device(p, None, None, mark, self._ha)
-                for t in (p.rr.params, p.rr.inliers, p.rr.n_inliers, p.rr.best_trial):
-                    t.record_stream(self.stream)
-                p.fitted_ev = self._tail_on(self.ana, _nomark)
-        else:
-            self._fit_device(p, None, None, mark, self._hs)
-            self._queued()
-        return p
-
-    def _fit_device(self, p: _SlabInFlight, choice: Optional[stages.ConsensusChoice], pack_dev: Optional[torch.Tensor],
-                    mark, hs: int) -> None:
-        """Lookup + RANSAC of a slab whose consensus is known, on the current stream (hs): the
-        analysis stream (corun) or the kernel stream."""
+    def _fit_device(self, p: _SlabInFlight, choice: stages.ConsensusChoice, pack_dev: torch.Tensor, mark) -> None:
+        """Lookup + RANSAC of a slab whose consensus is known, on the analysis stream (the
+        current stream here)."""
         n_tpl = p.inp.des_tpl.shape[0]
-        st = self.ana if self.corun and hs == self._ha else self.stream
+        st, hs = self.ana, self._ha
         self._tail_on(st, mark, "r0")
-        if p.dchoice is not None:
-            pt_off, pt_idx = stages.consensus_lookup_device(p.match.keep_bits, n_tpl, p.dchoice, stream=hs)
-            p.cons = stages.Consensus(np.zeros(0, np.int32), np.zeros(0, np.int32), pt_off_dev=pt_off,
-                                      pt_idx_dev=pt_idx)
-            p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, stream=hs, max_workgroups=self.ransac_grid,
-                                max_n=min(self.cfg.n_kp_global, n_tpl))
-        else:
-            p.cons = lookup_stage(p.match, n_tpl, choice, pack_dev, stream=hs)
-            p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, stream=hs, max_workgroups=self.ransac_grid)
+        p.cons = lookup_stage(p.match, n_tpl, choice, pack_dev, stream=hs)
+        p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, stream=hs)
         self._queued_on(st)
         after = self._tail_on(st, mark, "r1")
         params = p.rr.params
@@ -787,19 +645,14 @@ class OverlappedSlabs:
             # analysis stream and break the overlap
             self._d2h(p.slot.buf("pt_off", p.cons.pt_off_dev.numel(), torch.int32), p.cons.pt_off_dev, after,
                       p.slot.params_ev)
-        if p.dchoice is not None:  # the device merge's status and consensus, for _finish
-            d = p.dchoice
-            for name, t in (("meta", d.meta), ("cons", d.cons), ("cvotes", d.votes)):
-                self._d2h(p.slot.buf(name, t.numel(), torch.int32), t, after, p.slot.params_ev)
         self._d2h(p.slot.buf("params", params.numel(), torch.float64), params, after, p.slot.params_ev)
 
     def _warp_device_maps(self, p: _SlabInFlight, mark) -> None:
-        if p.fitted_ev is not None:
-            # RANSAC(k) ran beside warp(k-1) on the analysis stream: the host waits for it
-            # (it has nothing else to do before it blocks on this step's votes) instead of
-            # queueing a cross-stream wait, which leaves the device idle for tens of
-            # microseconds even when RANSAC finished long before
-            self._wait(p.fitted_ev)
+        # RANSAC(k) ran beside warp(k-1) on the analysis stream: the host waits for it (it
+        # has nothing else to do before it blocks on this step's votes) instead of queueing a
+        # cross-stream wait, which leaves the device idle for tens of microseconds even when
+        # RANSAC finished long before
+        self._wait(p.fitted_ev)
         self._at_tail(mark, "w0")
         p.aligned = warp_frames(p.inp.frames, p.rr.params, out=p.out, stream=self._hs)
         self._queued()
@@ -809,15 +662,6 @@ class OverlappedSlabs:
         """Host post-processing of slab p (VA:143-145) and the warps that need its maps."""
         self._wait(p.slot.params_ev)  # after RANSAC(k): its parameters are on the host
         n = p.inp.frames.shape[0]
-        if p.dchoice is not None:
-            # the device merge: N_KP_GLOBAL_MIN (AlignmentError, VA:241-244) and the consensus
-            nc = stages.check_device_choice(p.slot.buf("meta", 2, torch.int32).numpy())
-            k = p.dchoice.n_kp_global
-            p.cons.order = p.slot.buf("cons", k, torch.int32).numpy()[:nc].copy()
-            p.cons.votes = p.slot.buf("cvotes", k, torch.int32).numpy()[:nc].copy()
-            if self._rank == 0:
-                n_all = sum(self.counts) if self._sharded() else p.inp.q_off.numel() - 1
-                _log_rates(self.logger, p.cons.votes, n_all)
         if logging_enabled(self.logger) and "pt_off" in p.slot.bufs:
             pt_off = p.slot.buf("pt_off", p.cons.pt_off_dev.numel(), torch.int32).numpy()
             _log_low_counts(self.logger, np.diff(pt_off), self.cfg, p.f0)
@@ -862,25 +706,20 @@ class OverlappedSlabs:
         return res
 
     def flush(self, mark: Optional[Callable[[str, Optional[torch.cuda.Event]], None]] = None) -> List[SlabResult]:
-        """Finish every slab still in flight; their results, oldest first."""
+        """Finish the slab still in flight; its result (an empty list when none is)."""
         mark = mark or _nomark
         out: List[SlabResult] = []
         with torch.cuda.stream(self.stream):
-            while self._fitted is not None or self._matched is not None:
-                fitted, self._fitted = self._fitted, None
-                if fitted is not None and self._device_maps():
+            fitted, self._fitted = self._fitted, None
+            if fitted is not None:
+                if self._device_maps():
                     self._warp_device_maps(fitted, mark)
-                if self._matched is not None:
-                    self._fitted = self._fit(self._matched, mark)
-                    self._matched = None
-                if fitted is not None:
-                    out.append(self._finish(fitted, mark))
+                out.append(self._finish(fitted, mark))
         return out
 
     def synchronize(self) -> None:
         self.stream.synchronize()
-        if self.ana is not None:
-            self.ana.synchronize()
+        self.ana.synchronize()
         self.copy.synchronize()
 
 

@@ -64,6 +64,15 @@ def _stream(device: torch.device, stream: Optional[int] = None):
     return _P(torch.cuda.current_stream(device).cuda_stream)
 
 
+def on_stream(device: torch.device, stream: Optional[int] = None):
+    """A context in which torch's current stream is ``stream`` (a raw hipStream_t handle)
+    on ``device``, so that allocations and host reads made inside it are ordered with the
+    launches made on that stream; a no-op for None (torch's current stream already is)."""
+    if stream is None:
+        return contextlib.nullcontext()
+    return torch.cuda.stream(torch.cuda.ExternalStream(stream, device=device))
+
+
 def memcpy_async(dst: int, src: int, nbytes: int, stream: int) -> None:
     """hipMemcpyAsync(dst, src, nbytes, hipMemcpyDefault, stream) on raw pointers (pinned host
     <-> device transfers of the pipelines, without torch's per-copy dispatch)."""
@@ -239,7 +248,8 @@ def match_f32_prepare(des_tpl: torch.Tensor, des_q: torch.Tensor, q_off: torch.T
     nbytes = int(L.kcmc_match_f32_prep_bytes(n_tpl, F, max_nq))
     if nbytes < 0:
         raise ValueError("bad sizes")
-    prep = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    with on_stream(dev, stream):  # the buffer belongs to the stream that fills it
+        prep = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
     _lib.check(L.kcmc_match_f32_prepare(_ctx(dev).handle, _ptr(des_tpl), n_tpl, D, _ptr(des_q), _ptr(q_off), F, max_nq,
                                         _ptr(prep), nbytes, _stream(dev, stream)))
     return prep

@@ -32,6 +32,12 @@ def pytest_collection_modifyitems(config, items):
             it.add_marker(skip)
 
 
+def distinct_frames(base, F):
+    """F frames with pairwise different content: the base texture rolled by (37 f, 53 f)
+    pixels, so that a tile that read another frame's staged data cannot match by accident."""
+    return np.stack([np.roll(base, (37 * f, 53 * f), axis=(0, 1)) for f in range(F)])
+
+
 def load_golden(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 

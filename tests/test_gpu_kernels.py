@@ -7,7 +7,7 @@ import pytest
 import torch
 
 import oracle
-from conftest import load_golden
+from conftest import distinct_frames, load_golden
 from kcmc_amd import stages, synthetic
 
 pytestmark = pytest.mark.gpu
@@ -467,10 +467,10 @@ def test_warp_all_tile_paths_at_1080p(dev):
     Ms = [synthetic.rigid(np.deg2rad(6.0), 10.5, -7.25), synthetic.rigid(np.deg2rad(-30.0), 300, 100),
           np.array([[0.6, 0.01, 5.0], [-0.01, 0.6, 3.0]]), np.array([[1.8, 0.0, -400.0], [0.0, 1.8, -300.0]]),
           synthetic.rigid(0.0, 1500.0, 0.0)]
-    imgs = np.broadcast_to(img, (len(Ms), H, W)).copy()
+    imgs = distinct_frames(img, len(Ms))
     out = stages.warp_affine_u16(_t(imgs, dev), _t(np.stack(Ms), dev)).cpu().numpy()
     for f, M in enumerate(Ms):
-        assert np.array_equal(out[f], oracle.warp_affine_u16(img, M)), f
+        assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], M)), f
 
 
 @pytest.mark.parametrize("values", ["full", "14bit", "hot"])
@@ -492,10 +492,10 @@ def test_warp_64_row_tiles(dev, values):
           synthetic.rigid(np.deg2rad(6.0), 10.5, -7.25), synthetic.rigid(np.deg2rad(-30.0), 100, 50),
           np.array([[0.6, 0.01, 5.0], [-0.01, 0.6, 3.0]]), np.array([[1.02, 0.0, -3.0], [0.0, 0.98, 2.0]]),
           synthetic.rigid(0.0, 900.0, 0.0), synthetic.rigid(0.0, 0.0, 0.0)]
-    imgs = np.broadcast_to(img, (len(Ms), H, W)).copy()
+    imgs = distinct_frames(img, len(Ms))
     out = stages.warp_affine_u16(_t(imgs, dev), _t(np.stack(Ms), dev)).cpu().numpy()
     for f, M in enumerate(Ms):
-        assert np.array_equal(out[f], oracle.warp_affine_u16(img, M)), f
+        assert np.array_equal(out[f], oracle.warp_affine_u16(imgs[f], M)), f
 
 
 def test_warp_nan_map_gives_zeros(dev):

@@ -6,7 +6,7 @@ import pytest
 import torch
 
 import oracle
-from conftest import load_golden
+from conftest import distinct_frames, load_golden
 from kcmc_amd import VideoAligner, pipeline, stages, synthetic
 
 pytestmark = pytest.mark.gpu
@@ -100,17 +100,21 @@ def test_per_frame_helpers_match_reference_golden(monkeypatch):
 
 def test_config2_slab_end_to_end(dev):
     """A 1080p slab shaped like BASELINE config 2 (ORB-like D=32, n_tpl=500, rigid):
-    the recovered frame->template maps match the ground truth and every stage agrees
-    with the oracle on sampled frames."""
+    the recovered frame->template maps match the ground truth, RANSAC and the warp agree
+    with the oracle on every frame (each frame with its own content), and the input
+    frames are left untouched."""
     F, H, W = 48, 1080, 1920
     ks = synthetic.make_keypoints(F, 500, 32, (H, W), seed=7)
-    base = synthetic.make_texture((H, W), seed=0)
-    frames = torch.from_numpy(np.broadcast_to(base, (F, H, W)).copy()).to(dev)
+    host_frames = distinct_frames(synthetic.make_texture((H, W), seed=0), F)
+    frames = torch.from_numpy(host_frames).to(dev)
+    frames_before = frames.clone()
     inp = pipeline.SlabInputs(frames, torch.from_numpy(ks.des_tpl).to(dev), torch.from_numpy(ks.kp_tpl).to(dev),
                               torch.from_numpy(ks.des_q).to(dev), torch.from_numpy(ks.kp_q).to(dev),
                               torch.from_numpy(ks.q_off).to(dev), ks.q_off)
     cfg = pipeline.AlignConfig(n_kp_global=100)
     res = pipeline.align_slab(inp, cfg, logger=logging.getLogger("test"), keep_intermediates=True)
+    torch.cuda.synchronize()
+    assert torch.equal(frames, frames_before), "the pipeline wrote into its input frames"
     assert res.skipped == [] and res.interpolated == []
     np.testing.assert_allclose(res.affines[:, :, :2], ks.gt[:, :, :2], atol=2e-3)
     np.testing.assert_allclose(res.affines[:, :, 2], ks.gt[:, :, 2], atol=0.5)
@@ -118,66 +122,29 @@ def test_config2_slab_end_to_end(dev):
     kq = res.match.kp_ordered.cpu().numpy()
     inl = res.ransac.inliers.cpu().numpy().astype(bool)
     po, pi = res.consensus.pt_off, res.consensus.pt_idx
-    for f in range(0, F, 7):
+    best, n_in = res.ransac.best_trial.cpu().numpy(), res.ransac.n_inliers.cpu().numpy()
+    for f in range(F):
         L = pi[po[f]:po[f + 1]]
-        p, i_ref, _, _ = oracle.ransac_rigid(kq[f][L], ks.kp_tpl[L])
-        assert np.array_equal(inl[po[f]:po[f + 1]], i_ref)
+        p, i_ref, bt, ni = oracle.ransac_rigid(kq[f][L], ks.kp_tpl[L])
+        assert np.array_equal(inl[po[f]:po[f + 1]], i_ref), f
+        assert best[f] == bt and n_in[f] == ni, f
         np.testing.assert_allclose(res.affines[f], p, rtol=1e-4, atol=1e-6)
     out = res.aligned.cpu().numpy()
-    for f in (0, F - 1):
-        assert np.array_equal(out[f], oracle.warp_affine_u16(base, res.affines[f]))
+    for f in range(F):
+        assert np.array_equal(out[f], oracle.warp_affine_u16(host_frames[f], res.affines[f])), f
 
 
-@pytest.mark.parametrize("depth,corun,grid,beside,first", [(2, False, 0, False, True), (3, False, 0, False, True),
-                                                           (2, True, 0, False, True), (3, True, 0, False, True),
-                                                           (3, True, 0, False, False), (2, True, 5, False, True),
-                                                           (3, True, 0, True, True), (2, True, 0, True, False)])
-def test_overlapped_slabs_equal_align_slab(dev, depth, corun, grid, beside, first):
-    """OverlappedSlabs (depth 2: device order match(k) -> warp(k-1) -> RANSAC(k); depth 3:
-    match(k) -> warp(k-2) -> RANSAC(k-1); corun: RANSAC on a second stream beside the
-    warp, optionally on a narrow grid of workgroups that walk the frames; beside: the match
-    on that stream too (depth 3: ahead of RANSAC(k-1); depth 2: match(k) and RANSAC(k) both
-    beside warp(k-1)); first: at depth 3 RANSAC(k-1) queued before
-    the host waits for RANSAC(k-2)) gives the same affines and warped frames as the
-    sequential align_slab."""
+@pytest.mark.parametrize("beside", [False, True])
+def test_overlapped_slabs_equal_align_slab(dev, beside):
+    """OverlappedSlabs (kernel stream: [match(k)] -> warp(k-1); analysis stream: [match(k)]
+    -> lookup + RANSAC(k) beside the warp; beside: the match on the analysis stream too)
+    gives the same affines and warped frames as the sequential align_slab, leading,
+    interior and trailing gaps included."""
     cfg = pipeline.AlignConfig(n_kp_global=60)
     slabs = _gap_slabs(dev)
     ref = [pipeline.align_slab(s, cfg) for s in slabs]
-    ov = pipeline.OverlappedSlabs(dev, cfg, depth=depth, corun=corun, ransac_grid=grid, match_beside=beside,
-                                  fit_first=first)
-    _check_overlapped(ov, slabs, ref, depth)
-
-
-@pytest.mark.parametrize("depth,corun,beside", [(2, True, True), (3, True, True), (2, False, False),
-                                                (3, True, False)])
-def test_overlapped_slabs_device_merge(dev, depth, corun, beside):
-    """The consensus merged on the device (device_merge=True: lookup + RANSAC queued behind
-    the vote, no host round trip) gives the same results as align_slab."""
-    cfg = pipeline.AlignConfig(n_kp_global=60)
-    slabs = _gap_slabs(dev)
-    ref = [pipeline.align_slab(s, cfg) for s in slabs]
-    ov = pipeline.OverlappedSlabs(dev, cfg, depth=depth, corun=corun, match_beside=beside, device_merge=True)
-    _check_overlapped(ov, slabs, ref, depth)
-
-
-def test_overlapped_slabs_warp_first(dev):
-    """warp(k-1) queued before match(k) (depth 2, match beside): same results."""
-    cfg = pipeline.AlignConfig(n_kp_global=60)
-    slabs = _gap_slabs(dev)
-    ref = [pipeline.align_slab(s, cfg) for s in slabs]
-    ov = pipeline.OverlappedSlabs(dev, cfg, match_beside=True, warp_first=True)
-    _check_overlapped(ov, slabs, ref, 2)
-
-
-@pytest.mark.parametrize("cus,exclusive,beside", [(1, True, True), (2, False, True), (3, True, False)])
-def test_overlapped_slabs_cu_split(dev, cus, exclusive, beside):
-    """The analysis stream on a fixed CU slice (the first `cus` CUs of every shader engine;
-    the warp on the others, or on every CU) gives the same results as align_slab."""
-    cfg = pipeline.AlignConfig(n_kp_global=60)
-    slabs = _gap_slabs(dev)
-    ref = [pipeline.align_slab(s, cfg) for s in slabs]
-    ov = pipeline.OverlappedSlabs(dev, cfg, match_beside=beside, ana_cus_per_se=cus, warp_exclusive=exclusive)
-    _check_overlapped(ov, slabs, ref, 2)
+    ov = pipeline.OverlappedSlabs(dev, cfg, match_beside=beside)
+    _check_overlapped(ov, slabs, ref)
 
 
 def test_cu_split_stream_arguments(dev):
@@ -189,10 +156,10 @@ def test_cu_split_stream_arguments(dev):
     assert _lib.load().kcmc_stream_destroy(None) == 0
 
 
-def _check_overlapped(ov, slabs, ref, depth):
+def _check_overlapped(ov, slabs, ref):
     got = [ov.submit(s) for s in slabs]
-    assert all(g is None for g in got[:depth - 1])
-    got = got[depth - 1:] + ov.flush()
+    assert got[0] is None
+    got = got[1:] + ov.flush()
     assert ov.flush() == []
     ov.synchronize()
     assert [len(r.skipped) for r in ref] == [3, 4, 0]
@@ -260,10 +227,10 @@ def test_device_lists_follow_the_seed_after_host_list_ransac(dev, caplog):
         np.testing.assert_allclose(a7.affines[f], p, rtol=1e-9, atol=1e-9)
     logger = logging.getLogger("test_seed_lists")
     n_low = int((np.diff(po) < cfg42.n_kp_frame_skip).sum())
-    for merge in (False, True):
+    for beside in (False, True):
         caplog.clear()
         with caplog.at_level(logging.INFO, logger="test_seed_lists"):
-            ov = pipeline.OverlappedSlabs(dev, cfg42, logger=logger, match_beside=True, device_merge=merge)
+            ov = pipeline.OverlappedSlabs(dev, cfg42, logger=logger, match_beside=beside)
             got = [r for r in (ov.submit(inp), ov.submit(inp)) if r is not None] + ov.flush()
             ov.synchronize()
         low = [r.getMessage() for r in caplog.records if "low keypoint count" in r.getMessage()]
@@ -283,10 +250,9 @@ def test_euclidean_min_samples_other_than_two_raises(dev):
         pipeline.align_slab(inp, pipeline.AlignConfig(n_kp_global=30, ransac_min_samples=3))
 
 
-@pytest.mark.parametrize("model,rate,depth,corun", [("euclidean", 2, 2, True), ("euclidean", 2, 3, False),
-                                                    ("euclidean", 3, 3, True), ("projective", 1, 2, True),
-                                                    ("projective", 1, 3, True), ("projective", 1, 2, False)])
-def test_overlapped_slabs_host_maps_and_projective(dev, model, rate, depth, corun):
+@pytest.mark.parametrize("model,rate,beside", [("euclidean", 2, True), ("euclidean", 3, False),
+                                               ("projective", 1, False), ("projective", 1, True)])
+def test_overlapped_slabs_host_maps_and_projective(dev, model, rate, beside):
     """The OverlappedSlabs paths test_overlapped_slabs_equal_align_slab does not reach:
     frame_downsample_rate > 1 (every full-rate frame's map comes from the host NaN-padding
     + interpolation, so the warp waits for the host; with corun the host waits for RANSAC
@@ -310,9 +276,9 @@ def test_overlapped_slabs_host_maps_and_projective(dev, model, rate, depth, coru
                                          ks.q_off))
     ref = [pipeline.align_slab(s, cfg) for s in slabs]
     assert [len(r.skipped) for r in ref] == [2, 3, 0]
-    ov = pipeline.OverlappedSlabs(dev, cfg, depth=depth, corun=corun)
+    ov = pipeline.OverlappedSlabs(dev, cfg, match_beside=beside)
     got = [ov.submit(s) for s in slabs]
-    got = got[depth - 1:] + ov.flush()
+    got = got[1:] + ov.flush()
     ov.synchronize()
     for r, g in zip(ref, got):
         assert r.affines.shape[0] == S * rate

@@ -39,7 +39,7 @@ def _keypoints(rank: int, slab: int, model: str, world: int = 2, blind: bool = F
 
 def _frames(n: int):
     base = synthetic.make_texture(HW, seed=4)
-    return np.broadcast_to(base, (n,) + HW).copy()
+    return np.stack([np.roll(base, (5 * f, 11 * f), axis=(0, 1)) for f in range(n)])  # per-frame content
 
 
 def _inputs(ks_list, dev):
@@ -56,8 +56,8 @@ def _inputs(ks_list, dev):
                                t(q_off), q_off)
 
 
-def _rank_main(rank: int, port: int, out_dir: str, model: str, depth: int, world: int, blind: bool,
-               beside: bool = False, merge: bool = False) -> None:
+def _rank_main(rank: int, port: int, out_dir: str, model: str, world: int, blind: bool,
+               beside: bool = False) -> None:
     import torch.distributed as dist
 
     from kcmc_amd import distributed as kdist
@@ -81,14 +81,13 @@ def _rank_main(rank: int, port: int, out_dir: str, model: str, depth: int, world
     out["sharded_affines"] = res.affines
     out["sharded_skipped"] = np.asarray(res.skipped, np.int64)
     out["sharded_interpolated"] = np.asarray(res.interpolated, np.int64)
-    # 2. the pipelined schedule with the two exchanges, `depth` slabs in flight
-    ov = pipeline.OverlappedSlabs(dev, cfg, counts=list(COUNTS[world]), depth=depth, match_beside=beside,
-                                  device_merge=merge)
+    # 2. the pipelined schedule with the two exchanges
+    ov = pipeline.OverlappedSlabs(dev, cfg, counts=list(COUNTS[world]), match_beside=beside)
     r = [ov.submit(s) for s in slabs]
     rest = ov.flush()
     ov.synchronize()
-    assert all(x is None for x in r[:depth - 1]) and len(rest) == depth - 1
-    for k, r in enumerate(r[depth - 1:] + rest):
+    assert r[0] is None and len(rest) == 1
+    for k, r in enumerate(r[1:] + rest):
         out[f"ov{k}_aligned"] = r.aligned.cpu().numpy()
         out[f"ov{k}_affines"] = r.affines
         out[f"ov{k}_skipped"] = np.asarray(r.skipped, np.int64)
@@ -108,19 +107,14 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("model,depth,world,blind,beside,merge", [("euclidean", 2, 2, False, False, False),
-                                                                  ("affine", 3, 2, False, False, False),
-                                                                  ("euclidean", 2, 3, True, False, False),
-                                                                  ("euclidean", 2, 2, False, True, False),
-                                                                  ("affine", 2, 3, True, True, False),
-                                                                  ("euclidean", 2, 2, False, True, True),
-                                                                  ("affine", 3, 3, True, False, True)])
-def test_sharded_hip_path_equals_single_device(tmp_path, model, depth, world, blind, beside, merge):
-    """merge: the consensus merged on the device from the all-gathered votes (device_merge)."""
+@pytest.mark.parametrize("model,world,blind,beside", [("euclidean", 2, False, False), ("affine", 2, False, True),
+                                                     ("euclidean", 3, True, False), ("affine", 3, True, True)])
+def test_sharded_hip_path_equals_single_device(tmp_path, model, world, blind, beside):
+    """beside: the pipelined schedule with the match on the analysis stream (c2-c4's)."""
     port = _free_port()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), str(r), str(port), str(tmp_path), model,
-                               str(depth), str(world), str(int(blind)), str(int(beside)), str(int(merge))],
+                               str(world), str(int(blind)), str(int(beside))],
                               env=env, cwd=REPO)
              for r in range(world)]
     try:
@@ -155,5 +149,5 @@ def test_sharded_hip_path_equals_single_device(tmp_path, model, depth, world, bl
 
 
 if __name__ == "__main__":
-    _rank_main(int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5]), int(sys.argv[6]),
-               bool(int(sys.argv[7])), bool(int(sys.argv[8])), bool(int(sys.argv[9])))
+    _rank_main(int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5]),
+               bool(int(sys.argv[6])), bool(int(sys.argv[7])))

@@ -109,7 +109,7 @@ def main():
     inp, _ = bench.make_inputs(bc, bc.frames_per_gpu, 0, dev)
     out = torch.empty_like(inp.frames)
     cfg = pipeline.AlignConfig(n_kp_global=bc.n_kp_global, ransac_model=bc.model)
-    ov = pipeline.OverlappedSlabs(dev, cfg, corun=variant != "nocorun")
+    ov = pipeline.OverlappedSlabs(dev, cfg)
     torch.cuda.synchronize()
     with torch.cuda.stream(side if variant == "onstream" else torch.cuda.current_stream()):
         for _ in range(steps):

@@ -5,6 +5,7 @@
 # Steps (run in order; the batch stops at the first failing step):
 #   probe                 host CPU facts (cpu_count, affinity, cgroup quota) -> <out>/probe.txt
 #   tests[:<-k expr>]     pytest -m gpu (optionally -k; "+" stands for " or ") -> <out>/tests.log
+#   alttests:<lib>:<-k expr>  the same -k subset against another build of the library (ab/<lib>.so)
 #   envtests:<VAR=val>:<-k expr>  the same -k subset with one extra environment variable
 #   smoke                 __graft_entry__.smoke() -> <out>/smoke.log
 #   bench:<cfg>[:<tag>][:<args,comma,separated>]
@@ -40,6 +41,12 @@ for step in "$@"; do
       rc=$?
       echo "tests rc=$rc" >> "$OUT/tests.log"; tail -3 "$OUT/tests.log"
       [ $rc -eq 0 ] || exit 1 ;;
+    alttests)  # alttests:<ab/lib.so>:<-k expr>  pytest -m gpu -k <expr> against another build (e.g. the sentinel one)
+      KCMC_TEST_ONLY_ALT_LIB=1 KCMC_LIB_PATH="$a" timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 \
+        --timeout-method thread -k "${b//+/ or }" > "$OUT/tests_alt.log" 2>&1
+      rc=$?
+      echo "alttests $a rc=$rc" >> "$OUT/tests_alt.log"; tail -3 "$OUT/tests_alt.log"
+      [ $rc -eq 0 ] || exit 1 ;;
     envtests)  # envtests:<VAR=value>:<-k expr>  pytest -m gpu -k <expr> with one extra environment variable
       env "$a" timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "${b//+/ or }" \
         > "$OUT/tests_env.log" 2>&1
@@ -56,7 +63,7 @@ for step in "$@"; do
         2>> "$OUT/bench.err" || exit 1
       echo "$a $tag: $(head -c 160 "$OUT/${a}_$tag.json")" ;;
     abbench)  # abbench:<ab/lib.so>:<cfg>:<tag>  the bench against another build of the library
-      KCMC_LIB_PATH="$a" timeout -k 10 300 python bench.py --config "$b" --cpu-sample 0 > "$OUT/${b}_$c.json" \
+      KCMC_TEST_ONLY_ALT_LIB=1 KCMC_LIB_PATH="$a" timeout -k 10 300 python bench.py --config "$b" --cpu-sample 0 > "$OUT/${b}_$c.json" \
         2>> "$OUT/bench.err" || exit 1
       echo "$b $c ($a): $(head -c 160 "$OUT/${b}_$c.json")" ;;
     envbench)  # envbench:<VAR=value>:<cfg>:<tag>[:<args,comma>]  the bench with one extra environment variable
@@ -70,7 +77,7 @@ for step in "$@"; do
     profile)
       bash tools/profile_round.sh "$OUT/$a" --config "$a" || exit 1 ;;
     abpmc)
-      KCMC_LIB_PATH="$a" bash tools/pmc_warp.sh "$OUT/pmc_$c" "warp_affine_u16|warp_perspective_u16" --config "$b" \
+      KCMC_TEST_ONLY_ALT_LIB=1 KCMC_LIB_PATH="$a" bash tools/pmc_warp.sh "$OUT/pmc_$c" "warp_affine_u16|warp_perspective_u16" --config "$b" \
         || exit 1 ;;
     trace)
       IFS=, read -r -a X <<< "${c:-}"

@@ -1,7 +1,7 @@
 """Host timeline of the overlapped bench step (bench.py's workloads, default c2): where the
 host spends a step while the warp of the previous step runs on the GPU.
 
-    python tools/host_breakdown.py [--config c2] [--frames F] [--steps 8] [--depth 2|3]
+    python tools/host_breakdown.py [--config c2] [--frames F] [--steps 8]
 
 Prints, per step, host wall-clock milliseconds between the marks OverlappedSlabs.submit
 passes through (m0 match(k) launched, m1, w0/w1 around the warp(k-2) launch, r0 after
@@ -27,7 +27,6 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(bench.CONFIGS))
     ap.add_argument("--frames", type=int, default=None)
     ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--depth", type=int, default=None, choices=(2, 3), help="default: the config's (bench.py)")
     args = ap.parse_args()
     bc = bench.CONFIGS[args.config]
     args.frames = args.frames or bc.frames_per_gpu
@@ -36,7 +35,7 @@ def main():
     inp, _ = bench.make_inputs(bc, args.frames, 0, dev)
     out = torch.empty_like(inp.frames)
     cfg = pipeline.AlignConfig(n_kp_global=bc.n_kp_global, ransac_model=bc.model)
-    ov = pipeline.OverlappedSlabs(dev, cfg, depth=args.depth or bc.pipeline_depth)
+    ov = pipeline.OverlappedSlabs(dev, cfg, match_beside=bc.match_beside)
     rows = []
     for s in range(args.steps + 2):
         if s == 2:

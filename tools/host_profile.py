@@ -1,7 +1,7 @@
 """cProfile of the host side of the pipelined bench step (OverlappedSlabs.submit):
 which Python / torch / ctypes calls make up the per-step host chain.
 
-    python tools/host_profile.py [--config c3] [--steps 40] [--depth 3] [--top 45]
+    python tools/host_profile.py [--config c3] [--steps 40] [--top 45]
 
 Prints the step time with and without the profiler, then the top functions by own time
 and by cumulative time (per step, microseconds)."""
@@ -25,7 +25,6 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(bench.CONFIGS))
     ap.add_argument("--frames", type=int, default=None)
     ap.add_argument("--steps", type=int, default=40)
-    ap.add_argument("--depth", type=int, default=None, choices=(2, 3))
     ap.add_argument("--top", type=int, default=45)
     args = ap.parse_args()
     bc = bench.CONFIGS[args.config]
@@ -35,7 +34,7 @@ def main():
     inp, _ = bench.make_inputs(bc, frames, 0, dev)
     out = torch.empty_like(inp.frames)
     cfg = pipeline.AlignConfig(n_kp_global=bc.n_kp_global, ransac_model=bc.model)
-    ov = pipeline.OverlappedSlabs(dev, cfg, depth=args.depth or bc.pipeline_depth)
+    ov = pipeline.OverlappedSlabs(dev, cfg, match_beside=bc.match_beside)
 
     def run(n):
         torch.cuda.synchronize()

@@ -54,7 +54,7 @@ def _rank(rank, world, port, args, out_path):
     kdist.broadcast_template(inp.des_tpl, inp.kp_tpl)
     out = torch.empty_like(inp.frames)
     cfg = pipeline.AlignConfig(n_kp_global=bc.n_kp_global, ransac_model=bc.model)
-    ov = pipeline.OverlappedSlabs(dev, cfg, counts=[F] * world if world > 1 else None, depth=bc.pipeline_depth)
+    ov = pipeline.OverlappedSlabs(dev, cfg, counts=[F] * world if world > 1 else None, match_beside=bc.match_beside)
     rows = []
     for s in range(args.steps + 3):
         st0 = dict(ov.stats)

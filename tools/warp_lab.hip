@@ -172,7 +172,7 @@ int main(int argc, char** argv) {
     }
     if (getenv("LAB_ONLY56")) {  // the library's configuration only, 3 repeats
       for (int k = 0; k < 3; ++k)
-        report("128x56 (box 20 KB)", timeit([&] { launch_warp<1, C56, 0>(src, dst, M, F, H, W, 0, ws, 0); }, reps));
+        report("128x56 (box 20 KB)", timeit([&] { launch_warp<1, C56>(src, dst, M, F, H, W, 0, ws, 0); }, reps));
       continue;
     }
     if (getenv("LAB_PITCH")) {  // fast-path tile heights that keep 7-8 workgroups per CU at kFastPitch
@@ -181,27 +181,24 @@ int main(int argc, char** argv) {
       using P56 = WarpCfg<56, 11672, 9>;
       printf("   kFastPitch %d\n", kFastPitch);
       for (int k = 0; k < 2; ++k) {
-        report("128x56 (library cfg)", timeit([&] { launch_warp<1, C56, 0>(src, dst, M, F, H, W, 0, ws, 0); }, reps));
-        report("128x40 (18 KB)", timeit([&] { launch_warp<1, P40, 0>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+        report("128x56 (library cfg)", timeit([&] { launch_warp<1, C56>(src, dst, M, F, H, W, 0, ws, 0); }, reps));
+        report("128x40 (18 KB)", timeit([&] { launch_warp<1, P40>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
         printf("    mismatches: %llu\n", check());
-        report("128x48 (20 KB)", timeit([&] { launch_warp<1, P48, 0>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+        report("128x48 (20 KB)", timeit([&] { launch_warp<1, P48>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
         printf("    mismatches: %llu\n", check());
-        report("128x56 (22.8 KB)", timeit([&] { launch_warp<1, P56, 0>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+        report("128x56 (22.8 KB)", timeit([&] { launch_warp<1, P56>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
         printf("    mismatches: %llu\n", check());
       }
       continue;
     }
-    report("128x64 (box 24 KB)", timeit([&] { launch_warp<1, C64, 0>(src, dst, M, F, H, W, 0, ws, 0); }, reps));
-    report("128x64: no-compute (zeros)", timeit([&] { launch_warp<1, C64, 1>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
-    report("128x64: no staging loads", timeit([&] { launch_warp<1, C64, 2>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
-    report("128x32 (box 16 KB)", timeit([&] { launch_warp<1, C32, 0>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+    report("128x64 (box 24 KB)", timeit([&] { launch_warp<1, C64>(src, dst, M, F, H, W, 0, ws, 0); }, reps));
+    report("128x32 (box 16 KB)", timeit([&] { launch_warp<1, C32>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
     printf("    mismatches vs 128x64: %llu\n", check());
-    report("128x40 (box 16 KB)", timeit([&] { launch_warp<1, C40, 0>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+    report("128x40 (box 16 KB)", timeit([&] { launch_warp<1, C40>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
     printf("    mismatches vs 128x64: %llu\n", check());
-    report("128x48 (box 18 KB)", timeit([&] { launch_warp<1, C48, 0>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+    report("128x48 (box 18 KB)", timeit([&] { launch_warp<1, C48>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
     printf("    mismatches vs 128x64: %llu\n", check());
-    report("128x48: no staging loads", timeit([&] { launch_warp<1, C48, 2>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
-    report("128x56 (box 20 KB)", timeit([&] { launch_warp<1, C56, 0>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
+    report("128x56 (box 20 KB)", timeit([&] { launch_warp<1, C56>(src, dst2, M, F, H, W, 0, ws, 0); }, reps));
     printf("    mismatches vs 128x64: %llu\n", check());
   }
   report("uint4 copy", timeit([&] {
