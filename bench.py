@@ -35,6 +35,7 @@ sys.path.insert(0, REPO)
 
 import kcmc_amd  # noqa: E402,F401
 from kcmc_amd import distributed as kdist  # noqa: E402
+from kcmc_amd import multidevice as md  # noqa: E402
 from kcmc_amd import pipeline, stages, synthetic  # noqa: E402
 
 METRIC = "aligned frames/sec (whole node) at 1080p; RANSAC hypotheses scored/sec/GPU"
@@ -394,6 +395,62 @@ def load_traffic(config: str):
         return None, None
 
 
+def single_process(args, bc: BenchConfig) -> dict:
+    """The drop-in VideoAligner's multi-GPU path (kcmc_amd.multidevice.align_split): one
+    process, one contiguous frame slab per device of ``devices`` (a device may repeat), the
+    consensus merge and the gap interpolation once on the host per step.  Steps are not
+    pipelined across each other (each align_split call returns the aligned frames), which is
+    what a caller of VideoAligner.align_keypoints with device-resident frames gets."""
+    devices = [int(d) for d in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    cfg = pipeline.AlignConfig(n_kp_global=bc.n_kp_global, ransac_model=bc.model)
+    slabs, ranges = [], []
+    for k, d in enumerate(devices):
+        dev = torch.device("cuda", d)
+        inp, _ = make_inputs(bc, args.frames, k, dev)  # same template (seed 3), own frames per slab
+        slabs.append(inp)
+        f0 = k * args.frames
+        ranges.append(md.SlabRange(f0, f0 + args.frames, f0, f0 + args.frames))
+    log(f"single process: {len(devices)} slab(s) of {args.frames} frames on devices {devices}")
+
+    def sync():
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+
+    for _ in range(args.warmup):
+        md.align_split(slabs, ranges, cfg)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = md.align_split(slabs, ranges, cfg)
+    sync()
+    elapsed = time.perf_counter() - t0
+    total = args.frames * len(devices)
+    ms_step = 1e3 * elapsed / args.steps
+    out0 = torch.empty_like(slabs[0].frames)
+    torch.cuda.set_device(slabs[0].frames.device)
+    iso, _ = isolated_stage_ms(slabs[0], cfg, out0)
+    warp_bytes = 2 * slabs[0].frames.numel() * slabs[0].frames.element_size()
+    achieved = warp_bytes / (iso["warp"] * 1e-3) / 1e9
+    result = {
+        "metric": METRIC, "value": round(total * args.steps / elapsed, 1), "unit": "frames/s",
+        "n_gpus": len(set(devices)), "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u16 frames; u8/f32 descriptors, f64 RANSAC, f32 warp weights",
+        "data": "synthetic (seeded jittered texture + detector-shaped keypoints; no detector in image)",
+        "config": {"workload": bc.workload, "frames_per_slab": args.frames, "devices": devices,
+                   "parallelism": f"single-process split x{len(devices)} (VideoAligner drop-in path)"},
+        "skipped_frames": len(res.skipped),
+        "stage_ms_isolated_slab0": iso,
+        "roofline": {"kernel": (f"warp_perspective_u16_kernel<{bc.C}>" if bc.model == "projective"
+                                else f"warp_affine_u16_kernel<{bc.C}>"), "bound": "hbm",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "algorithmic_bytes_per_launch": warp_bytes, "avg_launch_ms": iso["warp"],
+                     "note": "slab 0's warp alone (median of per-dispatch HIP events)"},
+    }
+    return result
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -414,6 +471,11 @@ def main():
     ap.add_argument("--detect", action="store_true",
                     help="also time align from raw uint16 frames on the device: normalisation + ORB-style "
                          "detection + the hot path (pipeline.align_frames); reported as `with_detection`")
+    ap.add_argument("--single-process", action="store_true",
+                    help="one process over --gpus devices (or --devices): the drop-in VideoAligner's split path "
+                         "(kcmc_amd.multidevice), not the torchrun one-process-per-GPU path")
+    ap.add_argument("--devices", default=None,
+                    help="with --single-process: comma-separated device list, a device may repeat (e.g. 0,0)")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
@@ -426,6 +488,12 @@ def main():
         # at least 4 frames per process, within the frames the config makes
         args.cpu_sample = min(max(bc.cpu_sample * max(1, args.cpu_procs) // 2, 4 * args.cpu_procs),
                               args.frames if args.frames else bc.frames_per_gpu)
+
+    if args.single_process:
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            raise SystemExit("--single-process runs in one process (not under torchrun)")
+        print(json.dumps(single_process(args, bc)), flush=True)
+        return
 
     # KCMC_BENCH_BACKEND=gloo + KCMC_BENCH_ONE_DEVICE=1: rehearsal of the multi-rank
     # path with every rank on cuda:0 (a 1-GPU box cannot host two RCCL ranks)

@@ -797,26 +797,39 @@ def _numpy_linear_percentile(n: int, q: float, value_at) -> np.float64:
     return np.float64(np.add(a, diff * gamma))
 
 
-def brightest_px(frames: torch.Tensor, percentile: float = 99.99) -> np.float64:
+def brightest_px(frames, percentile: float = 99.99) -> np.float64:
     """VA:479-482 on the device: np.percentile(images, 99.99) of a uint16 stack, exact
-    (two order statistics from two histogram passes, numpy's interpolation on the host)."""
-    dev = _device_of(frames)
-    _require(frames, "frames", torch.uint16, dev)
-    n = frames.numel()
+    (two order statistics from two histogram passes, numpy's interpolation on the host).
+    ``frames``: one device tensor, or the slabs of one stack on several devices (their
+    histograms are summed: the percentile of the whole stack)."""
+    parts = [frames] if isinstance(frames, torch.Tensor) else list(frames)
+    for p in parts:
+        _require(p, "frames", torch.uint16, _device_of(p))
+    n = sum(p.numel() for p in parts)
     if n == 0:
         raise ValueError("percentile of an empty stack")
     L = _lib.load()
-    ctx = _ctx(dev).handle
-    hist = torch.empty(256, dtype=torch.int64, device=dev)
-    _lib.check(L.kcmc_histogram_u16(ctx, _ptr(frames), n, 8, -1, _ptr(hist), _stream(dev)))
-    coarse = np.cumsum(hist.cpu().numpy())
+
+    def histogram(shift: int, hb: int) -> np.ndarray:
+        hs = []
+        for p in parts:  # queued on every device before the first host read
+            dev = _device_of(p)
+            h = torch.empty(256, dtype=torch.int64, device=dev)
+            if p.numel():
+                _lib.check(L.kcmc_histogram_u16(_ctx(dev).handle, _ptr(p), p.numel(), shift, hb, _ptr(h),
+                                                _stream(dev)))
+            else:
+                h.zero_()
+            hs.append(h)
+        return np.sum([h.cpu().numpy() for h in hs], axis=0)
+
+    coarse = np.cumsum(histogram(8, -1))
     fine_cache = {}
 
     def value_at(rank: int) -> int:
         hb = int(np.searchsorted(coarse, rank, side="right"))
         if hb not in fine_cache:
-            _lib.check(L.kcmc_histogram_u16(ctx, _ptr(frames), n, 0, hb, _ptr(hist), _stream(dev)))
-            fine_cache[hb] = np.cumsum(hist.cpu().numpy())
+            fine_cache[hb] = np.cumsum(histogram(0, hb))
         below = int(coarse[hb - 1]) if hb > 0 else 0
         lb = int(np.searchsorted(fine_cache[hb], rank - below, side="right"))
         return (hb << 8) | lb

@@ -30,6 +30,7 @@ import numpy as np
 import torch
 
 from . import affines as _aff
+from . import multidevice as _md
 from . import pipeline as _pl
 from . import stages
 from .affines import AlignmentError
@@ -107,7 +108,15 @@ class VideoAligner:
     RANSAC_RESIDUAL_THRESH = 2
     RANSAC_MAX_TRIALS = 1000
     RANDOM_SEED = 42
-    # New: which GPU runs the hot path (None = torch's current device).
+    # New: the GPUs align_images / align_keypoints spread the frames over, as the
+    # reference's _parallelize spreads them over every core (VA:21, VA:460-471): None = every
+    # visible device (the current one first; one contiguous frame slab per device, the
+    # cross-frame consensus and gap interpolation made once on the host, kcmc_amd.multidevice);
+    # a list pins them (a device may repeat: two slabs on one GPU).
+    DEVICES: Optional[Sequence[int]] = None
+    # New: one GPU for everything (used when DEVICES is None; None = as DEVICES).  The
+    # per-frame helpers (_get_frame_keypoints, _compute_euclidean_affine, _apply_affine)
+    # run on the first device.
     DEVICE: Optional[int] = None
     # New (extension, BASELINE configs 3-5): the skimage model class RANSAC fits --
     # "euclidean" (the reference's EuclideanTransform, VA:311), "affine"
@@ -131,13 +140,26 @@ class VideoAligner:
 
     # ------------------------------------------------------------------ helpers
     @classmethod
-    def _device(cls) -> torch.device:
+    def _devices(cls) -> List[int]:
+        """The devices of the hot path: DEVICES, else [DEVICE], else every visible device
+        with the current one first."""
         if not torch.cuda.is_available():
             from ._lib import KcmcLibraryError
 
             raise KcmcLibraryError("no GPU visible: the kcmc hot path runs on MI355X only (no CPU fallback)")
-        idx = cls.DEVICE if cls.DEVICE is not None else torch.cuda.current_device()
-        return torch.device("cuda", idx)
+        if cls.DEVICES is not None:
+            devs = [int(d) for d in cls.DEVICES]
+            if not devs:
+                raise ValueError("VideoAligner.DEVICES is empty")
+            return devs
+        if cls.DEVICE is not None:
+            return [int(cls.DEVICE)]
+        cur = torch.cuda.current_device()
+        return [cur] + [d for d in _md.visible_devices() if d != cur]
+
+    @classmethod
+    def _device(cls) -> torch.device:
+        return torch.device("cuda", cls._devices()[0])
 
     def _config(self, n_kp_global: int, frame_downsample_rate: int = 1) -> _pl.AlignConfig:
         cls = type(self)
@@ -177,6 +199,13 @@ class VideoAligner:
             template = _as_numpy(images[template_idx])
             self.logger.info(f"no masked template provided. Using frame {template_idx} as template")
 
+        frame_downsample_rate = max(1, frame_rate // self.FRAME_SAMPLE_RATE)
+        devices = self._devices()
+        ranges = _md.split_frames(len(images), frame_downsample_rate, len(devices))
+        if len(ranges) > 1:
+            return self._align_images_split(images, template, n_kp_global, detector_algorithm, frame_downsample_rate,
+                                            patch, devices[:len(ranges)], ranges)
+
         self.logger.info("normalizing frames...")
         t_start = time.time()
         # VA:100-108 on the device: the stack is uploaded once (and reused by the warp),
@@ -188,7 +217,6 @@ class VideoAligner:
         brightest_px = self._get_brightest_px(frames)
         u8_dev = self._max_scale_images(frames, None, brightest_px, np.uint8)[0]
         _, template_i8 = self._max_scale_images(None, template, brightest_px, np.uint8)
-        frame_downsample_rate = max(1, frame_rate // self.FRAME_SAMPLE_RATE)
         detector = self.DETECTOR_CONSTRUCTOR_DICT[detector_algorithm]()
         on_gpu = isinstance(detector, GpuOrbDetector) and frames.dim() == 3
         if not on_gpu:
@@ -228,6 +256,77 @@ class VideoAligner:
             aligned = aligned.cpu().numpy()
         return aligned, eu, skipped
 
+    def _align_images_split(self, images, template, n_kp_global, detector_algorithm, rate, patch, devices, ranges):
+        """align_images with the stack split over several devices (kcmc_amd.multidevice):
+        each slab's frames uploaded to its device, the 99.99th percentile of the whole stack
+        from the summed per-device histograms, max-scaling and (GPU detector) detection per
+        device, then the split hot path."""
+        on_device = isinstance(images, torch.Tensor)
+        self.logger.info("normalizing frames...")
+        t_start = time.time()
+        assert (images.dtype == torch.uint16) if on_device else (np.asarray(images).dtype == np.uint16)  # VA:104
+        parts = _md.split_to_devices(images if on_device else np.asarray(images), ranges, devices)
+        brightest_px = stages.brightest_px(parts, self.IMAGE_NORM_MAX_PERCENTILE)
+        u8_parts = [self._max_scale_images(p, None, brightest_px, np.uint8)[0] for p in parts]
+        _, template_i8 = self._max_scale_images(None, template, brightest_px, np.uint8)
+        detector = self.DETECTOR_CONSTRUCTOR_DICT[detector_algorithm]()
+        on_gpu = isinstance(detector, GpuOrbDetector) and parts[0].dim() == 3
+        self.logger.info(f"normalized frames in: {round(time.time() - t_start)} s")
+
+        self.logger.info("identifying keypoints...")
+        t_start = time.time()
+        cfg = self._config(n_kp_global, rate)
+        if on_gpu:  # f1 per device: each slab's sample frames detected where they live
+            tpl_u8 = np.ascontiguousarray(template_i8)
+            samples = [_pl.downsample_u8(u, torch.from_numpy(tpl_u8).to(u.device)[None], rate,
+                                         self.SPATIAL_DOWNSAMPLE_RATE) for u in u8_parts]
+            kt = stages.detect_orb(samples[0][1], detector.params)
+            n_t = int(kt.count.cpu()[0])
+            self._kp_template = kt.kp[0, :n_t].cpu().numpy()
+            self._des_template = kt.des[0, :n_t].cpu().numpy()
+            slabs = []
+            for fr, (smp, _) in zip(parts, samples):
+                kp_q, des_q, q_off, q_off_host = stages.keypoints_csr(stages.detect_orb(smp, detector.params))
+                dev = fr.device
+                slabs.append(_pl.SlabInputs(fr, torch.from_numpy(self._des_template).to(dev),
+                                            torch.from_numpy(self._kp_template).to(dev), des_q, kp_q, q_off, q_off_host))
+        else:
+            images_i8 = np.concatenate([u.cpu().numpy() for u in u8_parts])
+            images_sample, template = self._downsample(images_i8, template_i8, rate, self.SPATIAL_DOWNSAMPLE_RATE)
+            kp_t, des_t = detector.detectAndCompute(template, None)
+            self._kp_template = np.array([p.pt for p in kp_t])
+            self._des_template = des_t
+            kp_list, des_list = [], []
+            for img in images_sample:
+                kq, dq = detector.detectAndCompute(img, None)
+                kp_list.append(np.array([p.pt for p in kq], dtype=np.float64).reshape(-1, 2))
+                des_list.append(np.asarray(dq, dtype=np.uint8).reshape(len(kq), -1))
+            kp_flat, des_flat, q_off = self._csr(kp_list, des_list, np.asarray(des_t).shape[1])
+            slabs = _md.make_slabs(parts, ranges, np.asarray(des_t, np.uint8), self._kp_template, kp_flat, des_flat,
+                                   q_off)
+        self.logger.info(f"identified keypoints in: {round(time.time() - t_start)} s")
+        return self._finish_split(slabs, ranges, cfg, patch, images.device if on_device else None)
+
+    def _finish_split(self, slabs, ranges, cfg, patch, out_device):
+        self.logger.info("generating keypoint consensus...")
+        t_start = time.time()
+        res = _md.align_split(slabs, ranges, cfg, logger=self.logger)
+        self.interpolated_idxs = res.interpolated
+        self.logger.info(f"aligned frames in: {round(time.time() - t_start)} s")
+        aligned = _md.gather_aligned(res, out_device)
+        if patch is not None:
+            x_start, y_start, width, height = patch
+            aligned = aligned[:, x_start:x_start + width, y_start:y_start + height]
+        return aligned, res.euclidean, res.skipped
+
+    @staticmethod
+    def _csr(kp_list, des_list, D):
+        q_off = np.zeros(len(kp_list) + 1, np.int32)
+        q_off[1:] = np.cumsum([len(k) for k in kp_list])
+        kp_flat = np.concatenate(kp_list).astype(np.float64) if q_off[-1] else np.zeros((0, 2))
+        des_flat = np.concatenate(des_list).astype(np.uint8) if q_off[-1] else np.zeros((0, D), np.uint8)
+        return kp_flat, des_flat, q_off
+
     def align_keypoints(
         self,
         images,
@@ -249,14 +348,17 @@ class VideoAligner:
                                     n_kp_global, rate, patch)
 
     def _align_detected(self, images, kp_template, des_template, kp_list, des_list, n_kp_global, rate, patch):
-        dev = self._device()
         to_host = not isinstance(images, torch.Tensor)
+        kp_flat, des_flat, q_off = self._csr(kp_list, des_list, des_template.shape[1])
+        devices = self._devices()
+        ranges = _md.split_frames(len(images), rate, len(devices))
+        if len(ranges) > 1:  # every device its slab of frames (kcmc_amd.multidevice)
+            parts = _md.split_to_devices(images if not to_host else np.asarray(images), ranges, devices)
+            slabs = _md.make_slabs(parts, ranges, des_template, kp_template, kp_flat, des_flat, q_off)
+            return self._finish_split(slabs, ranges, self._config(n_kp_global, rate), patch,
+                                      None if to_host else images.device)
+        dev = torch.device("cuda", devices[0])
         frames = torch.from_numpy(np.ascontiguousarray(images)).to(dev) if to_host else images.contiguous()
-        q_off = np.zeros(len(kp_list) + 1, np.int32)
-        q_off[1:] = np.cumsum([len(k) for k in kp_list])
-        D = des_template.shape[1]
-        kp_flat = np.concatenate(kp_list).astype(np.float64) if q_off[-1] else np.zeros((0, 2))
-        des_flat = np.concatenate(des_list).astype(np.uint8) if q_off[-1] else np.zeros((0, D), np.uint8)
         inp = _pl.SlabInputs(
             frames=frames,
             des_tpl=torch.from_numpy(np.ascontiguousarray(des_template, np.uint8)).to(dev),
