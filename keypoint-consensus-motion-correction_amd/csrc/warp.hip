@@ -301,12 +301,13 @@ __device__ __forceinline__ uint16_t round_q10(uint32_t S) {
 
 __device__ __forceinline__ uint32_t tap(const uint16_t* stile, int i) { return stile[i]; }
 
-// Bits 11-15 of v in one v_bfe_u32 (the backend otherwise selects a shift and a mask).
-__device__ __forceinline__ uint32_t bfe_11_5(uint32_t v) {
-  uint32_t r;
-  asm("v_bfe_u32 %0, %1, 11, 5" : "=v"(r) : "v"(v));
-  return r;
-}
+// Bits 11-15 of v in one v_bfe_u32 (a shift and a mask otherwise).  The builtin, not inline
+// asm: the compiler pads the wait state a VALU write of a VGPR needs after a wider-than-8-byte
+// store that reads it as data, but not around inline asm -- the round-4 inline-asm form landed
+// right behind the RGB path's buffer_store_dwordx3 and overwrote its first data VGPR, an
+// intermittent wrong pixel pair (tools/debug/store_hazard_scan.py checks the
+// built library for that pattern).
+__device__ __forceinline__ uint32_t bfe_11_5(uint32_t v) { return __builtin_amdgcn_ubfe(v, 11, 5); }
 
 
 // Fast-path staging: chunk q = tid + 256k of the box in row-major order at kFastChunks
@@ -1006,7 +1007,8 @@ template <class Cfg>
 struct PerspTab {
   static constexpr int kEntries = Cfg::kTileH * 2;                  // (row, block)
   static constexpr int kElems = kEntries * 3 * 4;                   // u16 elements of 3 doubles each
-  static constexpr int kBoxElems = Cfg::kLdsElems - kElems;         // the staged box's budget
+  static constexpr int kFlagWord = Cfg::kLdsElems / 2 - 4;          // the last 16 bytes: per-wave flags
+  static constexpr int kBoxElems = Cfg::kLdsElems - 8 - kElems;     // the staged box's budget
   static_assert((kBoxElems * 2) % 8 == 0, "table alignment");
 };
 
@@ -1118,6 +1120,16 @@ __device__ __forceinline__ int rint_small(double x) {
   return (int)(uint32_t)__double_as_longlong(x + 0x1.8p52);
 }
 
+// The staged path's coordinates relative to the box origin (cx = 1.5 * 2^52 - 32 ax0,
+// cy = 1.5 * 2^52 - 32 sy0): the low word of fl(fX) + cx is rint(fX) - 32 ax0, because the
+// constant is an even integer in the binade of unit ulp (the add's tie-to-even is rint's).
+__device__ __forceinline__ void persp_px_box(double X0, double Y0, double W0, double m0x1, double m3x1, double m6x1,
+                                             double cx, double cy, uint32_t& X, uint32_t& Y) {
+  const double w = div32_in_range(W0 + m6x1);
+  X = (uint32_t)__double_as_longlong((X0 + m0x1) * w + cx);
+  Y = (uint32_t)__double_as_longlong((Y0 + m3x1) * w + cy);
+}
+
 template <bool IN_RANGE>
 __device__ __forceinline__ void persp_px(double X0, double Y0, double W0, double m0x1, double m3x1, double m6x1,
                                          int& X, int& Y) {
@@ -1139,7 +1151,9 @@ __device__ __forceinline__ void persp_px(double X0, double Y0, double W0, double
   Y = (int)__builtin_rint(fY);
 }
 
-template <class Cfg, int C, int MODE, bool TAB>
+// DARK (MODE 0, C == 1): every staged value is < 16384, so the exact integer blend needs no
+// range check (as kDark of the affine fast path).
+template <class Cfg, int C, int MODE, bool TAB, bool DARK = false>
 __device__ __forceinline__ void persp_rows(const uint16_t* stile, const Box& box, const uint16_t* __restrict__ S,
                                            uint16_t* __restrict__ Dst, const double* M, int H, int W, int xb, int yb,
                                            int wave, int lane, int bw0, const double* ptab) {
@@ -1162,6 +1176,14 @@ __device__ __forceinline__ void persp_rows(const uint16_t* stile, const Box& box
   }
   const bool one_block = xo[0] == xo[1];  // the pair straddles a block edge only for odd bw0
   const double mx0 = M[0] * dxo[0], mx3 = M[3] * dxo[0], mx6 = M[6] * dxo[0];
+  // MODE 0, C == 1: box-relative fixed-point taps; (column, row) packed as two u16 from the
+  // coordinates shifted by 11 (bits 16+: the pixel, bits 11-15: the 1/32 fraction) and the
+  // LDS byte offset as one v_dot2 with (2, 2 pitch) -- as fast_rows (the generic form costs a
+  // quarter-rate v_mul_lo_u32 and two more subtractions per tap)
+  const double cx = 0x1.8p52 - 32.0 * box.ax0, cy = 0x1.8p52 - 32.0 * box.sy0;
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 pitch2 = {(unsigned short)2, (unsigned short)(2 * box.pitch)};
+  const char* sbytes = reinterpret_cast<const char*>(stile);
 #pragma unroll
   for (int i = 0; i < Cfg::kTileH / 4; ++i) {
     const int y = yb + wave + 4 * i;  // wave-uniform
@@ -1192,11 +1214,31 @@ __device__ __forceinline__ void persp_rows(const uint16_t* stile, const Box& box
     }
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
+      if constexpr (MODE == 0 && C == 1) {
+        uint32_t X, Y;
+        persp_px_box(X0[p], Y0[p], W0[p], m0x1[p], m3x1[p], m6x1[p], cx, cy, X, Y);
+        const uint32_t tX = X << 11, tY = Y << 11;
+        const uint32_t cr = __builtin_amdgcn_perm(tY, tX, 0x07060302u);  // (column, row) as u16 x 2
+        const uint32_t off = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, cr), pitch2, 0u, false);
+        const uint16_t* t = reinterpret_cast<const uint16_t*>(sbytes + off);
+        const uint32_t fx = X & 31, fy = Y & 31;
+        const uint32_t v00 = t[0], v01 = t[1], v10 = t[box.pitch], v11 = t[box.pitch + 1];
+        if constexpr (DARK) {
+          const uint32_t ax = 32 - fx, ay = 32 - fy;
+          uint32_t h0 = __umul24(v00, ax) + __umul24(v01, fx);
+          uint32_t h1 = __umul24(v10, ax) + __umul24(v11, fx);
+          asm volatile("" : "+v"(h0), "+v"(h1));  // keep the separable form (see output_rows)
+          o[p] = round_q10(__umul24(h0, ay) + __umul24(h1, fy));
+        } else {
+          o[p] = blend_exact(v00, v01, v10, v11, (int)fx, (int)fy);
+        }
+        continue;
+      }
       int X, Y;
       persp_px<MODE == 0>(X0[p], Y0[p], W0[p], m0x1[p], m3x1[p], m6x1[p], X, Y);
       if (MODE == 0) {
         const int fx = X & 31, fy = Y & 31;
-        const int li = ((Y >> 5) - box.sy0) * box.pitch + ((X >> 5) - box.ax0);
+        const int li = (int)__umul24((uint32_t)((Y >> 5) - box.sy0), (uint32_t)box.pitch) + ((X >> 5) - box.ax0);
 #pragma unroll
         for (int k = 0; k < C; ++k) {
           const int i00 = li * C + k, i10 = i00 + box.pitch * C;
@@ -1266,9 +1308,17 @@ warp_perspective_u16_kernel(const uint16_t* __restrict__ src, uint16_t* __restri
       ptab[3 * e + 2] = M[6] * dxo + M[7] * dy + M[8];
     }
   }
+  uint32_t* flags = reinterpret_cast<uint32_t*>(stile) + PerspTab<Cfg>::kFlagWord;
   if (box.mode == 0) {
     if (vec_stage) {
       stage_land<Cfg>(stile, box, tid, chunk);
+      // bright (>= 16384) staged chunks of the box, counted per wave into the flag words
+      uint32_t nb = 0;
+#pragma unroll
+      for (int k = 0; k < Cfg::kRowPasses; ++k)
+        nb += __builtin_popcountll(
+            __builtin_amdgcn_ballot_w64(((chunk[k].x | chunk[k].y | chunk[k].z | chunk[k].w) & 0xc000c000u) != 0));
+      if (lane == 0) flags[wave] = nb;
     } else if (C > 1 && (W & 7) == 0) {
       if constexpr (C > 1) stage_vec_c_land<Cfg, C>(stile, box, tid, cchunk);
     } else
@@ -1278,9 +1328,13 @@ warp_perspective_u16_kernel(const uint16_t* __restrict__ src, uint16_t* __restri
   if (box.mode == 1)
     persp_rows<Cfg, C, 1, false>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0, ptab);
   else if (tab) {
-    if (box.mode == 0)
-      persp_rows<Cfg, C, 0, true>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0, ptab);
-    else
+    if (box.mode == 0) {
+      const uint4 fl = *reinterpret_cast<const uint4*>(flags);
+      if (vec_stage && fl.x + fl.y + fl.z + fl.w == 0)
+        persp_rows<Cfg, C, 0, true, true>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0, ptab);
+      else
+        persp_rows<Cfg, C, 0, true>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0, ptab);
+    } else
       persp_rows<Cfg, C, 2, true>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0, ptab);
   } else if (box.mode == 0) {
     persp_rows<Cfg, C, 0, false>(stile, box, S, Dst, M, H, W, xb, yb, wave, lane, bw0, ptab);
