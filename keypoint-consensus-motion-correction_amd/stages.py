@@ -797,6 +797,13 @@ def _numpy_linear_percentile(n: int, q: float, value_at) -> np.float64:
     return np.float64(np.add(a, diff * gamma))
 
 
+def _aligned16(t: torch.Tensor) -> torch.Tensor:
+    """``t`` itself when its data is 16-byte aligned (the histogram / LUT kernels read 16
+    bytes per lane), else an aligned copy: a frame slab that starts mid-allocation (a view
+    of a stack whose frame size is not a multiple of 16 bytes)."""
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
 def brightest_px(frames, percentile: float = 99.99) -> np.float64:
     """VA:479-482 on the device: np.percentile(images, 99.99) of a uint16 stack, exact
     (two order statistics from two histogram passes, numpy's interpolation on the host).
@@ -805,6 +812,7 @@ def brightest_px(frames, percentile: float = 99.99) -> np.float64:
     parts = [frames] if isinstance(frames, torch.Tensor) else list(frames)
     for p in parts:
         _require(p, "frames", torch.uint16, _device_of(p))
+    parts = [_aligned16(p) for p in parts]
     n = sum(p.numel() for p in parts)
     if n == 0:
         raise ValueError("percentile of an empty stack")
@@ -855,8 +863,11 @@ def max_scale_u8(frames: torch.Tensor, brightest: float, out: Optional[torch.Ten
         if out.shape != frames.shape:
             raise ValueError("out must have the shape of frames")
     lut = torch.from_numpy(max_scale_lut(float(brightest), max_px)).to(dev)
-    _lib.check(_lib.load().kcmc_lut_u16_to_u8(_ctx(dev).handle, _ptr(frames), frames.numel(), _ptr(lut), _ptr(out),
-                                              _stream(dev)))
+    res = out if out.data_ptr() % 16 == 0 else torch.empty_like(out)
+    _lib.check(_lib.load().kcmc_lut_u16_to_u8(_ctx(dev).handle, _ptr(_aligned16(frames)), frames.numel(), _ptr(lut),
+                                              _ptr(res), _stream(dev)))
+    if res is not out:
+        out.copy_(res)
     return out
 
 

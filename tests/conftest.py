@@ -35,7 +35,7 @@ def pytest_collection_modifyitems(config, items):
 def distinct_frames(base, F):
     """F frames with pairwise different content: the base texture rolled by (37 f, 53 f)
     pixels, so that a tile that read another frame's staged data cannot match by accident."""
-    return np.stack([np.roll(base, (37 * f, 53 * f), axis=(0, 1)) for f in range(F)])
+    return np.ascontiguousarray(np.stack([np.roll(base, (37 * f, 53 * f), axis=(0, 1)) for f in range(F)]))
 
 
 def load_golden(name):

@@ -28,11 +28,12 @@ def _keypoint_stack(n_sample, rate, model, blind, seed=61):
     H, W = 96, 160
     ks = synthetic.make_keypoints(n_sample, 150, 32, (H, W), seed=seed, model=model)
     rng = np.random.default_rng(seed)
-    for f in blind:  # no model for these sample frames: a NaN gap to interpolate
+    for f in blind:  # every descriptor one row: no match passes the ratio test (d1 == d2), no model
         a, b = ks.q_off[f], ks.q_off[f + 1]
-        ks.des_q[a:b] = rng.integers(0, 256, (b - a, 32), dtype=np.uint8)
+        ks.des_q[a:b] = rng.integers(0, 256, (1, 32), dtype=np.uint8)
     base = synthetic.make_texture((H, W), seed=seed)
-    frames = np.stack([np.roll(base, (2 * f, 5 * f), axis=(0, 1)) for f in range(n_sample * rate - rate // 2)])
+    frames = np.ascontiguousarray(np.stack([np.roll(base, (2 * f, 5 * f), axis=(0, 1))
+                                            for f in range(n_sample * rate - rate // 2)]))
     kq = [ks.kp_q[ks.q_off[f]:ks.q_off[f + 1]] for f in range(n_sample)]
     dq = [ks.des_q[ks.q_off[f]:ks.q_off[f + 1]] for f in range(n_sample)]
     return ks, frames, kq, dq
@@ -74,7 +75,12 @@ def test_brightest_px_over_parts_equals_whole(dev):
     x[2, 3, 4] = 65535
     whole = torch.from_numpy(x).to(dev)
     parts = [whole[:3], whole[3:3], whole[3:]]
-    assert stages.brightest_px(parts) == stages.brightest_px(whole) == np.percentile(x, 99.99)
+    b = stages.brightest_px(parts)
+    assert b == stages.brightest_px(whole) == np.percentile(x, 99.99)
+    # a slab that starts mid-allocation (3 frames of 33 x 41 u16 = 8118 bytes in): the
+    # 16-byte kernels work on an aligned copy
+    assert whole[3:].data_ptr() % 16 != 0
+    np.testing.assert_array_equal(stages.max_scale_u8(whole[3:], b).cpu().numpy(), stages.max_scale_lut(b)[x[3:]])
 
 
 def test_align_images_gpu_detector_split(dev):

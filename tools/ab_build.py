@@ -2,7 +2,8 @@
 same-box A/B runs: KCMC_LIB_PATH=ab/<name>.so python tools/match_rates.py ...
 
     python tools/ab_build.py <name> [<git-rev>]     (no rev: the working tree)
-    KCMC_AB_FLAGS="-DKCMC_FASTC_PITCH=192" python tools/ab_build.py p192   (extra compile flags)
+    KCMC_AB_FLAGS="-DKCMC_WARP_SENTINEL" python tools/ab_build.py sentinel   (extra compile flags)
+    KCMC_AB_PATCH=tools/ab_patches/knn_grid.py python tools/ab_build.py knn_half  (edit the copy first)
 """
 import os
 import shutil
@@ -38,6 +39,9 @@ def main():
                 open(dst, "wb").write(r.stdout)
             else:
                 shutil.copy(os.path.join(REPO, f), dst)
+        patch = os.environ.get("KCMC_AB_PATCH")  # a script that edits the copied csrc/ (argv[1]) for this build
+        if patch:
+            subprocess.run([sys.executable, patch, csrc], check=True)
         srcs = [s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))]
         flags = [f if not f.startswith("-I") else f"-I{os.path.join(tmp, 'include')}" for f in B.COMMON_FLAGS]
         flags += os.environ.get("KCMC_AB_FLAGS", "").split()  # e.g. -DKCMC_FASTC_PITCH=192
