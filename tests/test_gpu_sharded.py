@@ -37,12 +37,13 @@ def _keypoints(rank: int, slab: int, model: str, world: int = 2, blind: bool = F
     return ks
 
 
-def _frames(n: int):
+def _frames(n: int, f0: int = 0):
+    """Frames f0 .. f0 + n - 1 of the job, each with its own content (global index f)."""
     base = synthetic.make_texture(HW, seed=4)
-    return np.stack([np.roll(base, (5 * f, 11 * f), axis=(0, 1)) for f in range(n)])  # per-frame content
+    return np.ascontiguousarray(np.stack([np.roll(base, (5 * f, 11 * f), axis=(0, 1)) for f in range(f0, f0 + n)]))
 
 
-def _inputs(ks_list, dev):
+def _inputs(ks_list, dev, f0: int = 0):
     """SlabInputs of the concatenation of several ranks' keypoint sets."""
     des_q = np.concatenate([k.des_q for k in ks_list])
     kp_q = np.concatenate([k.kp_q for k in ks_list])
@@ -52,7 +53,7 @@ def _inputs(ks_list, dev):
     q_off = np.asarray(off, np.int32)
     n = len(q_off) - 1
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-    return pipeline.SlabInputs(t(_frames(n)), t(ks_list[0].des_tpl), t(ks_list[0].kp_tpl), t(des_q), t(kp_q),
+    return pipeline.SlabInputs(t(_frames(n, f0)), t(ks_list[0].des_tpl), t(ks_list[0].kp_tpl), t(des_q), t(kp_q),
                                t(q_off), q_off)
 
 
@@ -67,7 +68,8 @@ def _rank_main(rank: int, port: int, out_dir: str, model: str, world: int, blind
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     cfg = pipeline.AlignConfig(n_kp_global=N_KP_GLOBAL, ransac_model=model)
-    slabs = [_inputs([_keypoints(rank, s, model, world, blind)], dev) for s in range(3)]
+    f0 = sum(COUNTS[world][:rank])
+    slabs = [_inputs([_keypoints(rank, s, model, world, blind)], dev, f0) for s in range(3)]
     for inp in slabs:
         if rank != 0:  # only rank 0 holds the template; the others receive it
             inp.des_tpl.zero_()
