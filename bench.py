@@ -401,7 +401,7 @@ def single_process(args, bc: BenchConfig) -> dict:
     consensus merge and the gap interpolation once on the host per step.  Steps are not
     pipelined across each other (each align_split call returns the aligned frames), which is
     what a caller of VideoAligner.align_keypoints with device-resident frames gets."""
-    devices = [int(d) for d in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    devices = [int(d) for d in args.devices.replace("+", ",").split(",")] if args.devices else list(range(args.gpus))
     cfg = pipeline.AlignConfig(n_kp_global=bc.n_kp_global, ransac_model=bc.model)
     slabs, ranges = [], []
     for k, d in enumerate(devices):
@@ -475,7 +475,7 @@ def main():
                     help="one process over --gpus devices (or --devices): the drop-in VideoAligner's split path "
                          "(kcmc_amd.multidevice), not the torchrun one-process-per-GPU path")
     ap.add_argument("--devices", default=None,
-                    help="with --single-process: comma-separated device list, a device may repeat (e.g. 0,0)")
+                    help="with --single-process: device list separated by , or +, a device may repeat (e.g. 0+0)")
     ap.add_argument("--serial", action="store_true",
                     help="run steps back to back on one stream (no warp/analysis overlap between steps)")
     args = ap.parse_args()
