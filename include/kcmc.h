@@ -358,6 +358,22 @@ int kcmc_warp_perspective_u16(kcmc_ctx* ctx, const uint16_t* src_dev, uint16_t* 
                               const double* M_dev, int n_frames, int H, int W, int C, int inverse_map,
                               kcmc_stream_t stream);
 
+/* The warp in two parts (round 5): the plan -- OpenCV's map inversion, every tile's
+ * source box and (affine) the per-frame row-origin table -- into a caller-owned device
+ * buffer plan_dev of at least kcmc_warp_plan_bytes(...) bytes (16-byte aligned), queued
+ * where the maps are produced, then the tiles, queued later (the caller orders them after
+ * the plan and keeps plan_dev alive until they have run).  perspective != 0: M_dev
+ * [n_frames, 3, 3] and warpPerspective, else [n_frames, 2, 3] and warpAffine.  Results are
+ * those of kcmc_warp_affine_u16 / kcmc_warp_perspective_u16 (which run both parts on one
+ * stream).  The pipeline queues the plan on its analysis stream right behind RANSAC, so
+ * the kernel stream goes from one slab's warp tiles straight to the next slab's.
+ * kcmc_warp_plan_bytes returns -1 for unsupported sizes. */
+long long kcmc_warp_plan_bytes(int n_frames, int H, int W, int C, int perspective);
+int kcmc_warp_u16_plan(kcmc_ctx* ctx, const double* M_dev, int n_frames, int H, int W, int C, int perspective,
+                       int inverse_map, void* plan_dev, long long plan_bytes, kcmc_stream_t stream);
+int kcmc_warp_u16_planned(kcmc_ctx* ctx, const uint16_t* src_dev, uint16_t* dst_dev, const void* plan_dev,
+                          int n_frames, int H, int W, int C, int perspective, kcmc_stream_t stream);
+
 /* ------------------------------------------- f2: normalisation front end (VA:100-104)
  * brightest = np.percentile(images, 99.99) (VA:479-482) needs two order statistics of
  * the flattened uint16 stack; they come from two streaming 256-bin histogram passes:

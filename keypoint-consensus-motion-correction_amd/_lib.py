@@ -59,6 +59,9 @@ EXPORTED_SYMBOLS = (
     "kcmc_ransac_model_grid",
     "kcmc_warp_affine_u16",
     "kcmc_warp_perspective_u16",
+    "kcmc_warp_plan_bytes",
+    "kcmc_warp_u16_plan",
+    "kcmc_warp_u16_planned",
     "kcmc_histogram_u16",
     "kcmc_lut_u16_to_u8",
     "kcmc_orb_detect",
@@ -130,6 +133,9 @@ _SIGNATURES = {
     "kcmc_ransac_model_grid": ([P, I, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, I, P], I),
     "kcmc_warp_affine_u16": ([P, P, P, P, I, I, I, I, I, P], I),
     "kcmc_warp_perspective_u16": ([P, P, P, P, I, I, I, I, I, P], I),
+    "kcmc_warp_plan_bytes": ([I, I, I, I, I], ctypes.c_longlong),
+    "kcmc_warp_u16_plan": ([P, P, I, I, I, I, I, I, P, ctypes.c_longlong, P], I),
+    "kcmc_warp_u16_planned": ([P, P, P, P, I, I, I, I, I, P], I),
     "kcmc_histogram_u16": ([P, P, ctypes.c_ulonglong, I, I, P, P], I),
     "kcmc_lut_u16_to_u8": ([P, P, ctypes.c_ulonglong, P, P, P], I),
     "kcmc_orb_detect": ([P, P, I, I, I, I, I, D, I, P, P, P, P, P, P], I),

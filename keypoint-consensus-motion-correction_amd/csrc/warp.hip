@@ -950,20 +950,44 @@ size_t warp_workspace_bytes(int n_frames, int H, int W) {
          (size_t)n_frames * 4 * rowtab_hq(H) * sizeof(int2);
 }
 
+// Workspace layout of the affine warp: minv [F, 6] f64, rowtab [F, 4, hq] int2, plan [tiles].
+template <class Cfg>
+struct WarpWs {
+  double* minv;
+  int2* rowtab;
+  TilePlan* plan;
+  int hq;
+  WarpWs(void* ws, int n_frames, int H) {
+    minv = static_cast<double*>(ws);
+    hq = rowtab_hq(H);
+    rowtab = reinterpret_cast<int2*>(minv + 6 * (size_t)n_frames);
+    plan = reinterpret_cast<TilePlan*>(rowtab + (size_t)n_frames * 4 * hq);
+  }
+};
+
+template <int C, class Cfg = typename CfgFor<C>::type>
+void launch_warp_plan(const double* M, int n_frames, int H, int W, int inverse_map, void* ws, hipStream_t s) {
+  const int ntx = ceil_div(W, kTileW), nty = ceil_div(H, Cfg::kTileH);
+  const long long tiles = (long long)ntx * nty * n_frames;
+  const WarpWs<Cfg> w(ws, n_frames, H);
+  hipLaunchKernelGGL((warp_plan_kernel<C, Cfg>), dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, s, M, n_frames,
+                     H, W, inverse_map, ntx, nty, w.plan, w.minv, w.rowtab, w.hq);
+}
+
+template <int C, class Cfg = typename CfgFor<C>::type>
+void launch_warp_tiles(const uint16_t* src, uint16_t* dst, int n_frames, int H, int W, const void* ws, hipStream_t s) {
+  const int ntx = ceil_div(W, kTileW), nty = ceil_div(H, Cfg::kTileH);
+  const WarpWs<Cfg> w(const_cast<void*>(ws), n_frames, H);
+  hipLaunchKernelGGL((warp_affine_u16_kernel<C, Cfg>), dim3(ntx, nty, n_frames), dim3(kThreads), 0, s, src,
+                     dst, w.plan, w.minv, w.rowtab, w.hq, H, W);
+}
+
 // Plan + tile launches on `s`; ws holds warp_workspace_bytes<Cfg>(n_frames, H, W) bytes.
 template <int C, class Cfg = typename CfgFor<C>::type>
 void launch_warp(const uint16_t* src, uint16_t* dst, const double* M, int n_frames, int H, int W, int inverse_map,
                  void* ws, hipStream_t s) {
-  const int ntx = ceil_div(W, kTileW), nty = ceil_div(H, Cfg::kTileH);
-  const long long tiles = (long long)ntx * nty * n_frames;
-  double* minv = static_cast<double*>(ws);
-  int2* rowtab = reinterpret_cast<int2*>(minv + 6 * (size_t)n_frames);
-  const int hq = rowtab_hq(H);
-  TilePlan* plan = reinterpret_cast<TilePlan*>(rowtab + (size_t)n_frames * 4 * hq);
-  hipLaunchKernelGGL((warp_plan_kernel<C, Cfg>), dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, s, M, n_frames,
-                     H, W, inverse_map, ntx, nty, plan, minv, rowtab, hq);
-  hipLaunchKernelGGL((warp_affine_u16_kernel<C, Cfg>), dim3(ntx, nty, n_frames), dim3(kThreads), 0, s, src,
-                     dst, plan, minv, rowtab, hq, H, W);
+  launch_warp_plan<C, Cfg>(M, n_frames, H, W, inverse_map, ws, s);
+  launch_warp_tiles<C, Cfg>(src, dst, n_frames, H, W, ws, s);
 }
 
 // ================================================================ warpPerspective
@@ -1349,20 +1373,98 @@ size_t persp_workspace_bytes(int n_frames, int H, int W) {
   return tiles * sizeof(TilePlan) + (size_t)n_frames * 9 * sizeof(double);
 }
 
+// WarpPerspectiveInvoker's block width: bh0 = min(16, H), bw0 = min(1024 / bh0, W)
+inline int persp_bw0(int H, int W) {
+  const int bh0 = H < 16 ? H : 16;
+  return 1024 / bh0 < W ? 1024 / bh0 : W;
+}
+
+// Workspace layout of the perspective warp: minv [F, 9] f64, plan [tiles].
 template <int C, class Cfg = typename CfgFor<C>::type>
-void launch_persp(const uint16_t* src, uint16_t* dst, const double* M, int n_frames, int H, int W, int inverse_map,
-                  void* ws, hipStream_t s) {
+void launch_persp_plan(const double* M, int n_frames, int H, int W, int inverse_map, void* ws, hipStream_t s) {
   const int ntx = ceil_div(W, kTileW), nty = ceil_div(H, Cfg::kTileH);
   const long long tiles = (long long)ntx * nty * n_frames;
-  // WarpPerspectiveInvoker's block width: bh0 = min(16, H), bw0 = min(1024 / bh0, W)
-  const int bh0 = H < 16 ? H : 16;
-  const int bw0 = 1024 / bh0 < W ? 1024 / bh0 : W;
   double* minv = static_cast<double*>(ws);
   TilePlan* plan = reinterpret_cast<TilePlan*>(minv + 9 * (size_t)n_frames);
   hipLaunchKernelGGL((persp_plan_kernel<C, Cfg>), dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, s, M, n_frames,
                      H, W, inverse_map, ntx, nty, plan, minv);
+}
+
+template <int C, class Cfg = typename CfgFor<C>::type>
+void launch_persp_tiles(const uint16_t* src, uint16_t* dst, int n_frames, int H, int W, const void* ws, hipStream_t s) {
+  const int ntx = ceil_div(W, kTileW), nty = ceil_div(H, Cfg::kTileH);
+  const double* minv = static_cast<const double*>(ws);
+  const TilePlan* plan = reinterpret_cast<const TilePlan*>(minv + 9 * (size_t)n_frames);
   hipLaunchKernelGGL((warp_perspective_u16_kernel<C, Cfg>), dim3(ntx, nty, n_frames), dim3(kThreads), 0, s, src, dst,
-                     plan, minv, H, W, bw0);
+                     plan, minv, H, W, persp_bw0(H, W));
+}
+
+template <int C, class Cfg = typename CfgFor<C>::type>
+void launch_persp(const uint16_t* src, uint16_t* dst, const double* M, int n_frames, int H, int W, int inverse_map,
+                  void* ws, hipStream_t s) {
+  launch_persp_plan<C, Cfg>(M, n_frames, H, W, inverse_map, ws, s);
+  launch_persp_tiles<C, Cfg>(src, dst, n_frames, H, W, ws, s);
+}
+
+// The plan workspace of one warp call (both launch forms use the same layout).
+size_t plan_bytes(int n_frames, int H, int W, int C, bool perspective) {
+  if (perspective)
+    return C == 1 ? persp_workspace_bytes<BlockCfg>(n_frames, H, W) : persp_workspace_bytes<ChanCfg>(n_frames, H, W);
+  if (C == 1) return use_tile64(H) ? warp_workspace_bytes<Block64Cfg>(n_frames, H, W)
+                                   : warp_workspace_bytes<BlockCfg>(n_frames, H, W);
+  return warp_workspace_bytes<ChanCfg>(n_frames, H, W);
+}
+
+// The plan / tile launches of a warp call; `tiles` false: the plan, true: the tiles.
+void launch_part(bool tiles, bool perspective, const uint16_t* src, uint16_t* dst, const double* M, int n_frames,
+                 int H, int W, int C, int inverse_map, void* ws, hipStream_t s) {
+  if (perspective) {
+    switch (C) {
+      case 1:
+        tiles ? launch_persp_tiles<1>(src, dst, n_frames, H, W, ws, s)
+              : launch_persp_plan<1>(M, n_frames, H, W, inverse_map, ws, s);
+        break;
+      case 3:
+        tiles ? launch_persp_tiles<3>(src, dst, n_frames, H, W, ws, s)
+              : launch_persp_plan<3>(M, n_frames, H, W, inverse_map, ws, s);
+        break;
+      default:
+        tiles ? launch_persp_tiles<4>(src, dst, n_frames, H, W, ws, s)
+              : launch_persp_plan<4>(M, n_frames, H, W, inverse_map, ws, s);
+        break;
+    }
+    return;
+  }
+  switch (C) {
+    case 1:
+      if (use_tile64(H))
+        tiles ? launch_warp_tiles<1, Block64Cfg>(src, dst, n_frames, H, W, ws, s)
+              : launch_warp_plan<1, Block64Cfg>(M, n_frames, H, W, inverse_map, ws, s);
+      else
+        tiles ? launch_warp_tiles<1>(src, dst, n_frames, H, W, ws, s)
+              : launch_warp_plan<1>(M, n_frames, H, W, inverse_map, ws, s);
+      break;
+    case 3:
+      tiles ? launch_warp_tiles<3>(src, dst, n_frames, H, W, ws, s)
+            : launch_warp_plan<3>(M, n_frames, H, W, inverse_map, ws, s);
+      break;
+    default:
+      tiles ? launch_warp_tiles<4>(src, dst, n_frames, H, W, ws, s)
+            : launch_warp_plan<4>(M, n_frames, H, W, inverse_map, ws, s);
+      break;
+  }
+}
+
+// The argument checks shared by every warp entry point.
+int check_warp_args(const char* who, int n_frames, int H, int W, int C) {
+  const std::string w(who);
+  if (n_frames < 0 || H < 0 || W < 0) return fail(KCMC_EINVAL, w + ": negative size");
+  if (H > 32767 || W > 32767) return fail(KCMC_EUNSUPPORTED, w + ": H, W must be < 32768");
+  if (n_frames > 65535) return fail(KCMC_EUNSUPPORTED, w + ": at most 65535 frames per call");
+  if (C != 1 && C != 3 && C != 4) return fail(KCMC_EUNSUPPORTED, w + ": C must be 1, 3 or 4");
+  if ((long long)ceil_div(W, kTileW) * ceil_div(H, ChanCfg::kTileH) * n_frames >= (1ll << 31))
+    return fail(KCMC_EUNSUPPORTED, w + ": too many tiles in one call");
+  return KCMC_OK;
 }
 
 }  // namespace
@@ -1373,30 +1475,16 @@ using namespace kcmc;
 extern "C" int kcmc_warp_perspective_u16(kcmc_ctx* ctx, const uint16_t* src, uint16_t* dst, const double* M,
                                          int n_frames, int H, int W, int C, int inverse_map, kcmc_stream_t stream) {
   if (!ctx) return fail(KCMC_EINVAL, "kcmc_warp_perspective_u16: ctx is NULL");
-  if (n_frames < 0 || H < 0 || W < 0) return fail(KCMC_EINVAL, "kcmc_warp_perspective_u16: negative size");
+  KCMC_TRY(check_warp_args("kcmc_warp_perspective_u16", n_frames, H, W, C));
   if (n_frames == 0 || H == 0 || W == 0) return KCMC_OK;
   if (!src || !dst || !M) return fail(KCMC_EINVAL, "kcmc_warp_perspective_u16: NULL pointer");
-  if (H > 32767 || W > 32767) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_perspective_u16: H, W must be < 32768");
-  if (n_frames > 65535) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_perspective_u16: at most 65535 frames per call");
-  if (C != 1 && C != 3 && C != 4) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_perspective_u16: C must be 1, 3 or 4");
   if (src == dst) return fail(KCMC_EINVAL, "kcmc_warp_perspective_u16: in-place warp is not supported");
-  if ((long long)ceil_div(W, kTileW) * ceil_div(H, ChanCfg::kTileH) * n_frames >= (1ll << 31))
-    return fail(KCMC_EUNSUPPORTED, "kcmc_warp_perspective_u16: too many tiles in one call");
   hipStream_t s = (hipStream_t)stream;
   void* ws = nullptr;
-  const size_t wsb = C == 1 ? persp_workspace_bytes<BlockCfg>(n_frames, H, W) : persp_workspace_bytes<ChanCfg>(n_frames, H, W);
+  const size_t wsb = plan_bytes(n_frames, H, W, C, true);
   KCMC_TRY(workspace_alloc(ctx, &ws, wsb, s));
-  switch (C) {
-    case 1:
-      launch_persp<1>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
-      break;
-    case 3:
-      launch_persp<3>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
-      break;
-    default:
-      launch_persp<4>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
-      break;
-  }
+  launch_part(false, true, src, dst, M, n_frames, H, W, C, inverse_map, ws, s);
+  launch_part(true, true, src, dst, M, n_frames, H, W, C, inverse_map, ws, s);
   const int rc = launch_check("warp_perspective_u16_kernel");
   KCMC_TRY(workspace_free(ctx, ws, s, wsb));
   return rc;
@@ -1405,37 +1493,49 @@ extern "C" int kcmc_warp_perspective_u16(kcmc_ctx* ctx, const uint16_t* src, uin
 extern "C" int kcmc_warp_affine_u16(kcmc_ctx* ctx, const uint16_t* src, uint16_t* dst, const double* M,
                                     int n_frames, int H, int W, int C, int inverse_map, kcmc_stream_t stream) {
   if (!ctx) return fail(KCMC_EINVAL, "kcmc_warp_affine_u16: ctx is NULL");
-  if (n_frames < 0 || H < 0 || W < 0) return fail(KCMC_EINVAL, "kcmc_warp_affine_u16: negative size");
+  KCMC_TRY(check_warp_args("kcmc_warp_affine_u16", n_frames, H, W, C));
   if (n_frames == 0 || H == 0 || W == 0) return KCMC_OK;
   if (!src || !dst || !M) return fail(KCMC_EINVAL, "kcmc_warp_affine_u16: NULL pointer");
-  if (H > 32767 || W > 32767) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: H, W must be < 32768");
-  if (n_frames > 65535) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: at most 65535 frames per call");
-  if (C != 1 && C != 3 && C != 4) return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: C must be 1, 3 or 4");
   if (src == dst) return fail(KCMC_EINVAL, "kcmc_warp_affine_u16: in-place warp is not supported");
-  if ((long long)ceil_div(W, kTileW) * ceil_div(H, ChanCfg::kTileH) * n_frames >= (1ll << 31))
-    return fail(KCMC_EUNSUPPORTED, "kcmc_warp_affine_u16: too many tiles in one call");
   hipStream_t s = (hipStream_t)stream;
   void* ws = nullptr;
-  const bool t64 = C == 1 && use_tile64(H);
-  const size_t wsb = C == 1 ? (t64 ? warp_workspace_bytes<Block64Cfg>(n_frames, H, W)
-                                   : warp_workspace_bytes<BlockCfg>(n_frames, H, W))
-                            : warp_workspace_bytes<ChanCfg>(n_frames, H, W);
+  const size_t wsb = plan_bytes(n_frames, H, W, C, false);
   KCMC_TRY(workspace_alloc(ctx, &ws, wsb, s));
-  switch (C) {
-    case 1:
-      if (t64)
-        launch_warp<1, Block64Cfg>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
-      else
-        launch_warp<1>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
-      break;
-    case 3:
-      launch_warp<3>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
-      break;
-    default:
-      launch_warp<4>(src, dst, M, n_frames, H, W, inverse_map, ws, s);
-      break;
-  }
+  launch_part(false, false, src, dst, M, n_frames, H, W, C, inverse_map, ws, s);
+  launch_part(true, false, src, dst, M, n_frames, H, W, C, inverse_map, ws, s);
   const int rc = launch_check("warp_affine_u16_kernel");
   KCMC_TRY(workspace_free(ctx, ws, s, wsb));
   return rc;
+}
+
+extern "C" long long kcmc_warp_plan_bytes(int n_frames, int H, int W, int C, int perspective) {
+  if (check_warp_args("kcmc_warp_plan_bytes", n_frames, H, W, C) != KCMC_OK) return -1;
+  return (long long)plan_bytes(n_frames, H, W, C, perspective != 0);
+}
+
+extern "C" int kcmc_warp_u16_plan(kcmc_ctx* ctx, const double* M, int n_frames, int H, int W, int C, int perspective,
+                                  int inverse_map, void* plan, long long plan_size, kcmc_stream_t stream) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_warp_u16_plan: ctx is NULL");
+  KCMC_TRY(check_warp_args("kcmc_warp_u16_plan", n_frames, H, W, C));
+  if (n_frames == 0 || H == 0 || W == 0) return KCMC_OK;
+  if (!M || !plan) return fail(KCMC_EINVAL, "kcmc_warp_u16_plan: NULL pointer");
+  if (plan_size < (long long)plan_bytes(n_frames, H, W, C, perspective != 0))
+    return fail(KCMC_EINVAL, "kcmc_warp_u16_plan: plan buffer smaller than kcmc_warp_plan_bytes");
+  if (((uintptr_t)plan & 15) != 0) return fail(KCMC_EINVAL, "kcmc_warp_u16_plan: plan must be 16-byte aligned");
+  launch_part(false, perspective != 0, nullptr, nullptr, M, n_frames, H, W, C, inverse_map, plan,
+              (hipStream_t)stream);
+  return launch_check("warp_plan_kernel");
+}
+
+extern "C" int kcmc_warp_u16_planned(kcmc_ctx* ctx, const uint16_t* src, uint16_t* dst, const void* plan, int n_frames,
+                                     int H, int W, int C, int perspective, kcmc_stream_t stream) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_warp_u16_planned: ctx is NULL");
+  KCMC_TRY(check_warp_args("kcmc_warp_u16_planned", n_frames, H, W, C));
+  if (n_frames == 0 || H == 0 || W == 0) return KCMC_OK;
+  if (!src || !dst || !plan) return fail(KCMC_EINVAL, "kcmc_warp_u16_planned: NULL pointer");
+  if (src == dst) return fail(KCMC_EINVAL, "kcmc_warp_u16_planned: in-place warp is not supported");
+  if (((uintptr_t)plan & 15) != 0) return fail(KCMC_EINVAL, "kcmc_warp_u16_planned: plan must be 16-byte aligned");
+  launch_part(true, perspective != 0, src, dst, nullptr, n_frames, H, W, C, 0, const_cast<void*>(plan),
+              (hipStream_t)stream);
+  return launch_check(perspective ? "warp_perspective_u16_kernel" : "warp_affine_u16_kernel");
 }

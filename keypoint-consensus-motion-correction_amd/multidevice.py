@@ -163,14 +163,21 @@ def split_to_devices(frames, ranges: Sequence[SlabRange], devices: Sequence[int]
     """Each slab's full-rate frames on its device: ``frames`` a host array [F, ...] (rows
     uploaded) or a device tensor (rows copied to the slab's device; no copy when it is
     already there)."""
-    parts = []
-    for d, r in zip(devices, ranges):
+    def upload(d, r):
         dev = torch.device("cuda", d)
         if isinstance(frames, torch.Tensor):
-            parts.append(frames[r.f0:r.f1].to(dev).contiguous())
-        else:
-            parts.append(torch.from_numpy(np.ascontiguousarray(frames[r.f0:r.f1])).to(dev))
-    return parts
+            return frames[r.f0:r.f1].to(dev).contiguous()
+        with torch.cuda.device(dev):
+            return torch.from_numpy(np.ascontiguousarray(frames[r.f0:r.f1])).to(dev)
+
+    if isinstance(frames, torch.Tensor) or len(set(devices)) < 2:
+        return [upload(d, r) for d, r in zip(devices, ranges)]
+    # host frames to several devices: one uploading thread per slab, so the devices' PCIe links
+    # run at once (a pageable copy blocks its caller; torch releases the GIL while it runs)
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(max_workers=len(ranges)) as ex:
+        return list(ex.map(upload, devices, ranges))
 
 
 def make_slabs(parts: Sequence[torch.Tensor], ranges: Sequence[SlabRange], des_tpl: np.ndarray, kp_tpl: np.ndarray,

@@ -651,9 +651,12 @@ class OverlappedSlabs:
         # RANSAC(k) ran beside warp(k-1) on the analysis stream: the host waits for it (it
         # has nothing else to do before it blocks on this step's votes) instead of queueing a
         # cross-stream wait, which leaves the device idle for tens of microseconds even when
-        # RANSAC finished long before
+        # RANSAC finished long before (round 5, same box: a device-side wait when RANSAC is
+        # still running, c2 / c3 / c4 / c5 within noise, profiles/r05_j_device_wait_ab.txt)
         self._wait(p.fitted_ev)
         self._at_tail(mark, "w0")
+        # one-call warp (plan + tiles) on the kernel stream: planning it on the analysis
+        # stream behind RANSAC measured slower (profiles/r05_k_plan_beside_ab.txt)
         p.aligned = warp_frames(p.inp.frames, p.rr.params, out=p.out, stream=self._hs)
         self._queued()
         self._at_tail(mark, "w1")

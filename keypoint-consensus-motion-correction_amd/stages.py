@@ -773,6 +773,60 @@ def warp_perspective_u16(frames: torch.Tensor, homographies: torch.Tensor, out: 
     return out
 
 
+def _warp_shape(frames_shape) -> Tuple[int, int, int, int]:
+    if len(frames_shape) not in (3, 4):
+        raise ValueError("frames must be [F, H, W] or [F, H, W, C]")
+    F, H, W = (int(v) for v in frames_shape[:3])
+    return F, H, W, 1 if len(frames_shape) == 3 else int(frames_shape[3])
+
+
+def warp_plan(maps: torch.Tensor, frames_shape, inverse_map: bool = False, stream: Optional[int] = None) -> torch.Tensor:
+    """The first part of warp_affine_u16 / warp_perspective_u16 (kcmc_warp_u16_plan): the
+    map inversion and every tile's source box for frames of ``frames_shape``, into a fresh
+    device buffer allocated on (and filled by) ``stream``; hand it to warp_planned on a
+    stream ordered after this one.  maps [F, 2, 3] (warpAffine) or [F, 3, 3]
+    (warpPerspective) f64."""
+    dev = _device_of(maps)
+    _require(maps, "maps", torch.float64, dev, 3)
+    F, H, W, C = _warp_shape(frames_shape)
+    persp = tuple(maps.shape[1:]) == (3, 3)
+    if tuple(maps.shape) != (F, 3 if persp else 2, 3):
+        raise ValueError(f"maps must be [{F}, 2, 3] or [{F}, 3, 3], got {tuple(maps.shape)}")
+    L = _lib.load()
+    nbytes = int(L.kcmc_warp_plan_bytes(F, H, W, C, int(persp)))
+    if nbytes < 0:
+        _lib.check(L.kcmc_warp_u16_plan(_ctx(dev).handle, _ptr(maps), F, H, W, C, int(persp), 0, _P(0), 0,
+                                        _stream(dev, stream)))
+    with on_stream(dev, stream):  # the buffer belongs to the stream that fills it
+        plan = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=dev)
+    _lib.check(L.kcmc_warp_u16_plan(_ctx(dev).handle, _ptr(maps), F, H, W, C, int(persp), int(bool(inverse_map)),
+                                    _ptr(plan), plan.numel(), _stream(dev, stream)))
+    plan.kcmc_perspective = persp  # which warp the plan is for
+    return plan
+
+
+def warp_planned(frames: torch.Tensor, plan: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 stream: Optional[int] = None) -> torch.Tensor:
+    """The second part (kcmc_warp_u16_planned): the tiles of a warp whose plan warp_plan
+    made for these frames; ``stream`` must be ordered after the plan's."""
+    dev = _device_of(frames)
+    _require(frames, "frames", torch.uint16, dev)
+    _require(plan, "plan", torch.uint8, dev, 1)
+    F, H, W, C = _warp_shape(frames.shape)
+    persp = bool(getattr(plan, "kcmc_perspective", False))
+    if plan.numel() < int(_lib.load().kcmc_warp_plan_bytes(F, H, W, C, int(persp))):
+        raise ValueError("plan was made for other frames")
+    if out is None:
+        out = torch.empty_like(frames)
+    else:
+        _require(out, "out", torch.uint16, dev)
+        if out.shape != frames.shape:
+            raise ValueError("out must have the shape of frames")
+    _lib.check(_lib.load().kcmc_warp_u16_planned(_ctx(dev).handle, _ptr(frames), _ptr(out), _ptr(plan), F, H, W, C,
+                                                 int(persp), _stream(dev, stream)))
+    return out
+
+
 # ------------------------------------------------------------ f2: normalisation
 def _numpy_linear_percentile(n: int, q: float, value_at) -> np.float64:
     """np.percentile(a, q) (default 'linear' method) of a flattened integer array of n
