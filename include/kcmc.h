@@ -119,6 +119,14 @@ int kcmc_match_frames(kcmc_ctx* ctx, const uint8_t* des_tpl_dev, const double* k
                       double* out_kp_ordered_dev, uint32_t* out_keep_bits_dev,
                       int32_t* out_counts_dev, kcmc_stream_t stream);
 
+/* VA:196-214 alone, on knn results of any of the matchers (out_idx / out_dist of
+ * kcmc_knn2_l2u8 / _hamming / _l2f32): the outputs of kcmc_match_frames after its knn, so that
+ * the filter can run on another stream than the knn (ordered after it by the caller). */
+int kcmc_match_filter(kcmc_ctx* ctx, const int32_t* idx_dev, const float* dist_dev, const double* kp_tpl_dev,
+                      const double* kp_q_dev, const int32_t* q_off_dev, int n_frames, int n_tpl, double ratio,
+                      double d_lo, double d_hi, double* out_kp_ordered_dev, uint32_t* out_keep_bits_dev,
+                      int32_t* out_counts_dev, kcmc_stream_t stream);
+
 /* -------------------------------------------------- K1 opt-in: binary descriptors, NORM_HAMMING
  * BFMatcher(NORM_HAMMING).knnMatch(k=2): distance = number of differing bits (as a float),
  * ties to the lower frame index.  NOT the reference's matcher (VA:194 uses the default

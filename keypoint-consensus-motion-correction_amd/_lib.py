@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "kcmc_destroy",
     "kcmc_knn2_l2u8",
     "kcmc_match_frames",
+    "kcmc_match_filter",
     "kcmc_knn2_l2f32",
     "kcmc_match_frames_f32",
     "kcmc_match_f32_prep_bytes",
@@ -105,6 +106,7 @@ _SIGNATURES = {
     "kcmc_destroy": ([P], I),
     "kcmc_knn2_l2u8": ([P, P, I, I, P, P, I, I, P, P, P], I),
     "kcmc_match_frames": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
+    "kcmc_match_filter": ([P, P, P, P, P, P, I, I, D, D, D, P, P, P, P], I),
     "kcmc_knn2_l2f32": ([P, P, I, I, P, P, I, I, P, P, P], I),
     "kcmc_match_frames_f32": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
     "kcmc_match_f32_prep_bytes": ([I, I, I], LL),

@@ -801,3 +801,18 @@ extern "C" int kcmc_match_frames(kcmc_ctx* ctx, const uint8_t* des_tpl, const do
   return launch_match_filter(out_idx, out_dist, kp_tpl, kp_q, q_off, n_frames, n_tpl, ratio, d_lo, d_hi,
                              out_kp_ordered, out_keep_bits, out_counts, s);
 }
+
+extern "C" int kcmc_match_filter(kcmc_ctx* ctx, const int32_t* idx, const float* dist, const double* kp_tpl,
+                                 const double* kp_q, const int32_t* q_off, int n_frames, int n_tpl, double ratio,
+                                 double d_lo, double d_hi, double* out_kp_ordered, uint32_t* out_keep_bits,
+                                 int32_t* out_counts, kcmc_stream_t stream) {
+  if (!ctx) return fail(KCMC_EINVAL, "kcmc_match_filter: ctx is NULL");
+  if (n_tpl < 0 || n_frames < 0) return fail(KCMC_EINVAL, "kcmc_match_filter: negative size");
+  if (n_frames > 65535) return fail(KCMC_EUNSUPPORTED, "kcmc_match_filter: at most 65535 frames per call");
+  if (n_tpl > 8192) return fail(KCMC_EUNSUPPORTED, "kcmc_match_filter: n_tpl > 8192");
+  if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
+  if (!idx || !dist || !kp_tpl || !kp_q || !q_off || !out_kp_ordered || !out_keep_bits || !out_counts)
+    return fail(KCMC_EINVAL, "kcmc_match_filter: NULL pointer");
+  return launch_match_filter(idx, dist, kp_tpl, kp_q, q_off, n_frames, n_tpl, ratio, d_lo, d_hi, out_kp_ordered,
+                             out_keep_bits, out_counts, (hipStream_t)stream);
+}

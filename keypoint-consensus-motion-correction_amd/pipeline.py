@@ -334,7 +334,6 @@ class _Slot:
     def __init__(self):
         self.bufs = {}
         self.votes_ev = torch.cuda.Event()
-        self.pack_ev = torch.cuda.Event()
         self.params_ev = torch.cuda.Event()
 
     def buf(self, name: str, numel: int, dtype: torch.dtype) -> torch.Tensor:
@@ -372,7 +371,9 @@ class OverlappedSlabs:
         kernel stream:    [match(k) -> vote(k)] -> warp(k-1) -> [waits RANSAC(k)] -> warp(k) ...
         analysis stream:  [match(k) -> vote(k)] -> lookup(k) -> RANSAC(k)   (beside warp(k-1))
 
-    with every transfer on a side stream; the match + vote run on the analysis stream with
+    with the parameter and map transfers on a side stream and the votes / consensus set in
+    the analysis stream's own order (between the kernels that make and read them); the
+    match + vote run on the analysis stream with
     ``match_beside`` (c2 / c3 / c4: the kernel stream then carries only the warps) and on
     the kernel stream ahead of the warp otherwise (c5: its 4 ms float match beside the
     1.4 ms warp starves it).  The consensus (VA:224-286) runs in three parts:
@@ -516,6 +517,15 @@ class OverlappedSlabs:
         stages.memcpy_async(host.data_ptr(), src.data_ptr(), src.numel() * src.element_size(), self._hc)
         done.record(self.copy)
 
+    def _d2h_ana(self, host: torch.Tensor, src: torch.Tensor, done: torch.cuda.Event) -> None:
+        """src (device) -> host (pinned) in the analysis stream's own order, ``done`` after it:
+        the analysis chain's transfers sit between two of its own kernels, and a copy on the
+        side stream costs the chain two cross-stream waits (tens of microseconds each on the
+        device, c3 trace)."""
+        stages.memcpy_async(host.data_ptr(), src.data_ptr(), src.numel() * src.element_size(), self._ha)
+        done.record(self.ana)
+        self._queued_on(self.ana)
+
     def submit(self, inp: SlabInputs, out: Optional[torch.Tensor] = None,
                mark: Optional[Callable[[str, Optional[torch.cuda.Event]], None]] = None) -> Optional[SlabResult]:
         """``mark(name, event)``: stage marks m0/m1 (match + vote), w0/w1 (warp), r0/r1
@@ -557,8 +567,8 @@ class OverlappedSlabs:
         self._at_tail(mark, "m0")
         for t in (inp.des_tpl, inp.kp_tpl, inp.des_q, inp.kp_q, inp.q_off):
             t.record_stream(self.stream)
-        match = match_stage(inp, self.cfg, stream=self._hs)
         n_tpl = inp.des_tpl.shape[0]
+        match = match_stage(inp, self.cfg, stream=self._hs)
         votes = stages.consensus_vote(match.keep_bits, n_tpl, self._f0, stream=self._hs)
         self._queued()
         matched = self._at_tail(mark, "m1")
@@ -587,9 +597,8 @@ class OverlappedSlabs:
             if self._sharded():
                 votes = self._gather(votes)  # the analysis stream waits for the collective
                 self._queued_on(self.ana)
-            ready = self._tail_on(self.ana, _nomark)
-        slot = self._slots.pop() if self._slots else _Slot()
-        self._d2h(slot.buf("votes", votes.numel(), torch.int64), votes, ready, slot.votes_ev)
+            slot = self._slots.pop() if self._slots else _Slot()
+            self._d2h_ana(slot.buf("votes", votes.numel(), torch.int64), votes, slot.votes_ev)
         return _SlabInFlight(inp, out, self._f0, match, slot, votes.numel(), matched=matched)
 
     def _fit(self, p: _SlabInFlight, mark) -> _SlabInFlight:
@@ -609,17 +618,17 @@ class OverlappedSlabs:
         self.stats["merge_s"] += time.perf_counter() - t0
         with torch.cuda.stream(self.ana):
             pack_dev = torch.empty(pack_h.numel(), dtype=torch.int32, device=self.dev)
-            stages.memcpy_async(pack_dev.data_ptr(), pack_h.data_ptr(), pack_h.numel() * 4, self._hc)
-            p.slot.pack_ev.record(self.copy)
-            self.ana.wait_event(p.matched)
-            self.ana.wait_event(p.slot.pack_ev)
+            if not self.match_beside:  # the match ran on the kernel stream
+                self.ana.wait_event(p.matched)
+            # the consensus set goes up in the analysis stream's own order, right in front of
+            # the lookup that reads it (no cross-stream wait on the device)
+            stages.memcpy_async(pack_dev.data_ptr(), pack_h.data_ptr(), pack_h.numel() * 4, self._ha)
             self._queued_on(self.ana)
             for t in (p.match.kp_ordered, p.match.keep_bits, p.inp.kp_tpl):
                 t.record_stream(self.ana)
             self._fit_device(p, choice, pack_dev, mark)
             for t in (p.rr.params, p.rr.inliers, p.rr.n_inliers, p.rr.best_trial):
                 t.record_stream(self.stream)
-            p.fitted_ev = self._tail_on(self.ana, _nomark)  # = the parameters' transfer event
         return p
 
     def _fit_device(self, p: _SlabInFlight, choice: stages.ConsensusChoice, pack_dev: torch.Tensor, mark) -> None:
@@ -632,20 +641,23 @@ class OverlappedSlabs:
         p.rr = ransac_stage(p.match, p.inp.kp_tpl, p.cons, self.cfg, stream=hs)
         self._queued_on(st)
         after = self._tail_on(st, mark, "r1")
+        p.fitted_ev = after  # the warp reads the parameters where RANSAC left them
         params = p.rr.params
+        # the parameters leave on the side stream: in the analysis stream their copy would sit
+        # in front of the next slab's match (c3 trace: +26 us before knn2)
+        d2h = (lambda host, src: self._d2h(host, src, after, p.slot.params_ev))
         if self._sharded():
             bound = self._gather(stages.params_boundary(params, stream=hs))
             self._queued_on(st)
             after = self._tail_on(st, _nomark)
             p.n_bound = bound.numel()
-            self._d2h(p.slot.buf("bound", bound.numel(), torch.float64), bound, after, p.slot.params_ev)
+            d2h(p.slot.buf("bound", bound.numel(), torch.float64), bound)
         if logging_enabled(self.logger):
             # the point counts for VA:279-283's log lines travel with the parameters (the
             # lines are written in _finish): reading pt_off here would block the host on the
             # analysis stream and break the overlap
-            self._d2h(p.slot.buf("pt_off", p.cons.pt_off_dev.numel(), torch.int32), p.cons.pt_off_dev, after,
-                      p.slot.params_ev)
-        self._d2h(p.slot.buf("params", params.numel(), torch.float64), params, after, p.slot.params_ev)
+            d2h(p.slot.buf("pt_off", p.cons.pt_off_dev.numel(), torch.int32), p.cons.pt_off_dev)
+        d2h(p.slot.buf("params", params.numel(), torch.float64), params)
 
     def _warp_device_maps(self, p: _SlabInFlight, mark) -> None:
         # RANSAC(k) ran beside warp(k-1) on the analysis stream: the host waits for it (it

@@ -180,6 +180,30 @@ def match_frames(
     against cv2 is unpinned -- see knn2_l2u8); ``norm`` "hamming" (uint8 only) is the
     opt-in NORM_HAMMING matcher for binary descriptors.  ``prep`` (float32 only): the
     output of match_f32_prepare for these descriptors, ordered before this call's stream."""
+    dev, f32, n_tpl, D, F, max_nq = _match_args(des_tpl, kp_tpl, des_q, kp_q, q_off, q_off_host, norm)
+    res = _match_result(dev, F, n_tpl)
+    L = _lib.load()
+    if prep is not None:
+        if not f32:
+            raise TypeError("prep: the prepared match is the float32 matcher's")
+        _require(prep, "prep", torch.uint8, dev, 1)
+        if prep.numel() < L.kcmc_match_f32_prep_bytes(n_tpl, F, max_nq):
+            raise ValueError("prep is smaller than kcmc_match_f32_prep_bytes")
+        _lib.check(L.kcmc_match_frames_f32_prepared(
+            _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F, max_nq,
+            _ptr(prep), float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist), _ptr(res.kp_ordered),
+            _ptr(res.keep_bits), _ptr(res.counts), _stream(dev, stream)))
+        return res
+    fn = L.kcmc_match_frames_f32 if f32 else (L.kcmc_match_frames_hamming if norm == "hamming" else L.kcmc_match_frames)
+    _lib.check(fn(
+        _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F,
+        max_nq, float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist),
+        _ptr(res.kp_ordered), _ptr(res.keep_bits), _ptr(res.counts), _stream(dev, stream)))
+    return res
+
+
+def _match_args(des_tpl, kp_tpl, des_q, kp_q, q_off, q_off_host, norm):
+    """match_frames' argument checks: (device, float32?, n_tpl, D, F, max_nq)."""
     if norm not in ("l2", "hamming"):
         raise ValueError(f"norm must be 'l2' or 'hamming' (got {norm!r})")
     dev = _device_of(des_tpl)
@@ -201,32 +225,54 @@ def match_frames(
         raise ValueError(f"frame {bad} has {int(nq[bad])} keypoints; knnMatch(k=2) needs >= 2 (VA:203)")
     if kp_tpl.shape != (n_tpl, 2) or kp_q.shape[0] != des_q.shape[0] or int(q_off_host[-1]) > des_q.shape[0]:
         raise ValueError("keypoint/descriptor shapes disagree")
-    words = (n_tpl + 31) // 32
-    res = MatchResult(
-        idx=torch.empty((F, n_tpl, 2), dtype=torch.int32, device=dev),
-        dist=torch.empty((F, n_tpl, 2), dtype=torch.float32, device=dev),
-        kp_ordered=torch.empty((F, n_tpl, 2), dtype=torch.float64, device=dev),
-        keep_bits=torch.empty((F, words), dtype=torch.int32, device=dev),
-        counts=torch.empty((F, 4), dtype=torch.int32, device=dev),
-    )
+    return dev, f32, n_tpl, D, F, int(nq.max()) if F else 0
+
+
+def _match_result(dev: torch.device, F: int, n_tpl: int, knn: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+    idx, dist = knn if knn is not None else (torch.empty((F, n_tpl, 2), dtype=torch.int32, device=dev),
+                                              torch.empty((F, n_tpl, 2), dtype=torch.float32, device=dev))
+    return MatchResult(idx=idx, dist=dist,
+                       kp_ordered=torch.empty((F, n_tpl, 2), dtype=torch.float64, device=dev),
+                       keep_bits=torch.empty((F, (n_tpl + 31) // 32), dtype=torch.int32, device=dev),
+                       counts=torch.empty((F, 4), dtype=torch.int32, device=dev))
+
+
+def knn_frames(des_tpl: torch.Tensor, kp_tpl: torch.Tensor, des_q: torch.Tensor, kp_q: torch.Tensor,
+               q_off: torch.Tensor, q_off_host: np.ndarray, norm: str = "l2",
+               stream: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """match_frames in two parts, the first: the knn k=2 of every frame (VA:194-195) on
+    ``stream``, idx / dist [F, n_tpl, 2]; filter_matches finishes it (on another stream
+    ordered after this one, if wanted).  Same checks and results as match_frames."""
+    dev, f32, n_tpl, D, F, max_nq = _match_args(des_tpl, kp_tpl, des_q, kp_q, q_off, q_off_host, norm)
+    idx = torch.empty((F, n_tpl, 2), dtype=torch.int32, device=dev)
+    dist = torch.empty((F, n_tpl, 2), dtype=torch.float32, device=dev)
     L = _lib.load()
-    max_nq = int(nq.max()) if F else 0
-    if prep is not None:
-        if not f32:
-            raise TypeError("prep: the prepared match is the float32 matcher's")
-        _require(prep, "prep", torch.uint8, dev, 1)
-        if prep.numel() < L.kcmc_match_f32_prep_bytes(n_tpl, F, max_nq):
-            raise ValueError("prep is smaller than kcmc_match_f32_prep_bytes")
-        _lib.check(L.kcmc_match_frames_f32_prepared(
-            _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F, max_nq,
-            _ptr(prep), float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist), _ptr(res.kp_ordered),
-            _ptr(res.keep_bits), _ptr(res.counts), _stream(dev, stream)))
-        return res
-    fn = L.kcmc_match_frames_f32 if f32 else (L.kcmc_match_frames_hamming if norm == "hamming" else L.kcmc_match_frames)
-    _lib.check(fn(
-        _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F,
-        max_nq, float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist),
-        _ptr(res.kp_ordered), _ptr(res.keep_bits), _ptr(res.counts), _stream(dev, stream)))
+    fn = L.kcmc_knn2_l2f32 if f32 else (L.kcmc_knn2_hamming if norm == "hamming" else L.kcmc_knn2_l2u8)
+    _lib.check(fn(_ctx(dev).handle, _ptr(des_tpl), n_tpl, D, _ptr(des_q), _ptr(q_off), F, max_nq, _ptr(idx), _ptr(dist),
+                  _stream(dev, stream)))
+    return idx, dist
+
+
+def filter_matches(knn: Tuple[torch.Tensor, torch.Tensor], kp_tpl: torch.Tensor, kp_q: torch.Tensor,
+                   q_off: torch.Tensor, ratio: float = 0.75, d_lo: float = 0.5, d_hi: float = 2.0,
+                   stream: Optional[int] = None) -> MatchResult:
+    """The second part: VA:196-214 on knn_frames' (idx, dist) (kcmc_match_filter), on
+    ``stream`` (its outputs are allocated there)."""
+    idx, dist = knn
+    dev = _device_of(idx)
+    _require(idx, "idx", torch.int32, dev, 3)
+    _require(dist, "dist", torch.float32, dev, 3)
+    _require(kp_tpl, "kp_tpl", torch.float64, dev, 2)
+    _require(kp_q, "kp_q", torch.float64, dev, 2)
+    _require(q_off, "q_off", torch.int32, dev, 1)
+    F, n_tpl = idx.shape[0], idx.shape[1]
+    if dist.shape != idx.shape or idx.shape[2] != 2 or q_off.numel() != F + 1 or kp_tpl.shape != (n_tpl, 2):
+        raise ValueError("knn results / keypoints shapes disagree")
+    with on_stream(dev, stream):
+        res = _match_result(dev, F, n_tpl, knn)
+    _lib.check(_lib.load().kcmc_match_filter(
+        _ctx(dev).handle, _ptr(idx), _ptr(dist), _ptr(kp_tpl), _ptr(kp_q), _ptr(q_off), F, n_tpl, float(ratio),
+        float(d_lo), float(d_hi), _ptr(res.kp_ordered), _ptr(res.keep_bits), _ptr(res.counts), _stream(dev, stream)))
     return res
 
 

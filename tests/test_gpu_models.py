@@ -382,6 +382,35 @@ def test_match_frames_f32_prepared_equals_one_call(dev):
                             _t(ku.q_off, dev), ku.q_off, prep=prep)
 
 
+@pytest.mark.parametrize("kind", ["u8", "hamming", "f32", "u8_big"])
+def test_knn_then_filter_on_two_streams_equals_match_frames(dev, kind):
+    """knn_frames on one stream + filter_matches on another ordered after it (the c5
+    schedule: knn on the kernel stream, filter + vote on the analysis stream) =
+    match_frames, bit for bit: L2 u8, Hamming, float32 and n_tpl 4096 (the filter's
+    workgroup kernel)."""
+    if kind == "f32":
+        ks = synthetic.make_keypoints(9, 300, 128, (270, 480), seed=16, descriptor="f32")
+    elif kind == "u8_big":
+        ks = synthetic.make_keypoints(3, 4096, 61, (512, 512), seed=17)
+    else:
+        ks = synthetic.make_keypoints(9, 500, 32, (1080, 1920), seed=18)
+    norm = "hamming" if kind == "hamming" else "l2"
+    args = (_t(ks.des_tpl, dev), _t(ks.kp_tpl, dev), _t(ks.des_q, dev), _t(ks.kp_q, dev), _t(ks.q_off, dev), ks.q_off)
+    ref = stages.match_frames(*args, norm=norm)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    s1.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s1):
+        knn = stages.knn_frames(*args, norm=norm, stream=s1.cuda_stream)
+    s2.wait_stream(s1)
+    with torch.cuda.stream(s2):
+        got = stages.filter_matches(knn, args[1], args[3], args[4], stream=s2.cuda_stream)
+    torch.cuda.current_stream(dev).wait_stream(s2)
+    for name in ("idx", "dist", "kp_ordered", "keep_bits", "counts"):
+        assert torch.equal(getattr(ref, name), getattr(got, name)), name
+    with pytest.raises(ValueError, match="shapes disagree"):
+        stages.filter_matches((knn[0][:1], knn[1]), args[1], args[3], args[4])
+
+
 # ------------------------------------------------------------ f2: normalisation
 def test_brightest_px_and_max_scale_vs_reference_golden(dev):
     g = load_golden("preprocess_golden.npz")

@@ -15,6 +15,7 @@
 #   cpubench:<cfg>        bench.py --config <cfg> with its CPU baseline -> <out>/<cfg>_cpu.json
 #   profile:<cfg>         tools/profile_round.sh (bench + rocprofv3 summary + warp PMC) -> <out>/<cfg>/
 #   abpmc:<lib>:<cfg>:<tag>  the warp PMC passes (tools/pmc_warp.sh) against another build -> <out>/pmc_<tag>/
+#   envtrace:<VAR=val>:<cfg>:<tag>  the same with one extra environment variable
 #   trace:<cfg>:<tag>[:<args,comma>]  rocprofv3 --kernel-trace --memory-copy-trace of a short bench
 #                         -> <out>/trace_<tag>/ (read with tools/timeline.py)
 #   rehearse:<cfg>:<ranks>  bench.py over gloo ranks that share cuda:0 (the multi-rank path on one GPU)
@@ -87,6 +88,13 @@ for step in "$@"; do
           -o run -- python bench.py --config "$a" --cpu-sample 0 --steps 12 --warmup 3 "${X[@]}" \
           > "$OUT/trace_$b.json" 2> "$OUT/trace_$b.err") || exit 1
       echo "trace $a $b: $(head -c 160 "$OUT/trace_$b.json")" ;;
+    envtrace)  # envtrace:<VAR=value>:<cfg>:<tag>  the trace step with one extra environment variable
+      R=$PWD
+      (cd /tmp && export TMPDIR=/tmp && cd "$R" &&
+        env "$a" timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$R/$OUT/trace_$c" \
+          -o run -- python bench.py --config "$b" --cpu-sample 0 --steps 12 --warmup 3 \
+          > "$OUT/trace_$c.json" 2> "$OUT/trace_$c.err") || exit 1
+      echo "trace $b $c ($a): $(head -c 160 "$OUT/trace_$c.json")" ;;
     envlab)  # envlab:<VAR=value>:<binary>:<tag>[:<args,comma>]  a lab with one extra environment variable
       IFS=, read -r -a X <<< "${d:-}"
       env "$a" timeout -k 10 240 "$b" "${X[@]}" > "$OUT/lab_$c.txt" 2>&1 || exit 1
