@@ -88,10 +88,11 @@ for step in "$@"; do
           -o run -- python bench.py --config "$a" --cpu-sample 0 --steps 12 --warmup 3 "${X[@]}" \
           > "$OUT/trace_$b.json" 2> "$OUT/trace_$b.err") || exit 1
       echo "trace $a $b: $(head -c 160 "$OUT/trace_$b.json")" ;;
-    envtrace)  # envtrace:<VAR=value>:<cfg>:<tag>  the trace step with one extra environment variable
+    envtrace)  # envtrace:<VAR=value[+VAR=value]>:<cfg>:<tag>  the trace step with extra environment variables
       R=$PWD
+      IFS=+ read -r -a E <<< "$a"
       (cd /tmp && export TMPDIR=/tmp && cd "$R" &&
-        env "$a" timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$R/$OUT/trace_$c" \
+        env "${E[@]}" timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$R/$OUT/trace_$c" \
           -o run -- python bench.py --config "$b" --cpu-sample 0 --steps 12 --warmup 3 \
           > "$OUT/trace_$c.json" 2> "$OUT/trace_$c.err") || exit 1
       echo "trace $b $c ($a): $(head -c 160 "$OUT/trace_$c.json")" ;;
