@@ -490,10 +490,14 @@ __device__ __forceinline__ void finish_row(const uint32_t (&ck)[kTop], int i, in
   const float T = ldexpf(1.f, key_bits - 23);
   const float thr = best.v[1] * (1.f + 2.f * T) + 2.f * Bs;
   const bool sane = fbad[f] == 0 && sc * (K + maxb * maxb) < 1e36f && Bs < 1e36f;
+  // (sanity first: a flagged frame's fp16 images overflow, and its values -- inf / NaN --
+  // must not read as "fewer than two frame rows"; round 5, tests/test_gpu_fuzz.py)
   int ncand;
-  if (!(best.v[1] < INFINITY)) {
+  if (!sane) {
+    ncand = -1;
+  } else if (!(best.v[1] < INFINITY)) {
     ncand = best.v[0] < INFINITY ? 1 : 0;  // fewer than two frame rows: all are listed
-  } else if (!sane || !(best.v[kTop - 1] > thr)) {
+  } else if (!(best.v[kTop - 1] > thr)) {
     ncand = -1;
   } else {
     ncand = 2;

@@ -353,6 +353,26 @@ def test_match_frames_f32_vs_oracle(dev):
         assert len(kept) > 250
 
 
+@pytest.mark.parametrize("n_q", [2, 3, 70])
+def test_knn2_f32_frame_beyond_fp16_range_goes_to_fallback(dev, n_q):
+    """A frame whose values are ~5e4 x the template's largest element overflows the fp16
+    tile image (flagged): every template row must come from the exact fallback, also when
+    the overflowed values would otherwise read as 'fewer than two frame rows' (round 5: the
+    fuzz sweep found such frames returned -1 / FLT_MAX)."""
+    rng = np.random.default_rng(n_q)
+    tpl = rng.normal(0, 1e-3, (300, 113)).astype(np.float32)
+    frames = [rng.normal(0, 1e-3, (40, 113)).astype(np.float32), rng.normal(0, 50.0, (n_q, 113)).astype(np.float32),
+              rng.normal(0, 1e-3, (9, 113)).astype(np.float32)]
+    off = np.zeros(4, np.int32)
+    off[1:] = np.cumsum([len(q) for q in frames])
+    idx, dist = stages.knn2_l2u8(_t(tpl, dev), _t(np.concatenate(frames), dev), _t(off, dev), int(np.diff(off).max()))
+    idx, dist = idx.cpu().numpy(), dist.cpu().numpy()
+    for f, q in enumerate(frames):
+        ri, rd = oracle.knn2_l2f32(tpl, q)
+        assert np.array_equal(idx[f], ri), f
+        assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), f
+
+
 def test_match_frames_f32_prepared_equals_one_call(dev):
     """kcmc_match_f32_prepare on a side stream + kcmc_match_frames_f32_prepared on another
     (ordered by an event) = kcmc_match_frames_f32, bit for bit, including the near-tie rows
