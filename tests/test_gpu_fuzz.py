@@ -131,3 +131,141 @@ def test_knn2_fuzz_vs_oracle(dev, kind, seed):
         ri, rd = ora(tpl, q)
         assert np.array_equal(idx[f], ri), (seed, kind, f, D, n_tpl, len(q))
         assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), (seed, kind, f)
+
+
+def _csr(lists):
+    off = np.zeros(len(lists) + 1, np.int32)
+    off[1:] = np.cumsum([len(x) for x in lists])
+    return off
+
+
+def _point_sets(rng, n_frames, model):
+    """Frame / template point pairs: random sizes (including 0-3 points), coordinate
+    scales from 1e-2 to 1e4, noise from exact to large, outlier shares, duplicated pairs."""
+    tpls, qs = [], []
+    for _ in range(n_frames):
+        N = int(rng.choice([0, 1, 2, 3, 4, 5, int(rng.integers(6, 60)), int(rng.integers(60, 400))]))
+        scale = 10.0 ** rng.uniform(-2, 4)
+        tpl = rng.uniform(0, scale, (N, 2))
+        a = rng.normal(0, 0.05)
+        A = np.array([[np.cos(a), -np.sin(a)], [np.sin(a), np.cos(a)]])
+        if model != "rigid":
+            A = A @ np.array([[rng.uniform(0.8, 1.25), rng.normal(0, 0.05)], [0.0, rng.uniform(0.8, 1.25)]])
+        q = tpl @ A.T + rng.normal(0, scale * 0.01, 2)
+        noise = rng.choice([0.0, 1e-9, 0.3, 1.5]) * (scale / 1000.0 if scale > 1000 else 1.0)
+        q = q + rng.normal(0, noise, (N, 2)) if noise else q
+        out = rng.random(N) < rng.uniform(0, 0.5)
+        q[out] = rng.uniform(0, scale, (int(out.sum()), 2))
+        if N > 10 and rng.random() < 0.3:
+            q[N // 2:], tpl[N // 2:] = q[: N - N // 2], tpl[: N - N // 2]
+        tpls.append(tpl)
+        qs.append(q)
+    return tpls, qs
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_ransac_rigid_fuzz_vs_oracle(dev, seed):
+    rng = np.random.default_rng(3000 + seed)
+    tpls, qs = _point_sets(rng, 24, "rigid")
+    thresh = float(rng.choice([2.0, 0.5, 5.0, 1e-3]))
+    off = _csr(qs)
+    r = stages.ransac_rigid(_t(np.concatenate(qs).reshape(-1, 2), dev), _t(np.concatenate(tpls).reshape(-1, 2), dev),
+                            _t(off, dev), off, residual_threshold=thresh)
+    params, inl = r.params.cpu().numpy(), r.inliers.cpu().numpy().astype(bool)
+    nin, best = r.n_inliers.cpu().numpy(), r.best_trial.cpu().numpy()
+    for f in range(len(qs)):
+        if len(qs[f]) < 3:  # N_KP_FRAME_SKIP: no model, NaN (VA:307)
+            assert np.isnan(params[f]).all(), (seed, f)
+            continue
+        p, i_ref, bt, ni = oracle.ransac_rigid(qs[f], tpls[f], thresh=thresh)
+        assert best[f] == bt and nin[f] == ni, (seed, f, len(qs[f]))
+        assert np.array_equal(inl[off[f]:off[f + 1]], i_ref), (seed, f)
+        np.testing.assert_allclose(params[f], p, rtol=1e-10, atol=1e-10 * max(1.0, np.abs(tpls[f]).max()),
+                                   equal_nan=True, err_msg=str((seed, f)))
+
+
+def _tls_gap(src, dst, model):
+    """s_min / s_next of skimage's normalised total-least-squares matrix for the refit on
+    these points (_geometric.py:548-562, 596-703).  Near 1 the refit's solution is not
+    determined by the data (two directions fit about equally well): any two SVD
+    implementations, LAPACK builds included, return different models there."""
+    def norm(p):
+        c = p.mean(0)
+        d = p - c
+        return d * (np.sqrt(2) / np.sqrt((d ** 2).sum() / len(p)))
+
+    a, b = norm(src), norm(dst)
+    n = len(a)
+    k = 7 if model == "affine" else 9
+    A = np.zeros((2 * n, k))
+    A[:n, 0:2], A[:n, 2], A[n:, 3:5], A[n:, 5] = a, 1, a, 1
+    if model == "affine":
+        A[:n, 6], A[n:, 6] = -b[:, 0], -b[:, 1]
+    else:
+        A[:n, 6:8], A[:n, 8] = -a * b[:, :1], -b[:, 0]
+        A[n:, 6:8], A[n:, 8] = -a * b[:, 1:2], -b[:, 1]
+    sv = np.linalg.svd(A, compute_uv=False)
+    return sv[-1] / sv[-2] if sv[-2] > 0 else 1.0
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("model", ["affine", "projective"])
+def test_ransac_model_fuzz_vs_oracle(dev, model, seed):
+    rng = np.random.default_rng(4000 + seed + (100 if model == "projective" else 0))
+    tpls, qs = _point_sets(rng, 12, model)
+    ms = 3 if model == "affine" else 4
+    for f in range(len(qs)):  # n_skip <= N <= min_samples raises ValueError, as skimage does
+        if 3 <= len(qs[f]) <= ms:
+            tpls[f], qs[f] = tpls[f][:2], qs[f][:2]
+    off = _csr(qs)
+    r = stages.ransac_model(_t(np.concatenate(qs).reshape(-1, 2), dev), _t(np.concatenate(tpls).reshape(-1, 2), dev),
+                            _t(off, dev), off, model=model)
+    params, inl = r.params.cpu().numpy(), r.inliers.cpu().numpy().astype(bool)
+    nin, best = r.n_inliers.cpu().numpy(), r.best_trial.cpu().numpy()
+    for f in range(len(qs)):
+        if len(qs[f]) < 3:
+            assert np.isnan(params[f]).all(), (seed, f)
+            continue
+        p, i_ref, bt, ni = oracle.ransac_model(qs[f], tpls[f], model)
+        assert best[f] == bt and nin[f] == ni, (seed, f, len(qs[f]))
+        assert np.array_equal(inl[off[f]:off[f + 1]], i_ref), (seed, f)
+        if ni > ms and _tls_gap(qs[f][i_ref], tpls[f][i_ref], model) > 0.3:
+            continue  # the refit's model is not determined by these points (see _tls_gap)
+        np.testing.assert_allclose(params[f], p, rtol=1e-8, atol=1e-9 * max(1.0, np.abs(tpls[f]).max()),
+                                   equal_nan=True, err_msg=str((seed, f)))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_match_filters_fuzz_vs_oracle(dev, seed):
+    """VA:196-221 on random knn results (kcmc_match_filter): ratio-test boundaries
+    (d0 == 0.75 d1 in float, equal distances, zeros), displacement medians with exact
+    boundary values, template counts on all three filter kernels (<= 512, <= 4096, more)."""
+    rng = np.random.default_rng(5000 + seed)
+    n_tpl = int(rng.choice([1, 2, 7, 100, 512, 513, 2000, 4096, 5000, 8192]))
+    F = int(rng.integers(1, 5))
+    q_lists = [rng.uniform(0, 500, (int(rng.integers(2, 300)), 2)) for _ in range(F)]
+    kp_tpl = rng.uniform(0, 500, (n_tpl, 2))
+    idx = np.zeros((F, n_tpl, 2), np.int32)
+    dist = np.zeros((F, n_tpl, 2), np.float32)
+    for f, q in enumerate(q_lists):
+        idx[f] = rng.integers(0, len(q), (n_tpl, 2))
+        d1 = rng.uniform(0, 300, n_tpl).astype(np.float32)
+        d0 = (d1 * rng.uniform(0, 1, n_tpl)).astype(np.float32)
+        k = rng.random(n_tpl)
+        d0[k < 0.1] = (np.float32(0.75) * d1[k < 0.1]).astype(np.float32)  # on the ratio boundary
+        d0[(k >= 0.1) & (k < 0.15)] = d1[(k >= 0.1) & (k < 0.15)]
+        d0[(k >= 0.15) & (k < 0.18)] = 0
+        dist[f, :, 0], dist[f, :, 1] = d0, d1
+        if n_tpl > 4:  # a few template points displaced exactly onto the 0.5x / 2x median boundaries
+            kp_tpl[:2] = q[idx[f, :2, 0]]
+    off = _csr(q_lists)
+    kq = np.concatenate(q_lists)
+    res = stages.filter_matches((_t(idx, dev), _t(dist, dev)), _t(kp_tpl, dev), _t(kq, dev), _t(off, dev))
+    bits = res.keep_bits.cpu().numpy().view(np.uint32)
+    kqo, cnt = res.kp_ordered.cpu().numpy(), res.counts.cpu().numpy()
+    for f, q in enumerate(q_lists):
+        s, kq_ref, c = oracle.filter_matches(idx[f], dist[f], kp_tpl, q)
+        kept = [i for i in range(n_tpl) if (bits[f, i >> 5] >> (i & 31)) & 1]
+        assert kept == sorted(s), (seed, f, n_tpl)
+        assert np.array_equal(kqo[f], kq_ref), (seed, f)
+        assert cnt[f].tolist() == list(c), (seed, f)
