@@ -269,3 +269,20 @@ def test_match_filters_fuzz_vs_oracle(dev, seed):
         assert kept == sorted(s), (seed, f, n_tpl)
         assert np.array_equal(kqo[f], kq_ref), (seed, f)
         assert cnt[f].tolist() == list(c), (seed, f)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_slab_end_to_end_fuzz_vs_oracle(dev, seed):
+    """align_slab on random slabs (frame count, size, channels, template size, descriptor
+    kind and length, RANSAC model, consensus size) against the oracle stage by stage
+    (test_gpu_configs._check_slab: match + filters on every frame, CPython-ordered
+    consensus, RANSAC on every frame, the warp of every frame bit-exact)."""
+    from test_gpu_configs import _check_slab
+
+    rng = np.random.default_rng(6000 + seed)
+    descriptor = str(rng.choice(["u8", "u8", "f32"]))
+    D = int(rng.integers(16, 65)) if descriptor == "u8" else int(rng.integers(16, 129))
+    _check_slab(dev, F=int(rng.integers(2, 25)), H=int(rng.integers(64, 301)), W=int(rng.integers(64, 401)),
+                C=int(rng.choice([1, 1, 3, 4])), n_tpl=int(rng.integers(40, 600)), D=D,
+                model=str(rng.choice(["euclidean", "affine", "projective"])),
+                n_kp_global=int(rng.integers(10, 120)), descriptor=descriptor, seed=7000 + seed)
