@@ -286,3 +286,98 @@ def test_slab_end_to_end_fuzz_vs_oracle(dev, seed):
                 C=int(rng.choice([1, 1, 3, 4])), n_tpl=int(rng.integers(40, 600)), D=D,
                 model=str(rng.choice(["euclidean", "affine", "projective"])),
                 n_kp_global=int(rng.integers(10, 120)), descriptor=descriptor, seed=7000 + seed)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_pyr_down_and_normalize_fuzz(dev, seed):
+    """pyrDown (VA:501-503) at random sizes and every admissible dstsize, and the
+    99.99th-percentile max-scale (VA:479-492) of random uint16 stacks (numpy's own
+    percentile and clip as the reference writes them) -- bit for bit."""
+    rng = np.random.default_rng(8000 + seed)
+    F, H, W = int(rng.integers(1, 4)), int(rng.integers(1, 260)), int(rng.integers(1, 400))
+    imgs = rng.integers(0, 256, (F, H, W)).astype(np.uint8)
+    sizes = [((W + 1) // 2, (H + 1) // 2)] + [(dw, dh) for dw in (W // 2, (W + 2) // 2) for dh in (H // 2, (H + 2) // 2)
+                                             if dw >= 1 and dh >= 1 and abs(2 * dw - W) <= 2 and abs(2 * dh - H) <= 2]
+    for dw, dh in sorted(set(sizes)):
+        out = stages.pyr_down_u8(_t(imgs, dev), (dw, dh)).cpu().numpy()
+        for f in range(F):
+            assert np.array_equal(out[f], oracle.pyr_down_u8(imgs[f], (dw, dh))), (seed, f, (H, W), (dw, dh))
+    hi = int(rng.choice([255, 4095, 16383, 65535]))
+    x = rng.integers(0, hi + 1, (F, H, W)).astype(np.uint16)
+    if rng.random() < 0.5:  # a few saturated / hot pixels above the bulk
+        x[rng.random(x.shape) < 1e-4] = 65535
+    b = stages.brightest_px(_t(x, dev))
+    assert b == np.percentile(x, 99.99), (seed, b)
+    if b > 0:
+        got = stages.max_scale_u8(_t(x, dev), b).cpu().numpy()
+        assert np.array_equal(got, np.clip(x / b * 255, a_min=0, a_max=255).astype(np.uint8)), seed
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_orb_detect_fuzz_vs_oracle(dev, seed):
+    """The build-defined GPU ORB detector (f1) against its C restatement on random
+    textures, sizes (down to a few pixels more than the border) and feature budgets:
+    the keypoints (positions, angles, responses) and descriptors bit for bit."""
+    from kcmc_amd import orb
+
+    rng = np.random.default_rng(9000 + seed)
+    F, H, W = int(rng.integers(1, 4)), int(rng.integers(36, 420)), int(rng.integers(36, 520))
+    cell = int(rng.choice([2, 4, 8]))
+    imgs = []
+    for _ in range(F):
+        lo = rng.integers(0, 256, (H // cell + 2, W // cell + 2)).astype(np.float64)
+        img = np.kron(lo, np.ones((cell, cell)))[:H, :W] + rng.normal(0, float(rng.choice([0, 6, 20])), (H, W))
+        imgs.append(np.clip(img, 0, 255).astype(np.uint8))
+    imgs = np.stack(imgs)
+    nf = int(rng.choice([1, 7, 100, 500, 2000]))
+    k = stages.detect_orb(_t(imgs, dev), orb.OrbParams(n_features=nf))
+    kp, des, cnt = k.kp.cpu().numpy(), k.des.cpu().numpy(), k.count.cpu().numpy()
+    for f in range(F):
+        rkp, rdes = oracle.orb_detect(imgs[f], n_features=nf, pattern=orb.rotated_patterns(), bin_cs=orb.bin_edges())
+        assert cnt[f] == len(rkp), (seed, f, cnt[f], len(rkp))
+        assert np.array_equal(kp[f, :cnt[f]], rkp), (seed, f)
+        assert np.array_equal(des[f, :cnt[f]], rdes), (seed, f)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_multidevice_split_fuzz(dev, seed):
+    """VideoAligner over 2-5 slabs on cuda:0 (DEVICES = [0] * k) against one slab, with
+    random frame counts (fewer frames than slabs included), model-less runs of frames at
+    random places (gaps that cross slab boundaries), the model and the frame rate
+    (temporal downsampling) drawn at random: identical arrays."""
+    from kcmc_amd import VideoAligner, synthetic
+
+    rng = np.random.default_rng(9500 + seed)
+    model = str(rng.choice(["euclidean", "affine"]))
+    rate = int(rng.choice([1, 2]))
+    n_sample = int(rng.integers(2, 18))
+    H, W = 72, 120
+    ks = synthetic.make_keypoints(n_sample, 120, 32, (H, W), seed=9600 + seed, model=model)
+    for f in rng.choice(n_sample, int(rng.integers(0, n_sample // 2 + 1)), replace=False):
+        a, b = ks.q_off[f], ks.q_off[f + 1]
+        ks.des_q[a:b] = rng.integers(0, 256, (1, 32), dtype=np.uint8)  # no ratio survivor: no model
+    base = synthetic.make_texture((H, W), seed=seed)
+    frames = np.ascontiguousarray(np.stack([np.roll(base, (f, 3 * f), axis=(0, 1))
+                                            for f in range(n_sample * rate - rate // 2)]))
+    kq = [ks.kp_q[ks.q_off[f]:ks.q_off[f + 1]] for f in range(n_sample)]
+    dq = [ks.des_q[ks.q_off[f]:ks.q_off[f + 1]] for f in range(n_sample)]
+    out = []
+    for k in (1, int(rng.integers(2, 6))):
+        class VA(VideoAligner):
+            DEVICES = [0] * k
+            RANSAC_MODEL = model
+            N_KP_GLOBAL_MIN = 3
+
+        va = VA()
+        try:
+            res = va.align_keypoints(frames, ks.kp_tpl, ks.des_tpl, kq, dq, n_kp_global=30, frame_rate=100 * rate)
+        except VideoAligner.AlignmentError as e:  # every frame model-less: the same error either way
+            res = ("AlignmentError", str(e))
+        out.append((res, getattr(va, "interpolated_idxs", None)))
+    (r1, i1), (r2, i2) = out
+    if isinstance(r1[0], str):
+        assert r1 == r2
+        return
+    np.testing.assert_array_equal(r2[0], r1[0])
+    np.testing.assert_array_equal(r2[1], r1[1])
+    assert r2[2] == r1[2] and i2 == i1
