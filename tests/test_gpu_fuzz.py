@@ -381,3 +381,21 @@ def test_multidevice_split_fuzz(dev, seed):
     np.testing.assert_array_equal(r2[0], r1[0])
     np.testing.assert_array_equal(r2[1], r1[1])
     assert r2[2] == r1[2] and i2 == i1
+
+
+@pytest.mark.parametrize("shape,persp", [((1, 4320, 7680), False), ((1, 4320, 7680), True), ((1, 2160, 3840, 4), False),
+                                         ((2, 4097, 257), True)])
+def test_warp_large_frames_vs_oracle(dev, shape, persp):
+    """8K one-channel, 4K RGBA and a 4097-row strip: tile grids far beyond the configs',
+    every tile path, bit for bit."""
+    rng = np.random.default_rng(sum(shape) + persp)
+    imgs = _values(rng, shape)
+    F, H, W = shape[:3]
+    Ms = np.stack([(_perspective if persp else _affine)(rng, H, W) for _ in range(F)])
+    if persp:
+        Ms[:, 2, :2] = rng.normal(0, 1e-6, (F, 2))
+    fn = stages.warp_perspective_u16 if persp else stages.warp_affine_u16
+    ref = oracle.warp_perspective_u16 if persp else oracle.warp_affine_u16
+    out = fn(_t(imgs, dev), _t(Ms, dev)).cpu().numpy()
+    for f in range(F):
+        assert np.array_equal(out[f], ref(imgs[f], Ms[f])), (shape, persp, f)
