@@ -373,8 +373,11 @@ int kcmc_warp_perspective_u16(kcmc_ctx* ctx, const uint16_t* src_dev, uint16_t* 
  * the plan and keeps plan_dev alive until they have run).  perspective != 0: M_dev
  * [n_frames, 3, 3] and warpPerspective, else [n_frames, 2, 3] and warpAffine.  Results are
  * those of kcmc_warp_affine_u16 / kcmc_warp_perspective_u16 (which run both parts on one
- * stream).  The pipeline queues the plan on its analysis stream right behind RANSAC, so
- * the kernel stream goes from one slab's warp tiles straight to the next slab's.
+ * stream).  kcmc_warp_u16_planned must get the n_frames, H, W, C and perspective the plan
+ * was made with (the plan is not self-describing; a mismatch reads it with the wrong
+ * layout).  One plan serves any number of stacks of that shape.  (Planning on the
+ * pipeline's analysis stream behind RANSAC measured slower than the one-call warp,
+ * DESIGN 6f, so the pipeline keeps the one-call form.)
  * kcmc_warp_plan_bytes returns -1 for unsupported sizes. */
 long long kcmc_warp_plan_bytes(int n_frames, int H, int W, int C, int perspective);
 int kcmc_warp_u16_plan(kcmc_ctx* ctx, const double* M_dev, int n_frames, int H, int W, int C, int perspective,

@@ -859,7 +859,9 @@ def warp_planned(frames: torch.Tensor, plan: torch.Tensor, out: Optional[torch.T
     _require(frames, "frames", torch.uint16, dev)
     _require(plan, "plan", torch.uint8, dev, 1)
     F, H, W, C = _warp_shape(frames.shape)
-    persp = bool(getattr(plan, "kcmc_perspective", False))
+    persp = getattr(plan, "kcmc_perspective", None)
+    if persp is None:  # the layout (affine or perspective) travels with the tensor warp_plan made
+        raise ValueError("plan must be the tensor warp_plan returned")
     if plan.numel() < int(_lib.load().kcmc_warp_plan_bytes(F, H, W, C, int(persp))):
         raise ValueError("plan was made for other frames")
     if out is None:
