@@ -1,0 +1,54 @@
+"""A longer run of the seeded fuzz sweeps of tests/test_gpu_fuzz.py (bug hunting on the GPU
+box, not part of the suite): every test function over seeds [start, start + n), failures
+printed with their seed so they can be pinned as a regular test case.
+
+    python tools/debug/fuzz_campaign.py <n> [start] [name-filter]
+"""
+import os
+import sys
+import time
+import traceback
+
+import torch
+
+R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [R, os.path.join(R, "oracle"), os.path.join(R, "tests")]
+import kcmc_amd  # noqa: E402,F401
+import test_gpu_fuzz as T  # noqa: E402
+
+n = int(sys.argv[1])
+start = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
+filt = sys.argv[3] if len(sys.argv) > 3 else ""
+dev = torch.device("cuda", 0)
+cases = [("warp", lambda s: T.test_warp_fuzz_vs_oracle(dev, s)),
+         ("knn_l2u8", lambda s: T.test_knn2_fuzz_vs_oracle(dev, "l2u8", s)),
+         ("knn_hamming", lambda s: T.test_knn2_fuzz_vs_oracle(dev, "hamming", s)),
+         ("knn_l2f32", lambda s: T.test_knn2_fuzz_vs_oracle(dev, "l2f32", s)),
+         ("ransac_rigid", lambda s: T.test_ransac_rigid_fuzz_vs_oracle(dev, s)),
+         ("ransac_affine", lambda s: T.test_ransac_model_fuzz_vs_oracle(dev, "affine", s)),
+         ("ransac_projective", lambda s: T.test_ransac_model_fuzz_vs_oracle(dev, "projective", s)),
+         ("filters", lambda s: T.test_match_filters_fuzz_vs_oracle(dev, s)),
+         ("slab", lambda s: T.test_slab_end_to_end_fuzz_vs_oracle(dev, s)),
+         ("pyr_norm", lambda s: T.test_pyr_down_and_normalize_fuzz(dev, s)),
+         ("orb", lambda s: T.test_orb_detect_fuzz_vs_oracle(dev, s)),
+         ("split", lambda s: T.test_multidevice_split_fuzz(dev, s))]
+fails = 0
+for name, fn in cases:
+    if filt and filt not in name:
+        continue
+    t0 = time.time()
+    bad = []
+    for s in range(start, start + n):
+        if (s - start) % 250 == 249:
+            print(f"  {name}: {s - start + 1}/{n} ({len(bad)} failed, {time.time() - t0:.0f} s)", flush=True)
+        try:
+            fn(s)
+        except Exception as e:  # noqa: BLE001 - report and go on
+            bad.append(s)
+            print(f"FAIL {name} seed {s}: {type(e).__name__}: {str(e)[:300]}", flush=True)
+            if len(bad) == 1:
+                traceback.print_exc()
+    fails += len(bad)
+    print(f"{name}: {n - len(bad)}/{n} ok in {time.time() - t0:.1f} s", flush=True)
+print(f"total failures: {fails}")
+sys.exit(1 if fails else 0)
