@@ -404,3 +404,54 @@ def test_warp_large_frames_vs_oracle(dev, shape, persp):
     out = fn(_t(imgs, dev), _t(Ms, dev)).cpu().numpy()
     for f in range(F):
         assert np.array_equal(out[f], ref(imgs[f], Ms[f])), (shape, persp, f)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_overlapped_slabs_fuzz(dev, seed):
+    """The pipelined schedule (OverlappedSlabs: streams, events, slot reuse, device maps and
+    the re-warp of model-less frames) on random slab sequences -- slab sizes that change from
+    slab to slab, model-less runs anywhere, the match beside the warp or ahead of it, the
+    three models, temporal downsampling, float or byte descriptors -- equal to align_slab
+    slab by slab."""
+    from kcmc_amd import pipeline, synthetic
+
+    rng = np.random.default_rng(9700 + seed)
+    model = str(rng.choice(["euclidean", "affine", "projective"]))
+    rate = int(rng.choice([1, 1, 2]))
+    descriptor = str(rng.choice(["u8", "u8", "f32"]))
+    beside = bool(rng.integers(0, 2)) and descriptor == "u8"
+    H, W = int(rng.integers(64, 200)), int(rng.integers(64, 260))
+    cfg = pipeline.AlignConfig(n_kp_global=int(rng.integers(12, 60)), ransac_model=model, frame_downsample_rate=rate)
+    slabs = []
+    for k in range(int(rng.integers(1, 5))):
+        S = int(rng.integers(3, 14))
+        D = 32 if descriptor == "u8" else 48
+        ks = synthetic.make_keypoints(S, int(rng.integers(60, 220)), D, (H, W), seed=9800 + 10 * seed + k, model=model,
+                                      descriptor=descriptor)
+        for f in rng.choice(S, int(rng.integers(0, S // 2 + 1)), replace=False):
+            a, b = ks.q_off[f], ks.q_off[f + 1]  # one descriptor row: no ratio survivor, no model
+            ks.des_q[a:b] = ks.des_q[a] if descriptor == "f32" else rng.integers(0, 256, (1, D), dtype=np.uint8)
+        frames = torch.from_numpy(np.ascontiguousarray(np.stack(
+            [np.roll(synthetic.make_texture((H, W), seed=k), (f, 2 * f), axis=(0, 1)) for f in range(S * rate)]))).to(dev)
+        slabs.append(pipeline.SlabInputs(frames, _t(ks.des_tpl, dev), _t(ks.kp_tpl, dev), _t(ks.des_q, dev),
+                                         _t(ks.kp_q, dev), _t(ks.q_off, dev), ks.q_off))
+    ref = []
+    for s in slabs:
+        try:
+            ref.append(pipeline.align_slab(s, cfg))
+        except Exception as e:  # noqa: BLE001 - the same error must come out of the pipeline
+            ref.append(e)
+    if any(isinstance(r, Exception) for r in ref):
+        with pytest.raises(type(next(r for r in ref if isinstance(r, Exception)))):
+            ov = pipeline.OverlappedSlabs(dev, cfg, match_beside=beside)
+            [ov.submit(s) for s in slabs] + ov.flush()
+            ov.synchronize()
+        return
+    ov = pipeline.OverlappedSlabs(dev, cfg, match_beside=beside)
+    got = [ov.submit(s) for s in slabs]
+    got = got[1:] + ov.flush()
+    ov.synchronize()
+    for r, g in zip(ref, got):
+        assert np.array_equal(r.affines, g.affines, equal_nan=True), seed
+        assert r.skipped == g.skipped and r.interpolated == g.interpolated, seed
+        assert torch.equal(r.aligned, g.aligned), seed

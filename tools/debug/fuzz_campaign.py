@@ -31,7 +31,8 @@ cases = [("warp", lambda s: T.test_warp_fuzz_vs_oracle(dev, s)),
          ("slab", lambda s: T.test_slab_end_to_end_fuzz_vs_oracle(dev, s)),
          ("pyr_norm", lambda s: T.test_pyr_down_and_normalize_fuzz(dev, s)),
          ("orb", lambda s: T.test_orb_detect_fuzz_vs_oracle(dev, s)),
-         ("split", lambda s: T.test_multidevice_split_fuzz(dev, s))]
+         ("split", lambda s: T.test_multidevice_split_fuzz(dev, s)),
+         ("overlapped", lambda s: T.test_overlapped_slabs_fuzz(dev, s))]
 fails = 0
 for name, fn in cases:
     if filt and filt not in name:
