@@ -33,6 +33,45 @@ cases = [("warp", lambda s: T.test_warp_fuzz_vs_oracle(dev, s)),
          ("orb", lambda s: T.test_orb_detect_fuzz_vs_oracle(dev, s)),
          ("split", lambda s: T.test_multidevice_split_fuzz(dev, s)),
          ("overlapped", lambda s: T.test_overlapped_slabs_fuzz(dev, s))]
+def knn_large(kind, seed):
+    """The matchers at config-4/5 sizes: n_tpl up to 6000, frames up to 5000 rows, D up to the
+    limit, exact template copies among the rows (ties), a few frames of 2 rows."""
+    import numpy as np
+
+    import oracle
+    from kcmc_amd import stages
+
+    rng = np.random.default_rng(50000 + seed)
+    if kind == "l2f32":
+        D = int(rng.choice([64, 100, 128]))
+        gen = lambda n: rng.normal(0, 1.0, (n, D)).astype(np.float32)  # noqa: E731
+    else:
+        D = int(rng.choice([32, 61, 64]))
+        gen = lambda n: rng.integers(0, 256, (n, D), dtype=np.uint8)  # noqa: E731
+    n_tpl = int(rng.integers(1000, 6001))
+    tpl = gen(n_tpl)
+    frames = []
+    for _ in range(int(rng.integers(1, 4))):
+        n_q = int(rng.choice([2, int(rng.integers(1000, 5001))]))
+        q = gen(n_q)
+        k = n_q // 3
+        q[:k] = tpl[rng.integers(0, n_tpl, k)]
+        frames.append(q)
+    off = np.zeros(len(frames) + 1, np.int32)
+    off[1:] = np.cumsum([len(q) for q in frames])
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    fn = stages.knn2_hamming if kind == "hamming" else stages.knn2_l2u8
+    idx, dist = fn(t(tpl), t(np.concatenate(frames)), t(off), int(np.diff(off).max()))
+    idx, dist = idx.cpu().numpy(), dist.cpu().numpy()
+    ora = {"l2u8": oracle.knn2_l2u8, "hamming": oracle.knn2_hamming, "l2f32": oracle.knn2_l2f32}[kind]
+    for f, q in enumerate(frames):
+        ri, rd = ora(tpl, q)
+        assert np.array_equal(idx[f], ri), (kind, seed, f, n_tpl, len(q), D)
+        assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), (kind, seed, f)
+
+
+cases += [("large_knn_l2u8", lambda s: knn_large("l2u8", s)), ("large_knn_hamming", lambda s: knn_large("hamming", s)),
+          ("large_knn_l2f32", lambda s: knn_large("l2f32", s))]
 fails = 0
 for name, fn in cases:
     if filt and filt not in name:
