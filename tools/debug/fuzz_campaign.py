@@ -70,6 +70,31 @@ def knn_large(kind, seed):
         assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), (kind, seed, f)
 
 
+def warp_large(seed):
+    """The warp at config sizes (1080p / 4K, C = 1 / 3 / 4, 1-2 frames) with the sweep's map
+    families, affine and perspective, forward and inverse."""
+    import numpy as np
+
+    import oracle
+    from kcmc_amd import stages
+
+    rng = np.random.default_rng(60000 + seed)
+    H, W = [(1080, 1920), (2160, 3840), (1079, 1917)][int(rng.integers(0, 3))]
+    C = int(rng.choice([1, 3, 4]))
+    F = int(rng.integers(1, 3))
+    shape = (F, H, W) if C == 1 else (F, H, W, C)
+    imgs = T._values(rng, shape)
+    persp = bool(rng.integers(0, 2))
+    Ms = np.stack([(T._perspective if persp else T._affine)(rng, H, W) for _ in range(F)])
+    inv = bool(rng.integers(0, 2))
+    fn = stages.warp_perspective_u16 if persp else stages.warp_affine_u16
+    ref = oracle.warp_perspective_u16 if persp else oracle.warp_affine_u16
+    out = fn(torch.from_numpy(imgs).to(dev), torch.from_numpy(Ms).to(dev), inverse_map=inv).cpu().numpy()
+    for f in range(F):
+        assert np.array_equal(out[f], ref(imgs[f], Ms[f], inverse_map=inv)), (seed, shape, persp, inv, f)
+
+
+cases += [("large_warp", warp_large)]
 cases += [("large_knn_l2u8", lambda s: knn_large("l2u8", s)), ("large_knn_hamming", lambda s: knn_large("hamming", s)),
           ("large_knn_l2f32", lambda s: knn_large("l2f32", s))]
 fails = 0
