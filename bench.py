@@ -605,7 +605,8 @@ def main():
         "dtype": ("u16 frames; " + ("f32 descriptors: fp16 MFMA candidate search (certified bound) + exact f64 re-rank"
                                     if bc.descriptor == "f32" else "u8 descriptors: i8 MFMA exact integer distances")
                   + ", f64 RANSAC, f32 warp weights"),
-        "data": "synthetic (seeded jittered 1080p texture + ORB-shaped keypoints; no detector in image)",
+        "data": (f"synthetic (seeded jittered {bc.W}x{bc.H}{'x%d' % bc.C if bc.C > 1 else ''} u16 texture + "
+                 f"{'SIFT' if bc.descriptor == 'f32' else 'ORB/AKAZE'}-shaped keypoints; no detector in image)"),
         "config": {
             "workload": bc.workload,
             "frames_per_gpu": args.frames, "height": bc.H, "width": bc.W, "channels": bc.C, "n_tpl": bc.n_tpl,
