@@ -26,9 +26,9 @@
 //     the winner's inlier mask and model.
 // refit_frame (fused at the end of each scoring workgroup) -- one wave per frame: the final total-least-squares fit on
 //   the inliers (fit.py:871-875 -> ProjectiveTransform.estimate): Hartley
-//   normalisation, A^T A of the 2N x 7 (affine) / 2N x 9 (projective) system in fp64
-//   (its smallest eigenvector is the last right singular vector of A that skimage
-//   takes from np.linalg.svd), found by Cholesky inverse iteration, then
+//   normalisation, the last right singular vector of the 2N x 7 (affine) / 2N x 9
+//   (projective) system A that skimage takes from np.linalg.svd -- by a Givens QR of A in
+//   the wave and a one-sided Jacobi SVD of its triangle, in fp64 -- then
 //   H = inv(N_dst) Hn N_src.  As in skimage, a refit with |v_last| <= 1e-8 keeps the
 //   hypothesis model and rms == 0 gives NaN.
 // Output params [F, 3, 3] (row-major), NaN where skimage returns no model, scaled for
@@ -769,72 +769,240 @@ __device__ __forceinline__ void ransac_model_score_frame(
 }
 
 // ------------------------------------------------------------------------ refit
-// Smallest eigenvector of a symmetric positive semi-definite n x n matrix by inverse
-// iteration on its Cholesky factor (pivots floored at trace * 2^-52, a shift far below
-// the second-smallest eigenvalue of any non-degenerate point set).  Every lane of the
-// wave runs it on identical data, so the iteration count is wave-uniform.
-template <int n>
-__device__ __forceinline__ void smallest_eigvec(const double (&A)[n][n], double (&x)[n]) {
-  double L[n][n];
-  double dinv[n];
-  double tr = 0.0;
-#pragma unroll
-  for (int i = 0; i < n; ++i) tr += A[i][i];
-  const double floor_v = tr * 2.220446049250313e-16 + DBL_MIN;
+// skimage takes the TLS solution from np.linalg.svd of the 2N x n system A (n = 7 affine,
+// 9 projective; _geometric.py:596-703).  The refit computes that right singular vector from
+// A itself, never from A^T A (whose smallest eigenvector carries the square of A's
+// condition number: the round-5 inverse iteration on A^T A missed skimage by up to 1e-3 on
+// a near-degenerate homography, and stalled on nearly equal singular values):
+//   1. Householder QR of A in the wave: each lane holds the two rows of up to P point pairs
+//      (chunks of 64 P pairs) and, in lanes 0..n-1, one row of the running triangle R;
+//      column j's reflection takes n - j wave sums;
+//   2. inverse iteration on R^T R (two triangular solves with R per step; pivots floored at
+//      |R|_F 2^-52) while it converges (successive iterates within 1e-15, at most 40 steps);
+//   3. otherwise (nearly equal smallest singular values) a one-sided Jacobi SVD of R, one row
+//      of R and of V per lane: V's column of the smallest R V column norm.
+// tools/debug/refit_spread.py restates all three in numpy: within 1e-11 of skimage on every
+// fuzz case of the GPU sweeps, where LAPACK's own drivers spread by ~1e-12.
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Sum over the 16 lanes of a DPP row: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror.  Each step adds a partner's value to one's own, so every lane of the row ends
+// with the bitwise same sum (a + b == b + a).
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  v += dpp_d<0x140>(v);
+  return v;
+}
+
+// Sum over the wave, the same value in every lane: the four row sums read from lanes 0, 16,
+// 32 and 48.
+__device__ __forceinline__ double wave_sum_u(double v) {
+  v = row16_sum(v);
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
+// One chunk of the Householder QR: the rows are the S data rows m[0..S-1] of every lane and,
+// in lanes 0..n-1, the triangle's row rr (row index = lane; rows < j are final at step j).
+// Column j is reflected onto lane j's rr[j] (LAPACK's sign: beta = -sign(x_j) |x|).
+template <int n, int S>
+__device__ __forceinline__ void householder_chunk(double (&m)[S][n], double (&rr)[n], int lane) {
 #pragma unroll
   for (int j = 0; j < n; ++j) {
-    double d = A[j][j];
+    const bool ract = lane >= j && lane < n;
+    const double xr = ract ? rr[j] : 0.0;
+    double part = xr * xr;
 #pragma unroll
-    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
-    if (!(d > floor_v)) d = floor_v;
-    const double ljj = sqrt(d);
-    L[j][j] = ljj;
-    dinv[j] = 1.0 / ljj;
+    for (int s = 0; s < S; ++s) part += m[s][j] * m[s][j];
+    const double alpha = wave_sum_u(part);
+    if (alpha == 0.0) continue;  // the column is zero below the diagonal: R[j][j] = 0 (uniform)
+    const double xj = readlane_d(rr[j], j);
+    const double nx = sqrt(alpha);
+    const double beta = xj >= 0.0 ? -nx : nx;
+    const double f2 = 1.0 / (alpha - beta * xj);  // 2 / v^T v, v = x - beta e_j
+    const double vr = lane == j ? xj - beta : xr;
+    double dot[n];
 #pragma unroll
-    for (int i = j + 1; i < n; ++i) {
-      double a = A[i][j];
+    for (int c = j + 1; c < n; ++c) {
+      double d = ract ? vr * rr[c] : 0.0;
 #pragma unroll
-      for (int k = 0; k < j; ++k) a -= L[i][k] * L[j][k];
-      L[i][j] = a * dinv[j];
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < n; ++i) x[i] = 1.0;
-  for (int it = 0; it < 200; ++it) {
-    double y[n], z[n];
-#pragma unroll
-    for (int i = 0; i < n; ++i) {
-      double a = x[i];
-#pragma unroll
-      for (int k = 0; k < i; ++k) a -= L[i][k] * y[k];
-      y[i] = a * dinv[i];
+      for (int s = 0; s < S; ++s) d += m[s][j] * m[s][c];
+      dot[c] = d;
     }
 #pragma unroll
-    for (int i = n - 1; i >= 0; --i) {
-      double a = y[i];
+    for (int c = j + 1; c < n; ++c) dot[c] = wave_sum_u(dot[c]) * f2;
 #pragma unroll
-      for (int k = i + 1; k < n; ++k) a -= L[k][i] * z[k];
-      z[i] = a * dinv[i];
-    }
-    double nn = 0.0, dot = 0.0;
+    for (int c = j + 1; c < n; ++c) {
+      if (ract) rr[c] -= vr * dot[c];
 #pragma unroll
-    for (int i = 0; i < n; ++i) {
-      nn += z[i] * z[i];
-      dot += z[i] * x[i];
+      for (int s = 0; s < S; ++s) m[s][c] -= m[s][j] * dot[c];
     }
-    const double s = (dot < 0.0 ? -1.0 : 1.0) / sqrt(nn);
-    double diff = 0.0;
+    if (lane == j) rr[j] = beta;
+    else if (ract) rr[j] = 0.0;
 #pragma unroll
-    for (int i = 0; i < n; ++i) {
-      const double v = z[i] * s;
-      diff = fmax(diff, fabs(v - x[i]));
-      x[i] = v;
-    }
-    if (it > 0 && diff < 1e-15) break;
+    for (int s = 0; s < S; ++s) m[s][j] = 0.0;
   }
 }
 
-// Workgroup g scores frames g, g + grid, ... (kcmc_set_ransac_grid; default one per frame).
+// One-sided (Hestenes) Jacobi on the n x n R held one row per lane (lane & 15 = row; rows
+// >= n zero; the four DPP rows of the wave identical, so every branch is uniform).  Returns
+// in v, in every lane, the column of V whose column of R V has the smallest norm.
+template <int n>
+__device__ __forceinline__ void jacobi_smallest(double (&rr)[n], double (&vr)[n], double (&v)[n]) {
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    double nrm[n];
+#pragma unroll
+    for (int j = 0; j < n; ++j) nrm[j] = row16_sum(rr[j] * rr[j]);
+    bool rotated = false;
+#pragma unroll
+    for (int p = 0; p < n - 1; ++p)
+#pragma unroll
+      for (int q = p + 1; q < n; ++q) {
+        const double g = row16_sum(rr[p] * rr[q]);
+        const double a = nrm[p], b = nrm[q];
+        if (fabs(g) > 7.105427357601002e-15 * sqrt(fmax(a * b, 0.0))) {  // 32 eps: above a dot's rounding
+          const double zeta = (b - a) / (2.0 * g);
+          const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+          const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+          const double rp = rr[p], rq = rr[q], vp = vr[p], vq = vr[q];
+          rr[p] = c * rp - s * rq;
+          rr[q] = s * rp + c * rq;
+          vr[p] = c * vp - s * vq;
+          vr[q] = s * vp + c * vq;
+          nrm[p] = a - t * g;
+          nrm[q] = b + t * g;
+          rotated = true;
+        }
+      }
+    if (!rotated) break;
+  }
+  int js = 0;
+  double best = INFINITY;
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+    const double q = row16_sum(rr[j] * rr[j]);
+    if (q < best) {
+      best = q;
+      js = j;
+    }
+  }
+  double mine = 0.0;
+#pragma unroll
+  for (int j = 0; j < n; ++j)
+    if (j == js) mine = vr[j];
+#pragma unroll
+  for (int i = 0; i < n; ++i) v[i] = readlane_d(mine, i);
+}
+
+// Inverse iteration on R^T R (every lane holds R whole).  Returns false if it has not
+// converged in 40 steps (the two smallest singular values nearly equal).
+template <int n>
+__device__ __forceinline__ bool inverse_iteration(const double (&R)[n][n], double (&x)[n]) {
+  double fro = 0.0;
+#pragma unroll
+  for (int i = 0; i < n; ++i)
+#pragma unroll
+    for (int j = i; j < n; ++j) fro += R[i][j] * R[i][j];
+  const double floor_v = sqrt(fro) * 2.220446049250313e-16 + DBL_MIN;
+  double dinv[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    double d = R[i][i];
+    if (!(fabs(d) > floor_v)) d = floor_v;
+    dinv[i] = 1.0 / d;
+  }
+#pragma unroll
+  for (int i = 0; i < n; ++i) x[i] = 1.0;
+  for (int it = 0; it < 40; ++it) {
+    double y[n], z[n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {  // R^T y = x
+      double a = x[i];
+#pragma unroll
+      for (int k = 0; k < i; ++k) a -= R[k][i] * y[k];
+      y[i] = a * dinv[i];
+    }
+#pragma unroll
+    for (int i = n - 1; i >= 0; --i) {  // R z = y
+      double a = y[i];
+#pragma unroll
+      for (int k = i + 1; k < n; ++k) a -= R[i][k] * z[k];
+      z[i] = a * dinv[i];
+    }
+    double nn = 0.0, dt = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      nn += z[i] * z[i];
+      dt += z[i] * x[i];
+    }
+    const double sc = (dt < 0.0 ? -1.0 : 1.0) / sqrt(nn);
+    double diff = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const double v = z[i] * sc;
+      diff = fmax(diff, fabs(v - x[i]));
+      x[i] = v;
+    }
+    if (it > 0 && diff < 1e-15) return true;
+  }
+  return false;
+}
+
+// The triangle of A's rows (point pairs k = base + lane + 64 i, i < P, inliers only).
+template <int MODEL, int P, class PointFn, class InlierFn>
+__device__ __forceinline__ void qr_rows(int N, int lane, PointFn point, InlierFn inlier, double csx, double csy,
+                                        double nfs, double cdx, double cdy, double nfd,
+                                        double (&rr)[MODEL == KCMC_MODEL_AFFINE ? 7 : 9]) {
+  constexpr int n = MODEL == KCMC_MODEL_AFFINE ? 7 : 9;
+  for (int base = 0; base < N; base += 64 * P) {
+    double m[2 * P][n];
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+#pragma unroll
+      for (int c = 0; c < n; ++c) m[2 * i][c] = m[2 * i + 1][c] = 0.0;
+      const int k = base + lane + 64 * i;
+      if (k < N && inlier(k)) {
+        double x, y, u, v;
+        point(k, x, y, u, v);
+        const double xs = (x - csx) * nfs, ys = (y - csy) * nfs;
+        const double e = (u - cdx) * nfd, g = (v - cdy) * nfd;
+        // skimage's rows (_geometric.py:665-680): (s, 0, -e xs, -e ys, e), (0, s, -g xs, -g ys, g)
+        // with s = (xs, ys, 1); the affine system keeps columns 0-5 and 8
+        m[2 * i][0] = m[2 * i + 1][3] = xs;
+        m[2 * i][1] = m[2 * i + 1][4] = ys;
+        m[2 * i][2] = m[2 * i + 1][5] = 1.0;
+        if constexpr (MODEL == KCMC_MODEL_AFFINE) {
+          m[2 * i][6] = e;
+          m[2 * i + 1][6] = g;
+        } else {
+          m[2 * i][6] = -e * xs;
+          m[2 * i][7] = -e * ys;
+          m[2 * i][8] = e;
+          m[2 * i + 1][6] = -g * xs;
+          m[2 * i + 1][7] = -g * ys;
+          m[2 * i + 1][8] = g;
+        }
+      }
+    }
+    householder_chunk<n, 2 * P>(m, rr, lane);
+  }
+}
+
+// Workgroup g scores frames g, g + grid, ... (the product launches one per frame).
 // (projective: 2 waves per SIMD, its scoring alone needs 231 VGPRs)
 template <int MODEL, bool LARGE>
 __global__ __launch_bounds__(kThreads, MODEL == KCMC_MODEL_AFFINE ? 1 : 2) void
@@ -913,99 +1081,36 @@ __device__ __forceinline__ void refit_frame(int N, int lane, PointFn point, Inli
   }
   const double nfs = kSqrt2 / rms_s, nfd = kSqrt2 / rms_d;
 
-  // Normal-equation sums of the normalised system.  Per point, with s = (xs, ys, 1),
-  // e = xd, g = yd, q = e^2 + g^2:  affine rows (s, 0, e), (0, s, g);
-  // projective rows (s, 0, -e xs, -e ys, e), (0, s, -g xs, -g ys, g).
-  // acc[0..5] = sums of xx, xy, yy, x, y, 1; then per weight w the same six moments
-  // times w (projective: w = e, g, q) or (affine) e*s, g*s, q.
-  constexpr int NA = MODEL == KCMC_MODEL_AFFINE ? 13 : 24;
-  double acc[NA];
+  // 1. QR: lane i (< n) ends with row i of R
+  double rr[n];
 #pragma unroll
-  for (int a = 0; a < NA; ++a) acc[a] = 0.0;
-  for (int k = lane; k < N; k += 64)
-    if (inlier(k)) {
-      double x, y, u, v;
-      point(k, x, y, u, v);
-      const double xs = (x - csx) * nfs, ys = (y - csy) * nfs;
-      const double e = (u - cdx) * nfd, g = (v - cdy) * nfd;
-      const double q = e * e + g * g;
-      const double xx = xs * xs, xy = xs * ys, yy = ys * ys;
-      acc[0] += xx;
-      acc[1] += xy;
-      acc[2] += yy;
-      acc[3] += xs;
-      acc[4] += ys;
-      acc[5] += 1.0;
-      if constexpr (MODEL == KCMC_MODEL_AFFINE) {
-        acc[6] += e * xs;
-        acc[7] += e * ys;
-        acc[8] += e;
-        acc[9] += g * xs;
-        acc[10] += g * ys;
-        acc[11] += g;
-        acc[12] += q;
-      } else {
-        const double w[3] = {e, g, q};
-#pragma unroll
-        for (int b = 0; b < 3; ++b) {
-          acc[6 + 6 * b] += w[b] * xx;
-          acc[7 + 6 * b] += w[b] * xy;
-          acc[8 + 6 * b] += w[b] * yy;
-          acc[9 + 6 * b] += w[b] * xs;
-          acc[10 + 6 * b] += w[b] * ys;
-          acc[11 + 6 * b] += w[b];
-        }
-      }
-    }
-#pragma unroll
-  for (int a = 0; a < NA; ++a) acc[a] = wave_sum(acc[a]);
-
-  double A[n][n];
+  for (int j = 0; j < n; ++j) rr[j] = 0.0;
+  if (N <= 64)
+    qr_rows<MODEL, 1>(N, lane, point, inlier, csx, csy, nfs, cdx, cdy, nfd, rr);
+  else
+    qr_rows<MODEL, 2>(N, lane, point, inlier, csx, csy, nfs, cdx, cdy, nfd, rr);
+  // 2. R in every lane, inverse iteration on it
+  double R[n][n];
 #pragma unroll
   for (int i = 0; i < n; ++i)
 #pragma unroll
-    for (int j = 0; j < n; ++j) A[i][j] = 0.0;
-  // the two identical 3x3 blocks: sum s s^T
-  const double ss[3][3] = {{acc[0], acc[1], acc[3]}, {acc[1], acc[2], acc[4]}, {acc[3], acc[4], acc[5]}};
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      A[i][j] = ss[i][j];
-      A[3 + i][3 + j] = ss[i][j];
-    }
-  if constexpr (MODEL == KCMC_MODEL_AFFINE) {
-    const double es[3] = {acc[6], acc[7], acc[8]}, gs[3] = {acc[9], acc[10], acc[11]};
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      A[i][n - 1] = A[n - 1][i] = es[i];
-      A[3 + i][n - 1] = A[n - 1][3 + i] = gs[i];
-    }
-    A[n - 1][n - 1] = acc[12];
-  } else {
-    // s u^T with s = (xs, ys, 1), u = (xs, ys) -> moment indices [[xx, xy], [xy, yy], [x, y]]
-    const int su[3][2] = {{0, 1}, {1, 2}, {3, 4}};
-    const int sw[3] = {3, 4, 5};  // s * w -> [x, y, 1] moments
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        A[i][6 + j] = A[6 + j][i] = -acc[6 + su[i][j]];
-        A[3 + i][6 + j] = A[6 + j][3 + i] = -acc[12 + su[i][j]];
-      }
-      A[i][8] = A[8][i] = acc[6 + sw[i]];
-      A[3 + i][8] = A[8][3 + i] = acc[12 + sw[i]];
-    }
-    A[6][6] = acc[18];
-    A[6][7] = A[7][6] = acc[19];
-    A[7][7] = acc[20];
-    A[6][8] = A[8][6] = -acc[21];
-    A[7][8] = A[8][7] = -acc[22];
-    A[8][8] = acc[23];
-  }
-
+    for (int j = 0; j < n; ++j) R[i][j] = j >= i ? readlane_d(rr[j], i) : 0.0;
   double v[n];
-  smallest_eigvec<n>(A, v);
+  if (!inverse_iteration<n>(R, v)) {
+    // 3. nearly equal smallest singular values: Jacobi SVD of R (row lane & 15 in every DPP row)
+    const int my = lane & 15;
+    double jr[n], jv[n];
+#pragma unroll
+    for (int j = 0; j < n; ++j) {
+      double r = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; ++i)
+        if (i == my) r = R[i][j];
+      jr[j] = r;
+      jv[j] = j == my ? 1.0 : 0.0;
+    }
+    jacobi_smallest<n>(jr, jv, v);
+  }
   double Hm[9];
   if (fabs(v[n - 1]) <= 1e-8) {
     // np.isclose(V[-1, -1], 0): estimate() returns False and keeps the hypothesis model
@@ -1105,14 +1210,5 @@ extern "C" int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src, co
                                  int max_n, int trials, double thresh, double rate, int n_skip, double* out_params,
                                  uint8_t* out_inliers, int32_t* out_n_inliers, int32_t* out_best_trial,
                                  kcmc_stream_t stream) {
-  return ransac_model_impl(ctx, model, src, dst, pt_idx, pt_off, src_frame_stride, n_frames, max_n, trials, thresh, rate, n_skip, out_params, out_inliers, out_n_inliers, out_best_trial, ctx ? ctx->ransac_grid : 0, stream);
-}
-
-extern "C" int kcmc_ransac_model_grid(kcmc_ctx* ctx, int model, const double* src, const double* dst,
-                                 const int32_t* pt_idx, const int32_t* pt_off, int src_frame_stride, int n_frames,
-                                 int max_n, int trials, double thresh, double rate, int n_skip, double* out_params,
-                                 uint8_t* out_inliers, int32_t* out_n_inliers, int32_t* out_best_trial,
-                                 int max_workgroups, kcmc_stream_t stream) {
-  if (max_workgroups < 0) return fail(KCMC_EINVAL, "kcmc_ransac_model_grid: max_workgroups < 0");
-  return ransac_model_impl(ctx, model, src, dst, pt_idx, pt_off, src_frame_stride, n_frames, max_n, trials, thresh, rate, n_skip, out_params, out_inliers, out_n_inliers, out_best_trial, max_workgroups, stream);
+  return ransac_model_impl(ctx, model, src, dst, pt_idx, pt_off, src_frame_stride, n_frames, max_n, trials, thresh, rate, n_skip, out_params, out_inliers, out_n_inliers, out_best_trial, 0, stream);
 }

@@ -8,6 +8,7 @@
 #   alttests:<lib>:<-k expr>  the same -k subset against another build of the library (ab/<lib>.so)
 #   envtests:<VAR=val>:<-k expr>  the same -k subset with one extra environment variable
 #   smoke                 __graft_entry__.smoke() -> <out>/smoke.log
+#   fuzz:<n>:<start>[:<filter>]  tools/debug/fuzz_campaign.py over seeds [start, start + n) -> <out>/fuzz_<filter>.txt
 #   bench:<cfg>[:<tag>][:<args,comma,separated>]
 #                         bench.py --config <cfg> --cpu-sample 0 [args] -> <out>/<cfg>_<tag>.json
 #   abbench:<lib>:<cfg>:<tag>  the same against KCMC_LIB_PATH=<lib> (tools/ab_build.py) -> <out>/<cfg>_<tag>.json
@@ -53,6 +54,11 @@ for step in "$@"; do
         > "$OUT/tests_env.log" 2>&1
       rc=$?
       echo "envtests $a rc=$rc" >> "$OUT/tests_env.log"; tail -3 "$OUT/tests_env.log"
+      [ $rc -eq 0 ] || exit 1 ;;
+    fuzz)
+      timeout -k 10 900 python -u tools/debug/fuzz_campaign.py "$a" "$b" "${c:-}" > "$OUT/fuzz_${c:-all}.txt" 2>&1
+      rc=$?
+      grep -E "ok in|total" "$OUT/fuzz_${c:-all}.txt"
       [ $rc -eq 0 ] || exit 1 ;;
     smoke)
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit 1
