@@ -17,6 +17,10 @@ inside the timed region.  --serial runs the steps strictly one after another.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
+Without torchrun, `--gpus N > 1` starts the N rank processes itself (spawn_ranks: before
+any GPU call, one child per GPU with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), and refuses
+(exit 2) when fewer than N devices are visible -- it never reports one GPU for --gpus N.
+
 Rank 0 prints ONE JSON line.  value = frames aligned by all ranks / max-over-ranks
 wall time of the K timed steps.
 """
@@ -395,6 +399,57 @@ def load_traffic(config: str):
         return None, None
 
 
+def rank_envs(n: int, base_env: dict, port: int) -> list:
+    """The environment of each rank process spawn_ranks starts (torchrun's variables)."""
+    envs = []
+    for r in range(n):
+        e = dict(base_env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        envs.append(e)
+    return envs
+
+
+def check_devices(n: int, visible: int, one_device: bool) -> None:
+    """--gpus n needs n visible devices (unless every rank shares cuda:0, the rehearsal)."""
+    if n > visible and not one_device:
+        raise SystemExit(f"bench.py: --gpus {n} but only {visible} device(s) visible; refusing to report a "
+                         f"{visible}-GPU number as {n} GPUs (set KCMC_BENCH_ONE_DEVICE=1 with "
+                         f"KCMC_BENCH_BACKEND=gloo to rehearse {n} ranks on cuda:0)")
+
+
+def spawn_ranks(n: int, argv: list) -> int:
+    """Start `n` rank processes of this script (one per GPU) and wait for them; rank 0 prints
+    the JSON line.  Runs before this process touches the GPU (device_count() does not
+    initialise it on this image); the children are started, never exec'd into."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:  # a free rendezvous port on the loopback
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=e)
+             for e in rank_envs(n, os.environ, port)]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                r = p.poll()
+                if r is None:
+                    continue
+                procs.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in procs:  # one rank failed: the others would wait in a collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc if rc >= 0 else 1
+
+
 def single_process(args, bc: BenchConfig) -> dict:
     """The drop-in VideoAligner's multi-GPU path (kcmc_amd.multidevice.align_split): one
     process, one contiguous frame slab per device of ``devices`` (a device may repeat), the
@@ -492,16 +547,26 @@ def main():
     if args.single_process:
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
             raise SystemExit("--single-process runs in one process (not under torchrun)")
+        if not args.devices:
+            check_devices(args.gpus, torch.cuda.device_count(), False)
         print(json.dumps(single_process(args, bc)), flush=True)
         return
 
     # KCMC_BENCH_BACKEND=gloo + KCMC_BENCH_ONE_DEVICE=1: rehearsal of the multi-rank
     # path with every rank on cuda:0 (a 1-GPU box cannot host two RCCL ranks)
+    one_device = os.environ.get("KCMC_BENCH_ONE_DEVICE") == "1"
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        check_devices(args.gpus, torch.cuda.device_count(), one_device)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     backend = os.environ.get("KCMC_BENCH_BACKEND", "nccl")
     rank, world, local = kdist.init_from_env(backend)
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    if os.environ.get("KCMC_BENCH_ONE_DEVICE") == "1":
+        if args.gpus != 1:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+        log(f"note: WORLD_SIZE={world} without --gpus; using WORLD_SIZE")
+    if not one_device:
+        check_devices(world, torch.cuda.device_count(), False)
+    if one_device:
         local = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)

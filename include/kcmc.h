@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define KCMC_ABI_VERSION 1
+#define KCMC_ABI_VERSION 2
 
 enum {
   KCMC_OK = 0,
@@ -70,16 +70,6 @@ const char* kcmc_last_error(void);
 /* hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, stream): the pinned-host <-> device
  * transfers of a pipelined caller (e.g. kcmc_amd.pipeline) without a runtime binding of its own. */
 int kcmc_memcpy_async(void* dst, const void* src, size_t bytes, kcmc_stream_t stream);
-
-/* A stream of `device` whose kernels run on a fixed CU subset (hipExtStreamCreateWithCUMask):
- * the first `cus_per_se` CUs of EVERY shader engine of every XCD, or with `complement` the
- * other CUs of every shader engine.  The pipeline's analysis / warp stream split (no
- * reference counterpart: the reference's joblib pool has no device).  Every XCD and every
- * shader engine keeps CUs in both halves (a mask that empties an XCD can leave a dispatch's
- * workgroups unplaceable); KCMC_EUNSUPPORTED on a device whose CU count is not 8 XCDs x 4
- * shader engines x 8 CUs (the layout verified on MI355X). */
-int kcmc_stream_create_cu_split(int device, int cus_per_se, int complement, kcmc_stream_t* out);
-int kcmc_stream_destroy(kcmc_stream_t stream);
 
 /* Create / destroy the per-device context (holds the uploaded RANSAC hypothesis
  * tables).  `device` is a HIP device ordinal. */
@@ -157,24 +147,6 @@ int kcmc_match_frames_f32(kcmc_ctx* ctx, const float* des_tpl_dev, const double*
                           double d_lo, double d_hi, int32_t* out_idx_dev, float* out_dist_dev,
                           double* out_kp_ordered_dev, uint32_t* out_keep_bits_dev,
                           int32_t* out_counts_dev, kcmc_stream_t stream);
-/* The same match in two parts, so that an integrator can run the first on another stream
- * ahead of the second (measured at c5 beside the previous slab's warp: no gain).
- * kcmc_match_f32_prepare: the template statistics and the frames' fp16 tile images into
- * prep_dev (device, 256-byte aligned, kcmc_match_f32_prep_bytes(n_tpl, n_frames, max_nq)
- * bytes; -1 for negative sizes); kcmc_match_frames_f32_prepared: kcmc_match_frames_f32 on
- * a prepared prep_dev (same des_tpl / des_q / q_off; ordered after the prepare by the
- * caller).  Results identical to kcmc_match_frames_f32. */
-long long kcmc_match_f32_prep_bytes(int n_tpl, int n_frames, int max_nq);
-int kcmc_match_f32_prepare(kcmc_ctx* ctx, const float* des_tpl_dev, int n_tpl, int D, const float* des_q_dev,
-                           const int32_t* q_off_dev, int n_frames, int max_nq, void* prep_dev,
-                           long long prep_bytes, kcmc_stream_t stream);
-int kcmc_match_frames_f32_prepared(kcmc_ctx* ctx, const float* des_tpl_dev, const double* kp_tpl_dev,
-                                   int n_tpl, int D, const float* des_q_dev, const double* kp_q_dev,
-                                   const int32_t* q_off_dev, int n_frames, int max_nq, const void* prep_dev,
-                                   double ratio, double d_lo, double d_hi, int32_t* out_idx_dev,
-                                   float* out_dist_dev, double* out_kp_ordered_dev,
-                                   uint32_t* out_keep_bits_dev, int32_t* out_counts_dev,
-                                   kcmc_stream_t stream);
 
 /* ------------------------------------------------------- host: keypoint consensus
  * VA:224-286 on the host, reproducing CPython 3 set/Counter iteration order exactly:
@@ -223,15 +195,6 @@ int kcmc_consensus_vote_host(const uint32_t* keep_bits_host, int n_frames, int n
 int kcmc_consensus_merge(const int64_t* votes_host, int world, int n_tpl, int n_kp_global, int n_min,
                          int32_t* out_consensus_host, int32_t* out_votes_host, int* out_n_consensus,
                          int32_t* out_cons_pack_host);
-/* The same merge on the device (no host round trip in a pipelined step): votes_dev
- * [world, 2, n_tpl]; out_consensus_dev / out_votes_dev [n_kp_global] (the first nc valid);
- * out_meta_dev [2] = (nc, status: 0 ok, 1 fewer than n_min voted -- the caller raises
- * VideoAligner.AlignmentError --, 2 invalid votes); out_pack_dev [n_kp_global + ceil(n_tpl/32)]:
- * set(consensus) iteration order in [0, nc), the consensus bitmask from n_kp_global on.
- * n_tpl <= 4096 and n_kp_global <= 1024 (KCMC_EUNSUPPORTED otherwise). */
-int kcmc_consensus_merge_device(kcmc_ctx* ctx, const int64_t* votes_dev, int world, int n_tpl, int n_kp_global,
-                                int n_min, int32_t* out_consensus_dev, int32_t* out_votes_dev, int32_t* out_meta_dev,
-                                int32_t* out_pack_dev, kcmc_stream_t stream);
 /* Device lookup: cons_pack_dev = kcmc_consensus_merge's pack (nc entries + bitmask words);
  * out_pt_off_dev [n_frames + 1], out_pt_idx_dev [n_frames * nc]; scratch_dev of at least
  * kcmc_consensus_lookup_scratch_bytes(n_frames, nc) bytes (the CPython set emulation tables
@@ -240,13 +203,6 @@ long long kcmc_consensus_lookup_scratch_bytes(int n_frames, int nc);
 int kcmc_consensus_lookup(kcmc_ctx* ctx, const uint32_t* keep_bits_dev, int n_frames, int n_tpl,
                           const int32_t* cons_pack_dev, int nc, int32_t* out_pt_off_dev,
                           int32_t* out_pt_idx_dev, void* scratch_dev, kcmc_stream_t stream);
-/* kcmc_consensus_lookup on kcmc_consensus_merge_device's outputs: the consensus size is read
- * from meta_dev[0] on the device; out_pt_idx_dev [n_frames * min(n_kp_global, n_tpl)], scratch
- * of kcmc_consensus_lookup_scratch_bytes(n_frames, min(n_kp_global, n_tpl)) bytes. */
-int kcmc_consensus_lookup_device(kcmc_ctx* ctx, const uint32_t* keep_bits_dev, int n_frames, int n_tpl,
-                                 const int32_t* cons_pack_dev, int n_kp_global, const int32_t* meta_dev,
-                                 int32_t* out_pt_off_dev, int32_t* out_pt_idx_dev, void* scratch_dev,
-                                 kcmc_stream_t stream);
 int kcmc_consensus_lookup_host(const uint32_t* keep_bits_host, int n_frames, int n_tpl,
                                const int32_t* cons_iter_host, int nc, int32_t* out_pt_off_host,
                                int32_t* out_pt_idx_host);
@@ -270,14 +226,7 @@ int kcmc_hypothesis_table(int n, int trials, uint32_t seed, int min_samples, int
  * point count that frame batch will run RANSAC on. */
 int kcmc_ransac_prepare(kcmc_ctx* ctx, const int32_t* n_values_host, int count, int trials, uint32_t seed);
 
-/* RANSAC scoring launches (kcmc_ransac_rigid, kcmc_ransac_model) of this context use at
- * most max_workgroups workgroups, each scoring frames g, g + max_workgroups, ... in turn
- * (0, the default: one workgroup per frame).  Results do not depend on it; a narrow grid
- * keeps RANSAC on a few CU slots when it runs beside another kernel (the warp).  Not
- * stream-ordered: it applies to the calls made after it. */
-int kcmc_set_ransac_grid(kcmc_ctx* ctx, int max_workgroups);
-
-/* Batched rigid RANSAC, one frame per workgroup (see kcmc_set_ransac_grid).
+/* Batched rigid RANSAC, one frame per workgroup.
  * Point k of frame f (k < N_f = pt_off[f+1]-pt_off[f]):
  *   pt_idx_dev == NULL: src = src_dev[pt_off[f]+k], dst = dst_dev[pt_off[f]+k]
  *   pt_idx_dev != NULL: q = pt_idx[pt_off[f]+k]; src = src_dev[f*src_frame_stride + q],
@@ -298,15 +247,6 @@ int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src_dev, const double* dst_de
                       double spatial_rate, int n_skip, double* out_params_dev,
                       uint8_t* out_inliers_dev, int32_t* out_n_inliers_dev,
                       int32_t* out_best_trial_dev, kcmc_stream_t stream);
-/* kcmc_ransac_rigid with the scoring grid given per call (max_workgroups, 0 = one workgroup
- * per frame) instead of the context-wide kcmc_set_ransac_grid value: safe when several
- * callers share the context. */
-int kcmc_ransac_rigid_grid(kcmc_ctx* ctx, const double* src_dev, const double* dst_dev,
-                           const int32_t* pt_idx_dev, const int32_t* pt_off_dev, int src_frame_stride,
-                           int n_frames, int max_n, int trials, double residual_threshold,
-                           double spatial_rate, int n_skip, double* out_params_dev,
-                           uint8_t* out_inliers_dev, int32_t* out_n_inliers_dev,
-                           int32_t* out_best_trial_dev, int max_workgroups, kcmc_stream_t stream);
 
 /* ------------------------------------------------- K2 extension: affine / projective
  * The reference only fits EuclideanTransform (VA:311).  BASELINE configs 3-5 need the
@@ -337,13 +277,6 @@ int kcmc_ransac_model(kcmc_ctx* ctx, int model, const double* src_dev, const dou
                       double spatial_rate, int n_skip, double* out_params_dev,
                       uint8_t* out_inliers_dev, int32_t* out_n_inliers_dev,
                       int32_t* out_best_trial_dev, kcmc_stream_t stream);
-/* kcmc_ransac_model with a per-call scoring grid (see kcmc_ransac_rigid_grid). */
-int kcmc_ransac_model_grid(kcmc_ctx* ctx, int model, const double* src_dev, const double* dst_dev,
-                           const int32_t* pt_idx_dev, const int32_t* pt_off_dev, int src_frame_stride,
-                           int n_frames, int max_n, int trials, double residual_threshold,
-                           double spatial_rate, int n_skip, double* out_params_dev,
-                           uint8_t* out_inliers_dev, int32_t* out_n_inliers_dev,
-                           int32_t* out_best_trial_dev, int max_workgroups, kcmc_stream_t stream);
 
 /* ------------------------------------------------------------------ K3: warp
  * cv2.warpAffine(frame, M_f, (W, H), flags=INTER_LINEAR [| WARP_INVERSE_MAP]) for
@@ -365,25 +298,6 @@ int kcmc_warp_affine_u16(kcmc_ctx* ctx, const uint16_t* src_dev, uint16_t* dst_d
 int kcmc_warp_perspective_u16(kcmc_ctx* ctx, const uint16_t* src_dev, uint16_t* dst_dev,
                               const double* M_dev, int n_frames, int H, int W, int C, int inverse_map,
                               kcmc_stream_t stream);
-
-/* The warp in two parts (round 5): the plan -- OpenCV's map inversion, every tile's
- * source box and (affine) the per-frame row-origin table -- into a caller-owned device
- * buffer plan_dev of at least kcmc_warp_plan_bytes(...) bytes (16-byte aligned), queued
- * where the maps are produced, then the tiles, queued later (the caller orders them after
- * the plan and keeps plan_dev alive until they have run).  perspective != 0: M_dev
- * [n_frames, 3, 3] and warpPerspective, else [n_frames, 2, 3] and warpAffine.  Results are
- * those of kcmc_warp_affine_u16 / kcmc_warp_perspective_u16 (which run both parts on one
- * stream).  kcmc_warp_u16_planned must get the n_frames, H, W, C and perspective the plan
- * was made with (the plan is not self-describing; a mismatch reads it with the wrong
- * layout).  One plan serves any number of stacks of that shape.  (Planning on the
- * pipeline's analysis stream behind RANSAC measured slower than the one-call warp,
- * DESIGN 6f, so the pipeline keeps the one-call form.)
- * kcmc_warp_plan_bytes returns -1 for unsupported sizes. */
-long long kcmc_warp_plan_bytes(int n_frames, int H, int W, int C, int perspective);
-int kcmc_warp_u16_plan(kcmc_ctx* ctx, const double* M_dev, int n_frames, int H, int W, int C, int perspective,
-                       int inverse_map, void* plan_dev, long long plan_bytes, kcmc_stream_t stream);
-int kcmc_warp_u16_planned(kcmc_ctx* ctx, const uint16_t* src_dev, uint16_t* dst_dev, const void* plan_dev,
-                          int n_frames, int H, int W, int C, int perspective, kcmc_stream_t stream);
 
 /* ------------------------------------------- f2: normalisation front end (VA:100-104)
  * brightest = np.percentile(images, 99.99) (VA:479-482) needs two order statistics of

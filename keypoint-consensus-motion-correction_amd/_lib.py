@@ -18,15 +18,13 @@ KCMC_EHIP = 2
 KCMC_ENOMEM = 3
 KCMC_EUNSUPPORTED = 4
 KCMC_EALIGN = 5
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # Every symbol include/kcmc.h declares (checked by tests/test_capi.py).
 EXPORTED_SYMBOLS = (
     "kcmc_abi_version",
     "kcmc_last_error",
     "kcmc_memcpy_async",
-    "kcmc_stream_create_cu_split",
-    "kcmc_stream_destroy",
     "kcmc_create",
     "kcmc_destroy",
     "kcmc_knn2_l2u8",
@@ -34,9 +32,6 @@ EXPORTED_SYMBOLS = (
     "kcmc_match_filter",
     "kcmc_knn2_l2f32",
     "kcmc_match_frames_f32",
-    "kcmc_match_f32_prep_bytes",
-    "kcmc_match_f32_prepare",
-    "kcmc_match_frames_f32_prepared",
     "kcmc_knn2_hamming",
     "kcmc_match_frames_hamming",
     "kcmc_consensus",
@@ -44,25 +39,17 @@ EXPORTED_SYMBOLS = (
     "kcmc_consensus_vote",
     "kcmc_consensus_vote_host",
     "kcmc_consensus_merge",
-    "kcmc_consensus_merge_device",
     "kcmc_consensus_lookup_scratch_bytes",
     "kcmc_consensus_lookup",
-    "kcmc_consensus_lookup_device",
     "kcmc_consensus_lookup_host",
     "kcmc_params_boundary",
     "kcmc_hypothesis_table",
     "kcmc_ransac_prepare",
-    "kcmc_set_ransac_grid",
     "kcmc_ransac_rigid",
-    "kcmc_ransac_rigid_grid",
     "kcmc_ransac_prepare_samples",
     "kcmc_ransac_model",
-    "kcmc_ransac_model_grid",
     "kcmc_warp_affine_u16",
     "kcmc_warp_perspective_u16",
-    "kcmc_warp_plan_bytes",
-    "kcmc_warp_u16_plan",
-    "kcmc_warp_u16_planned",
     "kcmc_histogram_u16",
     "kcmc_lut_u16_to_u8",
     "kcmc_orb_detect",
@@ -100,8 +87,6 @@ _SIGNATURES = {
     "kcmc_abi_version": ([], I),
     "kcmc_last_error": ([], ctypes.c_char_p),
     "kcmc_memcpy_async": ([P, P, ctypes.c_size_t, P], I),
-    "kcmc_stream_create_cu_split": ([I, I, I, ctypes.POINTER(P)], I),
-    "kcmc_stream_destroy": ([P], I),
     "kcmc_create": ([I, ctypes.POINTER(P)], I),
     "kcmc_destroy": ([P], I),
     "kcmc_knn2_l2u8": ([P, P, I, I, P, P, I, I, P, P, P], I),
@@ -109,9 +94,6 @@ _SIGNATURES = {
     "kcmc_match_filter": ([P, P, P, P, P, P, I, I, D, D, D, P, P, P, P], I),
     "kcmc_knn2_l2f32": ([P, P, I, I, P, P, I, I, P, P, P], I),
     "kcmc_match_frames_f32": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
-    "kcmc_match_f32_prep_bytes": ([I, I, I], LL),
-    "kcmc_match_f32_prepare": ([P, P, I, I, P, P, I, I, P, LL, P], I),
-    "kcmc_match_frames_f32_prepared": ([P, P, P, I, I, P, P, P, I, I, P, D, D, D, P, P, P, P, P, P], I),
     "kcmc_knn2_hamming": ([P, P, I, I, P, P, I, I, P, P, P], I),
     "kcmc_match_frames_hamming": ([P, P, P, I, I, P, P, P, I, I, D, D, D, P, P, P, P, P, P], I),
     "kcmc_consensus": ([P, I, I, I, I, P, P, P, P, P], I),
@@ -121,23 +103,15 @@ _SIGNATURES = {
     "kcmc_consensus_merge": ([P, I, I, I, I, P, P, P, P], I),
     "kcmc_consensus_lookup_scratch_bytes": ([I, I], LL),
     "kcmc_consensus_lookup": ([P, P, I, I, P, I, P, P, P, P], I),
-    "kcmc_consensus_merge_device": ([P, P, I, I, I, I, P, P, P, P, P], I),
-    "kcmc_consensus_lookup_device": ([P, P, I, I, P, I, P, P, P, P, P], I),
     "kcmc_consensus_lookup_host": ([P, I, I, P, I, P, P], I),
     "kcmc_params_boundary": ([P, P, I, I, P, P], I),
     "kcmc_hypothesis_table": ([I, I, U32, I, P], I),
     "kcmc_ransac_prepare": ([P, P, I, I, U32], I),
-    "kcmc_set_ransac_grid": ([P, I], I),
     "kcmc_ransac_rigid": ([P, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, P], I),
-    "kcmc_ransac_rigid_grid": ([P, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, I, P], I),
     "kcmc_ransac_prepare_samples": ([P, I, P, I, I, U32], I),
     "kcmc_ransac_model": ([P, I, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, P], I),
-    "kcmc_ransac_model_grid": ([P, I, P, P, P, P, I, I, I, I, D, D, I, P, P, P, P, I, P], I),
     "kcmc_warp_affine_u16": ([P, P, P, P, I, I, I, I, I, P], I),
     "kcmc_warp_perspective_u16": ([P, P, P, P, I, I, I, I, I, P], I),
-    "kcmc_warp_plan_bytes": ([I, I, I, I, I], ctypes.c_longlong),
-    "kcmc_warp_u16_plan": ([P, P, I, I, I, I, I, I, P, ctypes.c_longlong, P], I),
-    "kcmc_warp_u16_planned": ([P, P, P, P, I, I, I, I, I, P], I),
     "kcmc_histogram_u16": ([P, P, ctypes.c_ulonglong, I, I, P, P], I),
     "kcmc_lut_u16_to_u8": ([P, P, ctypes.c_ulonglong, P, P, P], I),
     "kcmc_orb_detect": ([P, P, I, I, I, I, I, D, I, P, P, P, P, P, P], I),
@@ -222,7 +196,6 @@ class Context:
 
     def __init__(self, device: int):
         self.device = device
-        self.ransac_grid = 0  # the context-wide kcmc_set_ransac_grid value (stages.ransac_grid)
         self._h = P()
         check(load().kcmc_create(device, ctypes.byref(self._h)))
 

@@ -46,47 +46,6 @@ extern "C" int kcmc_memcpy_async(void* dst, const void* src, size_t bytes, kcmc_
   return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)stream), "hipMemcpyAsync");
 }
 
-// CU-mask layout of a 256-CU MI355X (tools/cu_mask_lab.hip, profiles/r02_cu_mask_layout.txt):
-// bit b of the mask selects XCD b % 8, shader engine (b / 8) % 4 of it and CU b / 32 of that
-// shader engine, so bits [0, 32 n) are the first n CUs of every shader engine.
-constexpr int kMaskXcds = 8, kMaskSes = 4, kMaskCusPerSe = 8;
-constexpr int kMaskBits = kMaskXcds * kMaskSes * kMaskCusPerSe;
-
-extern "C" int kcmc_stream_create_cu_split(int device, int cus_per_se, int complement, kcmc_stream_t* out) {
-  if (!out) return fail(KCMC_EINVAL, "kcmc_stream_create_cu_split: out is NULL");
-  if (cus_per_se < 1 || cus_per_se >= kMaskCusPerSe)
-    return fail(KCMC_EINVAL, "kcmc_stream_create_cu_split: cus_per_se must be in [1, 7] (both halves keep CUs "
-                             "in every shader engine)");
-  int n = 0;
-  KCMC_TRY(hip_check(hipGetDeviceCount(&n), "hipGetDeviceCount"));
-  if (device < 0 || device >= n) return fail(KCMC_EINVAL, "kcmc_stream_create_cu_split: device out of range");
-  int cus = 0;
-  KCMC_TRY(hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device),
-                     "hipDeviceGetAttribute(CU count)"));
-  if (cus != kMaskBits)
-    return fail(KCMC_EUNSUPPORTED, "kcmc_stream_create_cu_split: the CU-mask layout is known for 256-CU devices "
-                                   "only (this one has " + std::to_string(cus) + ")");
-  uint32_t mask[kMaskBits / 32];
-  for (int w = 0; w < kMaskBits / 32; ++w) {
-    const bool first = w < cus_per_se;  // word w = CU w of every (XCD, shader engine)
-    mask[w] = (first != (complement != 0)) ? 0xffffffffu : 0u;
-  }
-  int prev = 0;
-  hipGetDevice(&prev);
-  KCMC_TRY(hip_check(hipSetDevice(device), "hipSetDevice"));
-  hipStream_t s = nullptr;
-  const int rc = hip_check(hipExtStreamCreateWithCUMask(&s, kMaskBits / 32, mask), "hipExtStreamCreateWithCUMask");
-  hipSetDevice(prev);
-  KCMC_TRY(rc);
-  *out = (kcmc_stream_t)s;
-  return KCMC_OK;
-}
-
-extern "C" int kcmc_stream_destroy(kcmc_stream_t stream) {
-  if (!stream) return KCMC_OK;
-  return hip_check(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
-}
-
 extern "C" int kcmc_create(int device, kcmc_ctx** out) {
   if (!out) return fail(KCMC_EINVAL, "kcmc_create: out is NULL");
   int n = 0;
@@ -205,13 +164,6 @@ static void free_tables(kcmc_ctx* ctx) {
   ctx->hyp = nullptr;
   ctx->hyp_off = nullptr;
   ctx->hyp_off_len = 0;
-}
-
-extern "C" int kcmc_set_ransac_grid(kcmc_ctx* ctx, int max_workgroups) {
-  if (!ctx) return fail(KCMC_EINVAL, "kcmc_set_ransac_grid: ctx is NULL");
-  if (max_workgroups < 0) return fail(KCMC_EINVAL, "kcmc_set_ransac_grid: max_workgroups < 0");
-  ctx->ransac_grid = max_workgroups;
-  return KCMC_OK;
 }
 
 extern "C" int kcmc_ransac_prepare(kcmc_ctx* ctx, const int32_t* n_values, int count, int trials, uint32_t seed) {

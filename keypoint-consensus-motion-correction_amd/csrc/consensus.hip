@@ -291,13 +291,9 @@ __device__ __forceinline__ int wave_compact(bool take, int32_t key, int32_t* dst
 }
 
 __global__ __launch_bounds__(64) void lookup_order_kernel(
-    const uint32_t* __restrict__ keep, int F, int W, const int32_t* __restrict__ cons_iter, int nc_arg,
-    const int32_t* __restrict__ nc_dev, const uint32_t* __restrict__ cons_bits, const int32_t* __restrict__ pt_off,
-    int32_t* __restrict__ pt_idx, int32_t* __restrict__ scratch, uint32_t cap, int r_lds, int s_lds) {
-  // nc_dev: the consensus size written by consensus_merge_kernel (the launch was sized for
-  // nc_arg >= it); cap, r_lds and s_lds follow nc_arg (a table of cap entries holds any set
-  // of up to nc_arg keys)
-  const int nc = nc_dev ? *nc_dev : nc_arg;
+    const uint32_t* __restrict__ keep, int F, int W, const int32_t* __restrict__ cons_iter, int nc,
+    const uint32_t* __restrict__ cons_bits, const int32_t* __restrict__ pt_off, int32_t* __restrict__ pt_idx,
+    int32_t* __restrict__ scratch, uint32_t cap, int r_lds, int s_lds) {
   // LDS: [W] frame words, [W] consensus words, [nc] staged keys, then the R tables
   // [2 cap] when r_lds and the S tables [2 cap] when s_lds
   extern __shared__ uint32_t lds[];
@@ -409,136 +405,6 @@ __global__ __launch_bounds__(64) void lookup_order_kernel(
   }
 }
 
-// Counter.most_common(n_kp_global) (VA:240) and set(consensus) (VA:248) on the device, from
-// the (all-gathered) votes [world, 2, n_tpl] (row 0 counts, row 1 first-occurrence keys) --
-// hostalg.cpp merge_impl, so that a pipelined step needs no host round trip between the
-// vote and the lookup (c3 trace: 0.12 ms from the vote to the lookup through the host).
-// One workgroup: sums / minima per template, a bitonic sort by (count desc, key asc) of the
-// P >= n_tpl slots in LDS (the keys of voted templates are distinct: the order is total),
-// the first nc = min(n_kp_global, voted) of it, and the iteration order of a CPython set
-// built from them (ascending when every key is below the final table size, else thread 0
-// replays the insertions).  Outputs: cons [n_kp_global] / votes [n_kp_global] (first nc),
-// meta [2] = (nc, 0 | 1: fewer than n_min voted (AlignmentError, VA:241-244) | 2: invalid
-// votes), pack = iteration order [0, n_kp_global) then the bitmask words.
-// 256 threads: one wave per SIMD fits in the slot a full warp grid leaves free (7 x 4-wave
-// tiles per CU); a 1024-thread workgroup waited for the warp to drain (c3 trace: 0.42 ms)
-constexpr int kMergeThreads = 256;
-constexpr int kMergeMaxTpl = 4096;
-constexpr int kMergeMaxCons = 1024;
-
-__host__ __device__ inline int merge_sort_slots(int n_tpl) {
-  int P = 2;
-  while (P < n_tpl) P <<= 1;
-  return P;
-}
-
-__host__ __device__ inline size_t merge_lds_bytes(int n_tpl, int n_kp_global) {
-  const size_t P = (size_t)merge_sort_slots(n_tpl);
-  return P * 20 + (size_t)n_kp_global * 4 + (size_t)pyset_table_size((uint32_t)n_kp_global) * 8;
-}
-
-__global__ __launch_bounds__(kMergeThreads) void consensus_merge_kernel(
-    const long long* __restrict__ votes, int world, int n_tpl, int n_kp_global, int n_min,
-    int32_t* __restrict__ out_cons, int32_t* __restrict__ out_votes, int32_t* __restrict__ meta,
-    int32_t* __restrict__ pack) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int P = merge_sort_slots(n_tpl);
-  long long* sc = reinterpret_cast<long long*>(smem);   // [P] counts (-1: padding)
-  long long* sk = sc + P;                                // [P] first-occurrence keys
-  int32_t* si = reinterpret_cast<int32_t*>(sk + P);      // [P] template index
-  int32_t* ord = si + P;                                 // [n_kp_global] the consensus, most_common order
-  int32_t* tab = ord + n_kp_global;                      // [2 cap] set tables
-  __shared__ int nvoted, bad, kmax;
-  __shared__ uint32_t bits[kMergeMaxTpl / 32];
-  __shared__ int woff[kMergeMaxTpl / 32 + 1];
-  const int tid = threadIdx.x;
-  const int W = (n_tpl + 31) / 32;
-  if (tid == 0) {
-    nvoted = 0;
-    bad = 0;
-    kmax = -1;
-  }
-  for (int w = tid; w < W; w += kMergeThreads) bits[w] = 0u;
-  __syncthreads();
-  for (int t = tid; t < P; t += kMergeThreads) {
-    long long c = -1, k = LLONG_MAX;
-    if (t < n_tpl) {
-      c = 0;
-      for (int r = 0; r < world; ++r) {
-        const long long* v = votes + (size_t)r * 2 * (size_t)n_tpl;
-        c += v[t];
-        k = min(k, v[n_tpl + t]);
-      }
-      if (c < 0 || (c > 0 && k == LLONG_MAX)) atomicOr(&bad, 1);
-      if (c > 0) atomicAdd(&nvoted, 1);
-      if (c < 0) c = 0;
-    }
-    sc[t] = c;
-    sk[t] = k;
-    si[t] = t;
-  }
-  // bitonic sort, "first" = (count desc, key asc); padding (count -1) sorts last
-  for (int size = 2; size <= P; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      __syncthreads();
-      for (int i = tid; i < P / 2; i += kMergeThreads) {
-        const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-        const bool asc = (lo & size) == 0;
-        const long long ca = sc[lo], cb = sc[hi], ka = sk[lo], kb = sk[hi];
-        const bool hi_first = cb > ca || (cb == ca && kb < ka);
-        if (hi_first == asc) {
-          sc[lo] = cb;
-          sc[hi] = ca;
-          sk[lo] = kb;
-          sk[hi] = ka;
-          const int32_t t = si[lo];
-          si[lo] = si[hi];
-          si[hi] = t;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  const int nc = min(n_kp_global, nvoted);
-  for (int k = tid; k < nc; k += kMergeThreads) {
-    const int32_t t = si[k];
-    out_cons[k] = t;
-    out_votes[k] = (int32_t)sc[k];
-    ord[k] = t;
-    atomicMax(&kmax, t);
-    atomicOr(&bits[t >> 5], 1u << (t & 31));
-  }
-  if (tid == 0) {
-    meta[0] = nc;
-    meta[1] = bad ? 2 : (nc < n_min ? 1 : 0);
-  }
-  __syncthreads();
-  for (int w = tid; w < W; w += kMergeThreads) pack[n_kp_global + w] = (int32_t)bits[w];
-  const uint32_t cap = pyset_table_size((uint32_t)nc);
-  if ((uint32_t)kmax < cap) {
-    // every key in its home slot: the set iterates in ascending key order
-    if (tid == 0) {
-      int o = 0;
-      for (int w = 0; w < W; ++w) {
-        woff[w] = o;
-        o += __popc(bits[w]);
-      }
-    }
-    __syncthreads();
-    for (int w = tid; w < W; w += kMergeThreads) {
-      int o = woff[w];
-      for (uint32_t b = bits[w]; b; b &= b - 1) pack[o++] = 32 * w + __ffs(b) - 1;
-    }
-  } else if (tid == 0) {
-    DevPySet S;
-    S.init(tab, tab + cap);
-    for (int k = 0; k < nc; ++k) S.add(ord[k]);
-    int o = 0;
-    for (uint32_t slot = 0; slot <= S.mask; ++slot)
-      if (S.t[slot] >= 0) pack[o++] = S.t[slot];
-  }
-}
-
 // First / last frame without NaN among params [F, E] and their parameters.
 constexpr int kBoundThreads = 256;
 __global__ __launch_bounds__(kBoundThreads) void params_boundary_kernel(const double* __restrict__ params, int F, int E,
@@ -608,25 +474,6 @@ extern "C" int kcmc_consensus_vote(kcmc_ctx* ctx, const uint32_t* keep_bits, int
   return rc;
 }
 
-extern "C" int kcmc_consensus_merge_device(kcmc_ctx* ctx, const int64_t* votes_dev, int world, int n_tpl,
-                                           int n_kp_global, int n_min, int32_t* out_consensus_dev,
-                                           int32_t* out_votes_dev, int32_t* out_meta_dev, int32_t* out_pack_dev,
-                                           kcmc_stream_t stream) {
-  if (!ctx) return fail(KCMC_EINVAL, "kcmc_consensus_merge_device: ctx is NULL");
-  if (world < 1 || n_tpl < 1 || n_kp_global < 1 || n_min < 0)
-    return fail(KCMC_EINVAL, "kcmc_consensus_merge_device: bad sizes");
-  if (n_tpl > kMergeMaxTpl || n_kp_global > kMergeMaxCons)
-    return fail(KCMC_EUNSUPPORTED, "kcmc_consensus_merge_device: n_tpl <= 4096 and n_kp_global <= 1024 "
-                                   "(kcmc_consensus_merge on the host otherwise)");
-  if (!votes_dev || !out_consensus_dev || !out_votes_dev || !out_meta_dev || !out_pack_dev)
-    return fail(KCMC_EINVAL, "kcmc_consensus_merge_device: NULL pointer");
-  const size_t lds = merge_lds_bytes(n_tpl, n_kp_global);
-  hipLaunchKernelGGL(consensus_merge_kernel, dim3(1), dim3(kMergeThreads), lds, (hipStream_t)stream,
-                     reinterpret_cast<const long long*>(votes_dev), world, n_tpl, n_kp_global, n_min, out_consensus_dev,
-                     out_votes_dev, out_meta_dev, out_pack_dev);
-  return launch_check("consensus_merge_kernel");
-}
-
 extern "C" long long kcmc_consensus_lookup_scratch_bytes(int n_frames, int nc) {
   if (n_frames < 0 || nc < 0) return -1;
   return (long long)n_frames * (long long)lookup_scratch_words(pyset_table_size((uint32_t)nc)) *
@@ -635,10 +482,9 @@ extern "C" long long kcmc_consensus_lookup_scratch_bytes(int n_frames, int nc) {
 
 namespace kcmc {
 namespace {
-// the lookup with the consensus size nc (host) or at nc_dev (device, <= nc), the bitmask at
-// cons_pack + bits_off
-int launch_lookup(const uint32_t* keep_bits, int n_frames, int n_tpl, const int32_t* cons_pack, int bits_off, int nc,
-                  const int32_t* nc_dev, int32_t* out_pt_off, int32_t* out_pt_idx, void* scratch, hipStream_t s) {
+// the lookup with the consensus size nc, the bitmask at cons_pack + nc
+int launch_lookup(const uint32_t* keep_bits, int n_frames, int n_tpl, const int32_t* cons_pack, int nc,
+                  int32_t* out_pt_off, int32_t* out_pt_idx, void* scratch, hipStream_t s) {
   if (n_frames == 0) return hip_check(hipMemsetAsync(out_pt_off, 0, sizeof(int32_t), s), "hipMemsetAsync(pt_off)");
   if (nc == 0 || n_tpl == 0)
     return hip_check(hipMemsetAsync(out_pt_off, 0, (size_t)(n_frames + 1) * sizeof(int32_t), s),
@@ -647,7 +493,7 @@ int launch_lookup(const uint32_t* keep_bits, int n_frames, int n_tpl, const int3
   if (!keep_bits || !cons_pack || !out_pt_idx || (!scratch && lookup_scratch_words(cap) > 0))
     return fail(KCMC_EINVAL, "kcmc_consensus_lookup: NULL pointer");
   const int W = (n_tpl + 31) / 32;
-  const uint32_t* cons_bits = reinterpret_cast<const uint32_t*>(cons_pack + bits_off);
+  const uint32_t* cons_bits = reinterpret_cast<const uint32_t*>(cons_pack + nc);
   hipLaunchKernelGGL(lookup_count_kernel, dim3(ceil_div(n_frames, kCountThreads)), dim3(kCountThreads), 0, s, keep_bits,
                      n_frames, W, cons_bits, out_pt_off);
   KCMC_TRY(launch_check("lookup_count_kernel"));
@@ -656,7 +502,7 @@ int launch_lookup(const uint32_t* keep_bits, int n_frames, int n_tpl, const int3
   const int r_lds = cap <= kOrderLdsCap, s_lds = cap <= kOrderLdsCap / 2;
   const size_t lds = ((size_t)2 * W + nc + (r_lds ? 2 * cap : 0) + (s_lds ? 2 * cap : 0)) * sizeof(int32_t);
   hipLaunchKernelGGL(lookup_order_kernel, dim3(n_frames), dim3(64), lds, s, keep_bits, n_frames, W, cons_pack, nc,
-                     nc_dev, cons_bits, out_pt_off, out_pt_idx, reinterpret_cast<int32_t*>(scratch), cap, r_lds, s_lds);
+                     cons_bits, out_pt_off, out_pt_idx, reinterpret_cast<int32_t*>(scratch), cap, r_lds, s_lds);
   return launch_check("lookup_order_kernel");
 }
 }  // namespace
@@ -668,20 +514,7 @@ extern "C" int kcmc_consensus_lookup(kcmc_ctx* ctx, const uint32_t* keep_bits, i
   if (!ctx) return fail(KCMC_EINVAL, "kcmc_consensus_lookup: ctx is NULL");
   if (n_frames < 0 || n_tpl < 0 || nc < 0 || nc > n_tpl) return fail(KCMC_EINVAL, "kcmc_consensus_lookup: bad sizes");
   if (!out_pt_off) return fail(KCMC_EINVAL, "kcmc_consensus_lookup: NULL pointer");
-  return launch_lookup(keep_bits, n_frames, n_tpl, cons_pack, nc, nc, nullptr, out_pt_off, out_pt_idx, scratch,
-                       (hipStream_t)stream);
-}
-
-extern "C" int kcmc_consensus_lookup_device(kcmc_ctx* ctx, const uint32_t* keep_bits, int n_frames, int n_tpl,
-                                            const int32_t* cons_pack_dev, int n_kp_global, const int32_t* meta_dev,
-                                            int32_t* out_pt_off, int32_t* out_pt_idx, void* scratch,
-                                            kcmc_stream_t stream) {
-  if (!ctx) return fail(KCMC_EINVAL, "kcmc_consensus_lookup_device: ctx is NULL");
-  if (n_frames < 0 || n_tpl < 0 || n_kp_global < 1)
-    return fail(KCMC_EINVAL, "kcmc_consensus_lookup_device: bad sizes");
-  if (!out_pt_off || !meta_dev) return fail(KCMC_EINVAL, "kcmc_consensus_lookup_device: NULL pointer");
-  return launch_lookup(keep_bits, n_frames, n_tpl, cons_pack_dev, n_kp_global, std::min(n_kp_global, n_tpl), meta_dev,
-                       out_pt_off, out_pt_idx, scratch, (hipStream_t)stream);
+  return launch_lookup(keep_bits, n_frames, n_tpl, cons_pack, nc, out_pt_off, out_pt_idx, scratch, (hipStream_t)stream);
 }
 
 extern "C" int kcmc_params_boundary(kcmc_ctx* ctx, const double* params, int n_frames, int E, double* out,

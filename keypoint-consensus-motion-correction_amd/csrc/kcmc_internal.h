@@ -37,9 +37,6 @@ struct kcmc_ctx {
   int hyp_off_len = 0;
   int hyp_trials = 0;
   uint32_t hyp_seed = 0;
-  // RANSAC scoring launches: at most this many workgroups, each walking frames g, g + grid,
-  // ... (0: one workgroup per frame).  kcmc_set_ransac_grid.
-  int ransac_grid = 0;
   // Stream-ordered scratch (per-call workspaces, e.g. the warp's tile plans): a private
   // memory pool that keeps its pages between calls.
   hipMemPool_t ws_pool = nullptr;

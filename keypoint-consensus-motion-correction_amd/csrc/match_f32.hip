@@ -838,8 +838,7 @@ int check_f32_args(const void* des_tpl, int n_tpl, int D, const void* des_q, con
 
 // Layout of the two work areas of a float match.  The prepared part (template stats,
 // the frames' max |b|^2 / max beta / bad flags, then the tile images: tpf = ceil(max_nq /
-// 64) per frame; the CSR total is a device value) can be filled ahead of the match on
-// another stream (kcmc_match_f32_prepare); the run part holds the per-frame fallback
+// 64) per frame; the CSR total is a device value); the run part holds the per-frame fallback
 // counters, the listed frames (count + ids) and lists (room for every template row) and
 // the fallback merge keys (set by the matcher when it lists a row).
 struct F32Layout {
@@ -921,23 +920,18 @@ int f32_layout_check(const F32Layout& L) {
   return KCMC_OK;
 }
 
-// prep: a prepared part (kcmc_match_f32_prepare) or nullptr (prepared here, in the same
-// stream-ordered workspace as the run part).
+// Both parts in one stream-ordered workspace.
 int launch_knn_f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const float* des_q, const int32_t* q_off,
-                   int n_frames, int max_nq, const void* prep, int32_t* out_idx, float* out_dist, hipStream_t s) {
+                   int n_frames, int max_nq, int32_t* out_idx, float* out_dist, hipStream_t s) {
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
   const F32Layout L = f32_layout(n_tpl, n_frames, max_nq);
   KCMC_TRY(f32_layout_check(L));
-  const size_t own = prep ? 0 : L.prep_bytes();
+  const size_t own = L.prep_bytes();
   void* ws = nullptr;
   KCMC_TRY(workspace_alloc(ctx, &ws, own + L.run_bytes(), s));
   char* w = static_cast<char*>(ws);
-  int rc = KCMC_OK;
-  if (!prep) {
-    rc = launch_f32_prepare(L, des_tpl, n_tpl, D, des_q, q_off, n_frames, w, s);
-    prep = w;
-  }
-  if (rc == KCMC_OK) rc = launch_f32_run(L, des_tpl, n_tpl, D, des_q, q_off, n_frames, prep, w + own, out_idx, out_dist, s);
+  int rc = launch_f32_prepare(L, des_tpl, n_tpl, D, des_q, q_off, n_frames, w, s);
+  if (rc == KCMC_OK) rc = launch_f32_run(L, des_tpl, n_tpl, D, des_q, q_off, n_frames, w, w + own, out_idx, out_dist, s);
   const int rf = workspace_free(ctx, ws, s);
   return rc != KCMC_OK ? rc : rf;
 }
@@ -952,28 +946,7 @@ extern "C" int kcmc_knn2_l2f32(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, i
                                kcmc_stream_t stream) {
   if (!ctx) return fail(KCMC_EINVAL, "kcmc_knn2_l2f32: ctx is NULL");
   KCMC_TRY(check_f32_args(des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, out_idx, out_dist));
-  return launch_knn_f32(ctx, des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, nullptr, out_idx, out_dist,
-                        (hipStream_t)stream);
-}
-
-extern "C" long long kcmc_match_f32_prep_bytes(int n_tpl, int n_frames, int max_nq) {
-  if (n_tpl < 0 || n_frames < 0 || max_nq < 0) return -1;
-  return (long long)f32_layout(n_tpl, n_frames, max_nq).prep_bytes();
-}
-
-extern "C" int kcmc_match_f32_prepare(kcmc_ctx* ctx, const float* des_tpl, int n_tpl, int D, const float* des_q,
-                                      const int32_t* q_off, int n_frames, int max_nq, void* prep_dev,
-                                      long long prep_bytes, kcmc_stream_t stream) {
-  if (!ctx) return fail(KCMC_EINVAL, "kcmc_match_f32_prepare: ctx is NULL");
-  int32_t dummy_i = 0;
-  float dummy_f = 0.f;
-  KCMC_TRY(check_f32_args(des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, &dummy_i, &dummy_f));
-  if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
-  const F32Layout L = f32_layout(n_tpl, n_frames, max_nq);
-  KCMC_TRY(f32_layout_check(L));
-  if (!prep_dev || prep_bytes < (long long)L.prep_bytes())
-    return fail(KCMC_EINVAL, "kcmc_match_f32_prepare: prep_dev must hold kcmc_match_f32_prep_bytes bytes");
-  return launch_f32_prepare(L, des_tpl, n_tpl, D, des_q, q_off, n_frames, prep_dev, (hipStream_t)stream);
+  return launch_knn_f32(ctx, des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, out_idx, out_dist, (hipStream_t)stream);
 }
 
 extern "C" int kcmc_match_frames_f32(kcmc_ctx* ctx, const float* des_tpl, const double* kp_tpl, int n_tpl, int D,
@@ -988,26 +961,7 @@ extern "C" int kcmc_match_frames_f32(kcmc_ctx* ctx, const float* des_tpl, const 
   if (n_tpl > 8192) return fail(KCMC_EUNSUPPORTED, "kcmc_match_frames_f32: n_tpl > 8192");
   if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
   hipStream_t s = (hipStream_t)stream;
-  KCMC_TRY(launch_knn_f32(ctx, des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, nullptr, out_idx, out_dist, s));
-  return launch_match_filter(out_idx, out_dist, kp_tpl, kp_q, q_off, n_frames, n_tpl, ratio, d_lo, d_hi,
-                             out_kp_ordered, out_keep_bits, out_counts, s);
-}
-
-extern "C" int kcmc_match_frames_f32_prepared(kcmc_ctx* ctx, const float* des_tpl, const double* kp_tpl, int n_tpl,
-                                              int D, const float* des_q, const double* kp_q, const int32_t* q_off,
-                                              int n_frames, int max_nq, const void* prep_dev, double ratio,
-                                              double d_lo, double d_hi, int32_t* out_idx, float* out_dist,
-                                              double* out_kp_ordered, uint32_t* out_keep_bits, int32_t* out_counts,
-                                              kcmc_stream_t stream) {
-  if (!ctx) return fail(KCMC_EINVAL, "kcmc_match_frames_f32_prepared: ctx is NULL");
-  KCMC_TRY(check_f32_args(des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, out_idx, out_dist));
-  if (n_frames > 0 && n_tpl > 0 && (!kp_tpl || !out_kp_ordered || !out_keep_bits || !out_counts || !prep_dev ||
-                                    (max_nq > 0 && !kp_q)))
-    return fail(KCMC_EINVAL, "kcmc_match_frames_f32_prepared: NULL pointer");
-  if (n_tpl > 8192) return fail(KCMC_EUNSUPPORTED, "kcmc_match_frames_f32_prepared: n_tpl > 8192");
-  if (n_frames == 0 || n_tpl == 0) return KCMC_OK;
-  hipStream_t s = (hipStream_t)stream;
-  KCMC_TRY(launch_knn_f32(ctx, des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, prep_dev, out_idx, out_dist, s));
+  KCMC_TRY(launch_knn_f32(ctx, des_tpl, n_tpl, D, des_q, q_off, n_frames, max_nq, out_idx, out_dist, s));
   return launch_match_filter(out_idx, out_dist, kp_tpl, kp_q, q_off, n_frames, n_tpl, ratio, d_lo, d_hi,
                              out_kp_ordered, out_keep_bits, out_counts, s);
 }

@@ -422,9 +422,8 @@ __device__ __forceinline__ void ransac_rigid_frame(
   (void)nin_local;
 }
 
-// Workgroup g scores frames g, g + grid, ...: one workgroup per frame by default; a
-// narrower grid (kcmc_set_ransac_grid) keeps RANSAC on a few CU slots when it runs beside
-// the warp (OverlappedSlabs corun).
+// Workgroup g scores frames g, g + grid, ... (the product launches one workgroup per frame;
+// narrower grids measured slower beside the warp).
 template <bool LARGE>
 __global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
     int n_frames, const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
@@ -487,13 +486,5 @@ extern "C" int kcmc_ransac_rigid(kcmc_ctx* ctx, const double* src, const double*
                                  const int32_t* pt_off, int src_frame_stride, int n_frames, int max_n, int trials,
                                  double thresh, double rate, int n_skip, double* out_params, uint8_t* out_inliers,
                                  int32_t* out_n_inliers, int32_t* out_best_trial, kcmc_stream_t stream) {
-  return ransac_rigid_impl(ctx, src, dst, pt_idx, pt_off, src_frame_stride, n_frames, max_n, trials, thresh, rate, n_skip, out_params, out_inliers, out_n_inliers, out_best_trial, ctx ? ctx->ransac_grid : 0, stream);
-}
-
-extern "C" int kcmc_ransac_rigid_grid(kcmc_ctx* ctx, const double* src, const double* dst, const int32_t* pt_idx,
-                                 const int32_t* pt_off, int src_frame_stride, int n_frames, int max_n, int trials,
-                                 double thresh, double rate, int n_skip, double* out_params, uint8_t* out_inliers,
-                                 int32_t* out_n_inliers, int32_t* out_best_trial, int max_workgroups, kcmc_stream_t stream) {
-  if (max_workgroups < 0) return fail(KCMC_EINVAL, "kcmc_ransac_rigid_grid: max_workgroups < 0");
-  return ransac_rigid_impl(ctx, src, dst, pt_idx, pt_off, src_frame_stride, n_frames, max_n, trials, thresh, rate, n_skip, out_params, out_inliers, out_n_inliers, out_best_trial, max_workgroups, stream);
+  return ransac_rigid_impl(ctx, src, dst, pt_idx, pt_off, src_frame_stride, n_frames, max_n, trials, thresh, rate, n_skip, out_params, out_inliers, out_n_inliers, out_best_trial, 0, stream);
 }

@@ -1507,35 +1507,3 @@ extern "C" int kcmc_warp_affine_u16(kcmc_ctx* ctx, const uint16_t* src, uint16_t
   KCMC_TRY(workspace_free(ctx, ws, s, wsb));
   return rc;
 }
-
-extern "C" long long kcmc_warp_plan_bytes(int n_frames, int H, int W, int C, int perspective) {
-  if (check_warp_args("kcmc_warp_plan_bytes", n_frames, H, W, C) != KCMC_OK) return -1;
-  return (long long)plan_bytes(n_frames, H, W, C, perspective != 0);
-}
-
-extern "C" int kcmc_warp_u16_plan(kcmc_ctx* ctx, const double* M, int n_frames, int H, int W, int C, int perspective,
-                                  int inverse_map, void* plan, long long plan_size, kcmc_stream_t stream) {
-  if (!ctx) return fail(KCMC_EINVAL, "kcmc_warp_u16_plan: ctx is NULL");
-  KCMC_TRY(check_warp_args("kcmc_warp_u16_plan", n_frames, H, W, C));
-  if (n_frames == 0 || H == 0 || W == 0) return KCMC_OK;
-  if (!M || !plan) return fail(KCMC_EINVAL, "kcmc_warp_u16_plan: NULL pointer");
-  if (plan_size < (long long)plan_bytes(n_frames, H, W, C, perspective != 0))
-    return fail(KCMC_EINVAL, "kcmc_warp_u16_plan: plan buffer smaller than kcmc_warp_plan_bytes");
-  if (((uintptr_t)plan & 15) != 0) return fail(KCMC_EINVAL, "kcmc_warp_u16_plan: plan must be 16-byte aligned");
-  launch_part(false, perspective != 0, nullptr, nullptr, M, n_frames, H, W, C, inverse_map, plan,
-              (hipStream_t)stream);
-  return launch_check("warp_plan_kernel");
-}
-
-extern "C" int kcmc_warp_u16_planned(kcmc_ctx* ctx, const uint16_t* src, uint16_t* dst, const void* plan, int n_frames,
-                                     int H, int W, int C, int perspective, kcmc_stream_t stream) {
-  if (!ctx) return fail(KCMC_EINVAL, "kcmc_warp_u16_planned: ctx is NULL");
-  KCMC_TRY(check_warp_args("kcmc_warp_u16_planned", n_frames, H, W, C));
-  if (n_frames == 0 || H == 0 || W == 0) return KCMC_OK;
-  if (!src || !dst || !plan) return fail(KCMC_EINVAL, "kcmc_warp_u16_planned: NULL pointer");
-  if (src == dst) return fail(KCMC_EINVAL, "kcmc_warp_u16_planned: in-place warp is not supported");
-  if (((uintptr_t)plan & 15) != 0) return fail(KCMC_EINVAL, "kcmc_warp_u16_planned: plan must be 16-byte aligned");
-  launch_part(true, perspective != 0, src, dst, nullptr, n_frames, H, W, C, 0, const_cast<void*>(plan),
-              (hipStream_t)stream);
-  return launch_check(perspective ? "warp_perspective_u16_kernel" : "warp_affine_u16_kernel");
-}

@@ -99,12 +99,10 @@ def _nomark(name, ev=None):
     return None
 
 
-def match_stage(inp: SlabInputs, cfg: AlignConfig, stream: Optional[int] = None,
-                prep: Optional[torch.Tensor] = None) -> stages.MatchResult:
-    """VA:194-214 for the slab; ``prep``: the float match's first part (stages.match_f32_prepare)."""
+def match_stage(inp: SlabInputs, cfg: AlignConfig, stream: Optional[int] = None) -> stages.MatchResult:
+    """VA:194-214 for the slab."""
     return stages.match_frames(inp.des_tpl, inp.kp_tpl, inp.des_q, inp.kp_q, inp.q_off, inp.q_off_host,
-                               ratio=cfg.ratio, d_lo=cfg.d_lo, d_hi=cfg.d_hi, norm=cfg.match_norm, stream=stream,
-                               prep=prep)
+                               ratio=cfg.ratio, d_lo=cfg.d_lo, d_hi=cfg.d_hi, norm=cfg.match_norm, stream=stream)
 
 
 def _log_rates(logger: Optional[logging.Logger], votes: np.ndarray, n_frames: int) -> None:
@@ -205,8 +203,7 @@ def _check_point_counts(cons: stages.Consensus, cfg: AlignConfig) -> None:
 
 def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.Consensus,
                  cfg: AlignConfig, lists_dev: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                 stream: Optional[int] = None, max_workgroups: int = 0,
-                 max_n: Optional[int] = None) -> stages.RansacResult:
+                 stream: Optional[int] = None, max_n: Optional[int] = None) -> stages.RansacResult:
     """VA:137-142: RANSAC of every frame's consensus points (src = the frame's matched
     keypoints, dst = template keypoints).  params [F, 2, 3] for the euclidean and
     affine models (model.params[:2], like VA:319), [F, 3, 3] for the projective one.
@@ -227,7 +224,7 @@ def ransac_stage(match: stages.MatchResult, kp_tpl: torch.Tensor, cons: stages.C
                                  max_n=max_n if max_n is not None else max(len(cons.order), 1),
                                  trials=cfg.ransac_trials,
                                  residual_threshold=cfg.ransac_threshold, spatial_rate=cfg.spatial_rate,
-                                 n_skip=cfg.effective_frame_skip, stream=stream, max_workgroups=max_workgroups)
+                                 n_skip=cfg.effective_frame_skip, stream=stream)
     else:
         pt_off, pt_idx = lists_dev if lists_dev is not None else consensus_to_device(cons, dev)
         if cfg.ransac_model == "euclidean":

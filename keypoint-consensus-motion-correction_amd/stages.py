@@ -84,27 +84,6 @@ def _ctx(device: torch.device) -> _lib.Context:
     return _lib.context(device.index if device.index is not None else torch.cuda.current_device())
 
 
-_CU_SPLIT_STREAMS = {}
-
-
-def cu_split_stream(device, cus_per_se: int, complement: bool = False) -> torch.cuda.ExternalStream:
-    """A stream whose kernels run on the first ``cus_per_se`` CUs of every shader engine
-    (``complement``: on the other CUs), as a torch ExternalStream (C ABI
-    kcmc_stream_create_cu_split).  One per (device, split, half), created on first use and
-    kept for the life of the process (in-flight work may still reference it)."""
-    dev = torch.device(device)
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    key = (idx, int(cus_per_se), bool(complement))
-    st = _CU_SPLIT_STREAMS.get(key)
-    if st is None:
-        h = _P()
-        _lib.check(_lib.load().kcmc_stream_create_cu_split(idx, int(cus_per_se), int(bool(complement)),
-                                                          ctypes.byref(h)))
-        st = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
-        _CU_SPLIT_STREAMS[key] = st
-    return st
-
-
 # ----------------------------------------------------------------------- K1
 @dataclass
 class MatchResult:
@@ -172,28 +151,15 @@ def match_frames(
     d_hi: float = 2.0,
     norm: str = "l2",
     stream: Optional[int] = None,
-    prep: Optional[torch.Tensor] = None,
 ) -> MatchResult:
     """VA:194-214 for every frame: knn k=2 + reorder + ratio + median filters.
     uint8 descriptors (the reference's) or float32 (SIFT-style extension; its distance is
     this build's fp64-accumulated L2, not OpenCV's float accumulation, so near-tie order
     against cv2 is unpinned -- see knn2_l2u8); ``norm`` "hamming" (uint8 only) is the
-    opt-in NORM_HAMMING matcher for binary descriptors.  ``prep`` (float32 only): the
-    output of match_f32_prepare for these descriptors, ordered before this call's stream."""
+    opt-in NORM_HAMMING matcher for binary descriptors."""
     dev, f32, n_tpl, D, F, max_nq = _match_args(des_tpl, kp_tpl, des_q, kp_q, q_off, q_off_host, norm)
     res = _match_result(dev, F, n_tpl)
     L = _lib.load()
-    if prep is not None:
-        if not f32:
-            raise TypeError("prep: the prepared match is the float32 matcher's")
-        _require(prep, "prep", torch.uint8, dev, 1)
-        if prep.numel() < L.kcmc_match_f32_prep_bytes(n_tpl, F, max_nq):
-            raise ValueError("prep is smaller than kcmc_match_f32_prep_bytes")
-        _lib.check(L.kcmc_match_frames_f32_prepared(
-            _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F, max_nq,
-            _ptr(prep), float(ratio), float(d_lo), float(d_hi), _ptr(res.idx), _ptr(res.dist), _ptr(res.kp_ordered),
-            _ptr(res.keep_bits), _ptr(res.counts), _stream(dev, stream)))
-        return res
     fn = L.kcmc_match_frames_f32 if f32 else (L.kcmc_match_frames_hamming if norm == "hamming" else L.kcmc_match_frames)
     _lib.check(fn(
         _ctx(dev).handle, _ptr(des_tpl), _ptr(kp_tpl), n_tpl, D, _ptr(des_q), _ptr(kp_q), _ptr(q_off), F,
@@ -244,8 +210,9 @@ def knn_frames(des_tpl: torch.Tensor, kp_tpl: torch.Tensor, des_q: torch.Tensor,
     ``stream``, idx / dist [F, n_tpl, 2]; filter_matches finishes it (on another stream
     ordered after this one, if wanted).  Same checks and results as match_frames."""
     dev, f32, n_tpl, D, F, max_nq = _match_args(des_tpl, kp_tpl, des_q, kp_q, q_off, q_off_host, norm)
-    idx = torch.empty((F, n_tpl, 2), dtype=torch.int32, device=dev)
-    dist = torch.empty((F, n_tpl, 2), dtype=torch.float32, device=dev)
+    with on_stream(dev, stream):  # the outputs belong to the stream that writes them
+        idx = torch.empty((F, n_tpl, 2), dtype=torch.int32, device=dev)
+        dist = torch.empty((F, n_tpl, 2), dtype=torch.float32, device=dev)
     L = _lib.load()
     fn = L.kcmc_knn2_l2f32 if f32 else (L.kcmc_knn2_hamming if norm == "hamming" else L.kcmc_knn2_l2u8)
     _lib.check(fn(_ctx(dev).handle, _ptr(des_tpl), n_tpl, D, _ptr(des_q), _ptr(q_off), F, max_nq, _ptr(idx), _ptr(dist),
@@ -270,35 +237,14 @@ def filter_matches(knn: Tuple[torch.Tensor, torch.Tensor], kp_tpl: torch.Tensor,
         raise ValueError("knn results / keypoints shapes disagree")
     with on_stream(dev, stream):
         res = _match_result(dev, F, n_tpl, knn)
+        if stream is not None:  # the knn tensors are read on this stream too
+            cur = torch.cuda.current_stream(dev)
+            idx.record_stream(cur)
+            dist.record_stream(cur)
     _lib.check(_lib.load().kcmc_match_filter(
         _ctx(dev).handle, _ptr(idx), _ptr(dist), _ptr(kp_tpl), _ptr(kp_q), _ptr(q_off), F, n_tpl, float(ratio),
         float(d_lo), float(d_hi), _ptr(res.kp_ordered), _ptr(res.keep_bits), _ptr(res.counts), _stream(dev, stream)))
     return res
-
-
-def match_f32_prepare(des_tpl: torch.Tensor, des_q: torch.Tensor, q_off: torch.Tensor, q_off_host: np.ndarray,
-                      stream: Optional[int] = None) -> torch.Tensor:
-    """The first part of the float32 match (template statistics, the frames' fp16 tile
-    images; kcmc_match_f32_prepare) into a fresh uint8 device buffer, on ``stream``; pass it
-    to match_frames(prep=...) on a stream ordered after this one."""
-    dev = _device_of(des_tpl)
-    _require(des_tpl, "des_tpl", torch.float32, dev, 2)
-    _require(des_q, "des_q", torch.float32, dev, 2)
-    _require(q_off, "q_off", torch.int32, dev, 1)
-    n_tpl, D = des_tpl.shape
-    F = q_off.numel() - 1
-    q_off_host = np.asarray(q_off_host)
-    _check_offsets(q_off_host, F)
-    max_nq = int(np.diff(q_off_host).max()) if F else 0
-    L = _lib.load()
-    nbytes = int(L.kcmc_match_f32_prep_bytes(n_tpl, F, max_nq))
-    if nbytes < 0:
-        raise ValueError("bad sizes")
-    with on_stream(dev, stream):  # the buffer belongs to the stream that fills it
-        prep = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
-    _lib.check(L.kcmc_match_f32_prepare(_ctx(dev).handle, _ptr(des_tpl), n_tpl, D, _ptr(des_q), _ptr(q_off), F, max_nq,
-                                        _ptr(prep), nbytes, _stream(dev, stream)))
-    return prep
 
 
 # ------------------------------------------------------------------ consensus
@@ -426,82 +372,6 @@ def consensus_merge(votes: np.ndarray, n_tpl: int, n_kp_global: int, n_min: int,
     return ConsensusChoice(order[:n].copy(), counts[:n].copy(), pack_out)
 
 
-@dataclass
-class DeviceChoice:
-    """kcmc_consensus_merge_device's outputs, on the device: the first meta[0] entries of
-    ``cons`` / ``votes`` are Counter.most_common(n_kp_global) (VA:240); meta[1] is 0, 1
-    (fewer than N_KP_GLOBAL_MIN voted: AlignmentError) or 2 (invalid votes); ``pack`` =
-    set(consensus) iteration order, then the consensus bitmask from n_kp_global on."""
-    cons: torch.Tensor
-    votes: torch.Tensor
-    meta: torch.Tensor
-    pack: torch.Tensor
-    n_kp_global: int
-
-
-def merge_device_supported(n_tpl: int, n_kp_global: int) -> bool:
-    return 1 <= n_tpl <= 4096 and 1 <= n_kp_global <= 1024
-
-
-def consensus_merge_device(votes: torch.Tensor, n_tpl: int, n_kp_global: int, n_min: int,
-                           stream: Optional[int] = None) -> DeviceChoice:
-    """consensus_merge on the device (no host round trip): votes [world, 2, n_tpl] or
-    [2, n_tpl] i64 device tensor.  The caller checks meta (check_device_choice) before it
-    uses the consensus on the host."""
-    dev = _device_of(votes)
-    _require(votes, "votes", torch.int64, dev)
-    world = votes.numel() // (2 * n_tpl) if n_tpl else 1
-    if not n_tpl or votes.numel() != world * 2 * n_tpl:
-        raise ValueError("votes must be [world, 2, n_tpl]")
-    words = (n_tpl + 31) // 32
-    ch = DeviceChoice(cons=torch.empty(n_kp_global, dtype=torch.int32, device=dev),
-                      votes=torch.empty(n_kp_global, dtype=torch.int32, device=dev),
-                      meta=torch.empty(2, dtype=torch.int32, device=dev),
-                      pack=torch.empty(n_kp_global + words, dtype=torch.int32, device=dev), n_kp_global=n_kp_global)
-    _lib.check(_lib.load().kcmc_consensus_merge_device(
-        _ctx(dev).handle, _ptr(votes), int(world), int(n_tpl), int(n_kp_global), int(n_min), _ptr(ch.cons),
-        _ptr(ch.votes), _ptr(ch.meta), _ptr(ch.pack), _stream(dev, stream)))
-    return ch
-
-
-ALIGNMENT_ERROR_TEXT = ("Too few keypoints found. Try a higher quality video, or decrease "
-                        "`VideoAligner.N_KP_GLOBAL_MIN`")
-
-
-def check_device_choice(meta: np.ndarray) -> int:
-    """The host side of a device merge: raises like kcmc_consensus_merge (AlignmentError below
-    N_KP_GLOBAL_MIN, VA:241-244; ValueError for invalid votes); returns nc."""
-    if int(meta[1]) == 1:
-        from .video_aligner import AlignmentError
-
-        raise AlignmentError(ALIGNMENT_ERROR_TEXT)
-    if int(meta[1]) != 0:
-        raise ValueError("consensus merge: invalid votes (a negative count or a voted template without a "
-                         "first-occurrence key)")
-    return int(meta[0])
-
-
-def consensus_lookup_device(keep_bits: torch.Tensor, n_tpl: int, ch: DeviceChoice,
-                            stream: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """consensus_lookup on a device merge: the consensus size is read on the device;
-    pt_idx is sized for min(n_kp_global, n_tpl) points per frame."""
-    dev = _device_of(keep_bits)
-    _require(keep_bits, "keep_bits", torch.int32, dev, 2)
-    F = keep_bits.shape[0]
-    if keep_bits.shape[1] != (n_tpl + 31) // 32:
-        raise ValueError("consensus_lookup_device: inconsistent shapes")
-    L = _lib.load()
-    ncap = min(ch.n_kp_global, n_tpl)
-    pt_off = torch.empty(F + 1, dtype=torch.int32, device=dev)
-    pt_idx = torch.empty(max(F * ncap, 1), dtype=torch.int32, device=dev)
-    sb = int(L.kcmc_consensus_lookup_scratch_bytes(F, ncap))
-    scratch = torch.empty(sb, dtype=torch.uint8, device=dev) if sb > 0 else None
-    _lib.check(L.kcmc_consensus_lookup_device(_ctx(dev).handle, _ptr(keep_bits), F, int(n_tpl), _ptr(ch.pack),
-                                              int(ch.n_kp_global), _ptr(ch.meta), _ptr(pt_off), _ptr(pt_idx),
-                                              _ptr(scratch), _stream(dev, stream)))
-    return pt_off, pt_idx
-
-
 def consensus_lookup(keep_bits: torch.Tensor, n_tpl: int, pack_dev: torch.Tensor, nc: int,
                      stream: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """The lookup part of the consensus (VA:274) on the device: every frame's
@@ -565,26 +435,6 @@ class RansacResult:
     inliers: torch.Tensor      # [P] u8 inlier mask of the best hypothesis (CSR like the points)
     n_inliers: torch.Tensor    # [F] i32
     best_trial: torch.Tensor   # [F] i32 (-1: none)
-
-
-@contextlib.contextmanager
-def ransac_grid(device, max_workgroups: int):
-    """RANSAC scoring launches on ``device`` inside the block use at most
-    ``max_workgroups`` workgroups, each scoring frames g, g + max_workgroups, ... (C ABI
-    kcmc_set_ransac_grid; 0 = one per frame, the default).  Results are identical; a narrow
-    grid keeps RANSAC on a few CU slots when it shares the device with the warp.  The value
-    in force before the block is restored after it.  The pipelines pass their grid per call
-    (ransac_lists(max_workgroups=...)), which other callers of the context cannot change."""
-    ctx = _ctx(torch.device(device))
-    L = _lib.load()
-    prev = ctx.ransac_grid
-    _lib.check(L.kcmc_set_ransac_grid(ctx.handle, int(max_workgroups)))
-    ctx.ransac_grid = int(max_workgroups)
-    try:
-        yield
-    finally:
-        _lib.check(L.kcmc_set_ransac_grid(ctx.handle, prev))
-        ctx.ransac_grid = prev
 
 
 def ransac_rigid(
@@ -727,8 +577,7 @@ def ransac_prepare_range(device, model: str, n_lo: int, n_hi: int, trials: int =
 
 def ransac_lists(model: str, src: torch.Tensor, dst: torch.Tensor, pt_off: torch.Tensor, pt_idx: torch.Tensor,
                  src_frame_stride: int, max_n: int, trials: int = 1000, residual_threshold: float = 2.0,
-                 spatial_rate: float = 1.0, n_skip: int = 3, stream: Optional[int] = None,
-                 max_workgroups: int = 0) -> RansacResult:
+                 spatial_rate: float = 1.0, n_skip: int = 3, stream: Optional[int] = None) -> RansacResult:
     """RANSAC of every frame on device point lists whose sizes the host does not know
     (the device consensus lookup): max_n bounds every frame's point count (n_kp_global) and
     the tables of every count in [n_skip, max_n] must be ready (ransac_prepare_range).
@@ -749,15 +598,15 @@ def ransac_lists(model: str, src: torch.Tensor, dst: torch.Tensor, pt_off: torch
     ctx = _ctx(dev).handle
     st = _stream(dev, stream)
     if model == "euclidean":
-        _lib.check(L.kcmc_ransac_rigid_grid(
+        _lib.check(L.kcmc_ransac_rigid(
             ctx, _ptr(src), _ptr(dst), _ptr(pt_idx), _ptr(pt_off), int(src_frame_stride), F, int(max_n), int(trials),
             float(residual_threshold), float(spatial_rate), int(n_skip), _ptr(res.params), _ptr(res.inliers),
-            _ptr(res.n_inliers), _ptr(res.best_trial), int(max_workgroups), st))
+            _ptr(res.n_inliers), _ptr(res.best_trial), st))
     else:
-        _lib.check(L.kcmc_ransac_model_grid(
+        _lib.check(L.kcmc_ransac_model(
             ctx, _lib.MODEL_IDS[model], _ptr(src), _ptr(dst), _ptr(pt_idx), _ptr(pt_off), int(src_frame_stride), F,
             int(max_n), int(trials), float(residual_threshold), float(spatial_rate), int(n_skip), _ptr(res.params),
-            _ptr(res.inliers), _ptr(res.n_inliers), _ptr(res.best_trial), int(max_workgroups), st))
+            _ptr(res.inliers), _ptr(res.n_inliers), _ptr(res.best_trial), st))
     return res
 
 
@@ -824,55 +673,6 @@ def _warp_shape(frames_shape) -> Tuple[int, int, int, int]:
         raise ValueError("frames must be [F, H, W] or [F, H, W, C]")
     F, H, W = (int(v) for v in frames_shape[:3])
     return F, H, W, 1 if len(frames_shape) == 3 else int(frames_shape[3])
-
-
-def warp_plan(maps: torch.Tensor, frames_shape, inverse_map: bool = False, stream: Optional[int] = None) -> torch.Tensor:
-    """The first part of warp_affine_u16 / warp_perspective_u16 (kcmc_warp_u16_plan): the
-    map inversion and every tile's source box for frames of ``frames_shape``, into a fresh
-    device buffer allocated on (and filled by) ``stream``; hand it to warp_planned on a
-    stream ordered after this one.  maps [F, 2, 3] (warpAffine) or [F, 3, 3]
-    (warpPerspective) f64."""
-    dev = _device_of(maps)
-    _require(maps, "maps", torch.float64, dev, 3)
-    F, H, W, C = _warp_shape(frames_shape)
-    persp = tuple(maps.shape[1:]) == (3, 3)
-    if tuple(maps.shape) != (F, 3 if persp else 2, 3):
-        raise ValueError(f"maps must be [{F}, 2, 3] or [{F}, 3, 3], got {tuple(maps.shape)}")
-    L = _lib.load()
-    nbytes = int(L.kcmc_warp_plan_bytes(F, H, W, C, int(persp)))
-    if nbytes < 0:
-        _lib.check(L.kcmc_warp_u16_plan(_ctx(dev).handle, _ptr(maps), F, H, W, C, int(persp), 0, _P(0), 0,
-                                        _stream(dev, stream)))
-    with on_stream(dev, stream):  # the buffer belongs to the stream that fills it
-        plan = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=dev)
-    _lib.check(L.kcmc_warp_u16_plan(_ctx(dev).handle, _ptr(maps), F, H, W, C, int(persp), int(bool(inverse_map)),
-                                    _ptr(plan), plan.numel(), _stream(dev, stream)))
-    plan.kcmc_perspective = persp  # which warp the plan is for
-    return plan
-
-
-def warp_planned(frames: torch.Tensor, plan: torch.Tensor, out: Optional[torch.Tensor] = None,
-                 stream: Optional[int] = None) -> torch.Tensor:
-    """The second part (kcmc_warp_u16_planned): the tiles of a warp whose plan warp_plan
-    made for these frames; ``stream`` must be ordered after the plan's."""
-    dev = _device_of(frames)
-    _require(frames, "frames", torch.uint16, dev)
-    _require(plan, "plan", torch.uint8, dev, 1)
-    F, H, W, C = _warp_shape(frames.shape)
-    persp = getattr(plan, "kcmc_perspective", None)
-    if persp is None:  # the layout (affine or perspective) travels with the tensor warp_plan made
-        raise ValueError("plan must be the tensor warp_plan returned")
-    if plan.numel() < int(_lib.load().kcmc_warp_plan_bytes(F, H, W, C, int(persp))):
-        raise ValueError("plan was made for other frames")
-    if out is None:
-        out = torch.empty_like(frames)
-    else:
-        _require(out, "out", torch.uint16, dev)
-        if out.shape != frames.shape:
-            raise ValueError("out must have the shape of frames")
-    _lib.check(_lib.load().kcmc_warp_u16_planned(_ctx(dev).handle, _ptr(frames), _ptr(out), _ptr(plan), F, H, W, C,
-                                                 int(persp), _stream(dev, stream)))
-    return out
 
 
 # ------------------------------------------------------------ f2: normalisation

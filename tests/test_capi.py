@@ -65,27 +65,9 @@ def test_launch_entry_points_validate_before_touching_the_gpu():
     assert L.kcmc_consensus_vote(None, None, 1, 8, 0, None, None) == _lib.KCMC_EINVAL
     assert L.kcmc_consensus_lookup(None, None, 1, 8, None, 1, None, None, None, None) == _lib.KCMC_EINVAL
     assert L.kcmc_params_boundary(None, None, 1, 6, None, None) == _lib.KCMC_EINVAL
-    assert L.kcmc_ransac_rigid_grid(None, None, None, None, None, 0, 1, 10, 1000, 2.0, 1.0, 3, None, None, None, None,
-                                    0, None) == _lib.KCMC_EINVAL
     assert L.kcmc_consensus_merge(None, 0, 8, 1, 1, None, None, None, None) == _lib.KCMC_EINVAL
     assert L.kcmc_memcpy_async(None, None, 8, None) == _lib.KCMC_EINVAL
-    # round 5: the two-part warp and the filter-only entry
-    assert L.kcmc_warp_u16_plan(None, None, 1, 4, 4, 1, 0, 0, None, 0, None) == _lib.KCMC_EINVAL
-    assert L.kcmc_warp_u16_planned(None, None, None, None, 1, 4, 4, 1, 0, None) == _lib.KCMC_EINVAL
+    # the filter-only entry (knn results from elsewhere)
     assert L.kcmc_match_filter(None, None, None, None, None, None, 1, 8, 0.75, 0.5, 2.0, None, None, None,
                                None) == _lib.KCMC_EINVAL
     del P
-
-
-def test_workspace_size_queries_are_host_only():
-    """kcmc_warp_plan_bytes / kcmc_match_f32_prep_bytes: pure host functions (callable
-    without a GPU), -1 for bad sizes, monotone in the frame count, and the perspective plan
-    holds the affine one plus its inverted maps."""
-    L = _lib.load()
-    assert L.kcmc_warp_plan_bytes(-1, 4, 4, 1, 0) == -1
-    assert L.kcmc_warp_plan_bytes(1, 4, 4, 2, 0) == -1  # C must be 1, 3 or 4
-    a1, a2 = L.kcmc_warp_plan_bytes(1, 1080, 1920, 1, 0), L.kcmc_warp_plan_bytes(2, 1080, 1920, 1, 0)
-    assert 0 < a1 < a2
-    assert L.kcmc_warp_plan_bytes(2, 1080, 1920, 1, 1) > 0
-    assert L.kcmc_match_f32_prep_bytes(-1, 1, 1) == -1
-    assert 0 < L.kcmc_match_f32_prep_bytes(4096, 10, 4500) < L.kcmc_match_f32_prep_bytes(4096, 20, 4500)

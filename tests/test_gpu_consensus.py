@@ -116,62 +116,3 @@ def test_params_boundary(dev, shape):
             assert got[0] == ok[0] and got[1] == ok[-1]
             np.testing.assert_array_equal(got[2:2 + E], p[ok[0]].ravel())
             np.testing.assert_array_equal(got[2 + E:], p[ok[-1]].ravel())
-
-
-@pytest.mark.parametrize("F,n_tpl,density", CASES)
-@pytest.mark.parametrize("n_kp_global", [1, 50, 100, 500])
-def test_device_merge_and_lookup_equal_host(dev, F, n_tpl, density, n_kp_global):
-    """kcmc_consensus_merge_device (Counter.most_common + set(consensus) order, VA:240-248)
-    equals the host merge -- one rank and the sum / min of three ranks' votes, consensus
-    smaller than and capped by n_kp_global, ascending and replayed set orders -- and the
-    lookup that reads the consensus size on the device equals the host-sized lookup."""
-    rng = np.random.default_rng(F * 11 + n_tpl + n_kp_global)
-    kb = _random_bits(rng, F, n_tpl, density)
-    votes1 = stages.consensus_vote_host(kb, n_tpl, 0)
-    kb2, kb3 = _random_bits(rng, F, n_tpl, density), _random_bits(rng, F, n_tpl, density)
-    votes3 = np.stack([votes1, stages.consensus_vote_host(kb2, n_tpl, F), stages.consensus_vote_host(kb3, n_tpl, 2 * F)])
-    for v in (votes1, votes3):
-        try:
-            exp = stages.consensus_merge(v, n_tpl, n_kp_global, 1)
-        except BaseException as e:  # AlignmentError: nothing voted
-            assert type(e).__name__ == "AlignmentError"
-            ch = stages.consensus_merge_device(torch.from_numpy(v).to(dev), n_tpl, n_kp_global, 1)
-            meta = ch.meta.cpu().numpy()
-            assert meta[0] == 0 and meta[1] == 1
-            continue
-        ch = stages.consensus_merge_device(torch.from_numpy(v).to(dev), n_tpl, n_kp_global, 1)
-        meta = ch.meta.cpu().numpy()
-        nc = stages.check_device_choice(meta)
-        assert nc == exp.nc
-        np.testing.assert_array_equal(ch.cons.cpu().numpy()[:nc], exp.order)
-        np.testing.assert_array_equal(ch.votes.cpu().numpy()[:nc], exp.votes)
-        words = (n_tpl + 31) // 32
-        pack = ch.pack.cpu().numpy()
-        np.testing.assert_array_equal(pack[:nc], exp.pack[:nc])
-        np.testing.assert_array_equal(pack[n_kp_global:n_kp_global + words], exp.pack[nc:nc + words])
-        if v is votes1:
-            kb_dev = torch.from_numpy(kb.view(np.int32)).to(dev)
-            off_d, idx_d = stages.consensus_lookup_device(kb_dev, n_tpl, ch)
-            off_h, idx_h = stages.consensus_lookup_host(kb, n_tpl, exp.cons_iter)
-            off_d = off_d.cpu().numpy()
-            np.testing.assert_array_equal(off_d, off_h)
-            np.testing.assert_array_equal(idx_d.cpu().numpy()[:off_d[-1]], idx_h)
-
-
-def test_device_merge_flags_too_few_and_invalid_votes(dev):
-    n_tpl = 64
-    v = np.zeros((2, n_tpl), np.int64)
-    v[1] = np.iinfo(np.int64).max
-    v[0, 3], v[1, 3] = 5, (2 << 32) | 3
-    ch = stages.consensus_merge_device(torch.from_numpy(v).to(dev), n_tpl, 10, 2)
-    meta = ch.meta.cpu().numpy()
-    assert list(meta) == [1, 1]
-    with pytest.raises(BaseException, match="Too few keypoints"):
-        stages.check_device_choice(meta)
-    v[0, 7] = 2  # voted, but no first-occurrence key
-    meta = stages.consensus_merge_device(torch.from_numpy(v).to(dev), n_tpl, 10, 1).meta.cpu().numpy()
-    assert meta[1] == 2
-    with pytest.raises(ValueError):
-        stages.check_device_choice(meta)
-    with pytest.raises(Exception, match="n_tpl <= 4096"):
-        stages.consensus_merge_device(torch.from_numpy(np.zeros((2, 5000), np.int64)).to(dev), 5000, 10, 1)

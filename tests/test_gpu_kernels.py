@@ -534,65 +534,3 @@ def test_warp_multichannel_vector_staging(dev, shape):
     outp = stages.warp_perspective_u16(_t(imgs, dev), _t(Hs, dev)).cpu().numpy()
     for f in range(F):
         assert np.array_equal(outp[f], oracle.warp_perspective_u16(imgs[f], Hs[f])), f
-
-
-@pytest.mark.parametrize("persp", [False, True])
-@pytest.mark.parametrize("shape", [(3, 1080, 1920), (4, 512, 512), (2, 250, 520, 3), (2, 96, 136, 4), (1, 5, 7)])
-def test_warp_planned_equals_one_call_warp(dev, shape, persp):
-    """kcmc_warp_u16_plan on one stream, kcmc_warp_u16_planned on another ordered after it
-    (the pipeline's analysis / kernel streams): the one-call warp's pixels, on every tile
-    path (small rotations, zoom, a shift off the frame, a NaN map), forward and inverse
-    maps, and one plan used for two stacks of the same shape."""
-    F = shape[0]
-    rng = np.random.default_rng(sum(shape) + persp)
-    a = _t(rng.integers(0, 65536, shape).astype(np.uint16), dev)
-    b = _t(rng.integers(0, 16384, shape).astype(np.uint16), dev)
-    Ms = np.stack([synthetic.rigid(np.deg2rad(0.4), 3.7, -2.2), synthetic.rigid(np.deg2rad(-25.0), 40.0, 10.0),
-                   np.array([[1.6, 0.02, -30.0], [0.01, 1.6, -20.0]]), synthetic.rigid(0.0, 5000.0, 0.0)][:F])
-    if F > 1:
-        Ms[1, 1, 2] = np.nan
-    if persp:
-        Ms = np.concatenate([Ms, np.tile([[[0.0, 0.0, 1.0]]], (F, 1, 1))], axis=1)
-        Ms[:, 2, :2] = [2e-5, -1e-5]
-    one = stages.warp_perspective_u16 if persp else stages.warp_affine_u16
-    maps = _t(Ms, dev)
-    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    for inv in (False, True):
-        ref = [one(x, maps, inverse_map=inv) for x in (a, b)]
-        s1.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s1):
-            plan = stages.warp_plan(maps, shape, inverse_map=inv, stream=s1.cuda_stream)
-        s2.wait_stream(s1)
-        with torch.cuda.stream(s2):
-            got = [stages.warp_planned(x, plan, stream=s2.cuda_stream) for x in (a, b)]
-        torch.cuda.current_stream(dev).wait_stream(s2)
-        for g, r in zip(got, ref):
-            assert torch.equal(g, r), inv
-    with pytest.raises(ValueError):
-        stages.warp_planned(_t(np.zeros((F + 1,) + shape[1:], np.uint16), dev), plan)
-
-
-@pytest.mark.parametrize("grid", [1, 3, 64])
-def test_ransac_narrow_grid_matches_one_workgroup_per_frame(dev, grid):
-    """kcmc_set_ransac_grid: workgroups walking several frames each give exactly the
-    one-workgroup-per-frame results, rigid and extension models, N <= 128 and N > 128."""
-    rng = np.random.default_rng(41)
-    tpls, qs = [], []
-    for N in [2, 5, 40, 90, 127, 129, 300, 0, 60]:
-        tpl = rng.uniform(0, 1000, (N, 2))
-        A = synthetic.rigid(rng.normal(0, 0.02), rng.normal(0, 5), rng.normal(0, 5))
-        q = (tpl - A[:, 2]) @ A[:, :2] + rng.normal(0, 0.7, (N, 2))
-        tpls.append(tpl)
-        qs.append(q)
-    off = _csr(qs)
-    args = (_t(np.concatenate(qs).reshape(-1, 2), dev), _t(np.concatenate(tpls).reshape(-1, 2), dev), _t(off, dev), off)
-    runs = [lambda: stages.ransac_rigid(*args), lambda: stages.ransac_model(*args, model="affine"),
-            lambda: stages.ransac_model(*args, model="projective", n_skip=5)]
-    for run in runs:
-        ref = run()
-        with stages.ransac_grid(dev, grid):
-            got = run()
-        for a, b in [(ref.params, got.params), (ref.inliers, got.inliers), (ref.n_inliers, got.n_inliers),
-                     (ref.best_trial, got.best_trial)]:
-            assert torch.equal(a.nan_to_num(7.0) if a.is_floating_point() else a,
-                               b.nan_to_num(7.0) if b.is_floating_point() else b)

@@ -373,35 +373,6 @@ def test_knn2_f32_frame_beyond_fp16_range_goes_to_fallback(dev, n_q):
         assert np.array_equal(dist[f].view(np.int32), rd.view(np.int32)), f
 
 
-def test_match_frames_f32_prepared_equals_one_call(dev):
-    """kcmc_match_f32_prepare on a side stream + kcmc_match_frames_f32_prepared on another
-    (ordered by an event) = kcmc_match_frames_f32, bit for bit, including the near-tie rows
-    that go to the exact fallback; a short prep buffer and uint8 descriptors are refused."""
-    rng = np.random.default_rng(5)
-    ks = synthetic.make_keypoints(9, 300, 128, (270, 480), seed=16, descriptor="f32")
-    des_q = ks.des_q.copy()
-    a, b = ks.q_off[4], ks.q_off[5]
-    des_q[a:a + 20] = ks.des_tpl[rng.integers(0, 300, 20)]  # exact copies: ties for the fallback
-    args = (_t(ks.des_tpl, dev), _t(ks.kp_tpl, dev), _t(des_q, dev), _t(ks.kp_q, dev), _t(ks.q_off, dev), ks.q_off)
-    ref = stages.match_frames(*args)
-    side = torch.cuda.Stream(dev)
-    side.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(side):
-        prep = stages.match_f32_prepare(args[0], args[2], args[4], ks.q_off)
-    done = torch.cuda.Event()
-    done.record(side)
-    torch.cuda.current_stream(dev).wait_event(done)
-    got = stages.match_frames(*args, prep=prep)
-    for name in ("idx", "dist", "kp_ordered", "keep_bits", "counts"):
-        assert torch.equal(getattr(ref, name), getattr(got, name)), name
-    with pytest.raises(ValueError, match="prep is smaller"):
-        stages.match_frames(*args, prep=prep[:16])
-    ku = synthetic.make_keypoints(2, 64, 32, (96, 128), seed=1)
-    with pytest.raises(TypeError, match="prepared match"):
-        stages.match_frames(_t(ku.des_tpl, dev), _t(ku.kp_tpl, dev), _t(ku.des_q, dev), _t(ku.kp_q, dev),
-                            _t(ku.q_off, dev), ku.q_off, prep=prep)
-
-
 @pytest.mark.parametrize("kind", ["u8", "hamming", "f32", "u8_big"])
 def test_knn_then_filter_on_two_streams_equals_match_frames(dev, kind):
     """knn_frames on one stream + filter_matches on another ordered after it (the c5

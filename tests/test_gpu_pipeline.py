@@ -147,15 +147,6 @@ def test_overlapped_slabs_equal_align_slab(dev, beside):
     _check_overlapped(ov, slabs, ref)
 
 
-def test_cu_split_stream_arguments(dev):
-    from kcmc_amd import _lib
-    for bad in (0, 8, -1):
-        with pytest.raises(ValueError):
-            stages.cu_split_stream(dev, bad)
-    assert stages.cu_split_stream(dev, 2) is stages.cu_split_stream(dev, 2)
-    assert _lib.load().kcmc_stream_destroy(None) == 0
-
-
 def _check_overlapped(ov, slabs, ref):
     got = [ov.submit(s) for s in slabs]
     assert got[0] is None

@@ -44,7 +44,8 @@ def main():
             subprocess.run([sys.executable, patch, csrc], check=True)
         srcs = [s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))]
         flags = [f if not f.startswith("-I") else f"-I{os.path.join(tmp, 'include')}" for f in B.COMMON_FLAGS]
-        flags += os.environ.get("KCMC_AB_FLAGS", "").split()  # e.g. -DKCMC_FASTC_PITCH=192
+        flags += os.environ.get("KCMC_AB_FLAGS", "").split()  # debug macros only (e.g. -DKCMC_WARP_SENTINEL);
+        # the product has no A/B macros any more: variants are edits of the copy (KCMC_AB_PATCH)
         objs = []
         for s in srcs:
             o = os.path.join(tmp, s + ".o")
