@@ -450,6 +450,34 @@ def spawn_ranks(n: int, argv: list) -> int:
     return rc if rc >= 0 else 1
 
 
+FP32_PEAK_TFLOPS = 157.3  # dense fp32 vector (packed) (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6   # fp64 vector
+# Algorithmic flops of one (trial, point) residual test: the map (X, Y) = A (x, y) + t
+# (4 mul + 4 add), the residual (2 sub), q = ex^2 + ey^2 (2 mul + 1 add); the projective
+# map adds w (2 mul + 2 add) and two divisions (counted as 1 each).
+RANSAC_FLOPS_PER_TEST = {"euclidean": 13, "affine": 13, "projective": 19}
+
+
+def ransac_roofline(model: str, cons, cfg, ransac_ms: float) -> dict:
+    """The RANSAC stage against its VALU peak: every trial of every fitted frame tests all N
+    of the frame's points (phase A), at RANSAC_FLOPS_PER_TEST flops each, over the isolated
+    stage time.  The rigid scorer's phase A runs in fp32 (ransac_common.h score32; priced
+    against the fp32 vector peak), the affine / projective ones in fp64."""
+    n = np.diff(cons.pt_off)
+    fitted = n[n >= cfg.effective_frame_skip]
+    tests = float(fitted.sum()) * TRIALS
+    fl = RANSAC_FLOPS_PER_TEST[model]
+    achieved = tests * fl / (ransac_ms * 1e-3) / 1e12
+    peak = FP32_PEAK_TFLOPS if model == "euclidean" else FP64_PEAK_TFLOPS
+    return {"kernel": "ransac_rigid_kernel (fp32 phase A)" if model == "euclidean"
+            else f"ransac_model_score_kernel<{model}> (fp64 phase A) + refit",
+            "bound": "valu", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": None, "avg_launch_ms": ransac_ms,
+            "trial_point_tests": tests, "flops_per_test": fl,
+            "note": "achieved = trials x points x flops per residual test / isolated stage time (fit, "
+                    "selection, exact re-scoring of tied trials and the refit are overhead, not counted)"}
+
+
 def single_process(args, bc: BenchConfig) -> dict:
     """The drop-in VideoAligner's multi-GPU path (kcmc_amd.multidevice.align_split): one
     process, one contiguous frame slab per device of ``devices`` (a device may repeat), the
@@ -681,6 +709,7 @@ def main():
         # RANSAC kernel alone (isolated_stage_ms); the overlapped figure shares the CUs
         # with the previous step's warp
         "ransac_hypotheses_per_s_per_gpu": round(iso_ransac * TRIALS / (iso["ransac"] * 1e-3), 1),
+        "roofline_ransac": ransac_roofline(bc.model, iso_cons, cfg, iso["ransac"]),
         "ransac_hypotheses_per_s_per_gpu_overlapped": round(n_ransac * TRIALS / (ransac_ms * 1e-3), 1),
         "ransac_mean_points": round(float(n_pts.mean()), 2),
         "stage_ms": stage_ms,

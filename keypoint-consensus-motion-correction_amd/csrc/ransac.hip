@@ -129,7 +129,7 @@ __device__ __forceinline__ void ransac_rigid_frame(
     int T, double thresh, double tq, double rate, int n_skip, double* __restrict__ out_params,
     uint8_t* __restrict__ out_inl, int32_t* __restrict__ out_nin, int32_t* __restrict__ out_best) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ double red[kThreads / 64 * 4];
+  __shared__ double red[kThreads / 64 * 8];
   __shared__ int s_cnt[kThreads / 64];
   __shared__ double s_min[kThreads / 64];
   __shared__ int s_best[kThreads / 64 * 2];
@@ -157,14 +157,17 @@ __device__ __forceinline__ void ransac_rigid_frame(
     return;
   }
 
-  // LDS: sx, sy, dx, dy [N] f64 | trial S [T] f64 | [LARGE: stack [kMaxStack][256] f64]
+  // LDS: sx, sy, dx, dy [N] f64 | the points as (x, y, u, v) [N] f32x4 | trial S (low bound)
+  //      [T] f64 | trial S high bound [T] f64 | [LARGE: stack [kMaxStack][256] f64]
   //      | per-wave leaf values [4][128] f64 | trial count [T] i32 | inlier flags [N] u8
   double* sx = smem;
   double* sy = sx + N;
   double* dxs = sy + N;
   double* dys = dxs + N;
-  double* tS = dys + N;
-  double* stk = tS + T;
+  float4* pk32 = reinterpret_cast<float4*>(dys + N);  // 16-byte aligned: 4 N doubles before it
+  double* tS = reinterpret_cast<double*>(pk32 + N);
+  double* tSh = tS + T;
+  double* stk = tSh + T;
   double* wvals = stk + (LARGE ? kMaxStack * kThreads : 0);
   int* tC = reinterpret_cast<int*>(wvals + kThreads / 64 * 128);
   uint8_t* inl = reinterpret_cast<uint8_t*>(tC + T);
@@ -189,34 +192,115 @@ __device__ __forceinline__ void ransac_rigid_frame(
   }
   if (tid == 0) s_any_zero = 0;
   __syncthreads();
+  __shared__ Mag mg;
+  frame_mag(sx, sy, dxs, dys, N, red, mg);
+  for (int k = tid; k < N; k += kThreads) pk32[k] = centred32(sx[k], sy[k], dxs[k], dys[k], mg);
+  __syncthreads();
 
   const Pts P{sx, sy, dxs, dys};
   const uint32_t* H = hyp + hoff;
 
-  // ---- phase A: every trial's inlier count (exact, through q < tq) and fp32 S estimate.
-  // Then the best count is known exactly, and only trials at that count whose S can be
-  // within the estimates' error of the smallest one need the exact S (phase B, one whole
-  // wave per candidate).  Frames where that does not hold -- no trial with inliers, an
-  // estimate outside [1e-30, 1e30] (so also every S == 0, skimage's early exit), or a
-  // NaN tq -- score every trial exactly (the original single-phase loop).
+  // ---- phase A: every trial's inlier count and a bracket [tS, tSh] of its S.  In fp32
+  // (ransac_common.h score32: certain inliers, outliers and the undecided points between
+  // them; a trial whose map or frame is too large for the fp32 bound runs the fp64 form,
+  // score_fast).  A trial whose undecided points could lift it to the best certain count
+  // is scored again in fp64 (phase A2), so the best count is exact.  Then only trials at
+  // that count whose bracket reaches the smallest upper bound need the exact S (phase B,
+  // one whole wave per candidate).  Frames the brackets cannot decide -- no trial with
+  // inliers, a bracket outside [1e-30, 1e30] (so also every S == 0, skimage's early exit),
+  // or a NaN tq -- score every trial exactly (the original single-phase loop).
   const bool fast = tq == tq;  // NaN: exact scoring only (threshold outside the fast range)
   int mcount = -1, flag = fast ? 0 : 1;
   if (fast) {
+    int mlo = -1;
+    bool deferred = false;  // trials the fp32 bound cannot take: the fp64 loop below
     for (int t = tid; t < T; t += kThreads) {
       const uint32_t pr = H[t];
       const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
       const Model m = fit2(sx[i], sy[i], sx[j], sy[j], dxs[i], dys[i], dxs[j], dys[j]);
-      int cnt = -1;
-      float S32 = NAN;
-      if (m.ok) {
-        cnt = 0;
-        S32 = score_fast(m, P, N, tq, cnt);
-        if (!s32_certain(S32)) flag = 1;
+      int v = -1;
+      double slo = NAN, shi = NAN;
+      Lin32 L;
+      if (m.ok && lin32_make(m.c, -m.s, m.tx, m.s, m.c, m.ty, mg, tq, L)) {
+        int clo = 0, chi = 0;
+        const float S32 = score32(pk32, N, L, clo, chi);
+        s32_bracket(S32, N, L.be, slo, shi);
+        v = pack_cnt(clo, chi - clo);
+        if (!(slo >= 1e-30 && shi <= 1e30)) flag = 1;
+      } else if (m.ok) {
+        v = INT_MIN;
+        deferred = true;
       }
-      tC[t] = cnt;
-      tS[t] = (double)S32;
-      mcount = max(mcount, cnt);
+      tC[t] = v;
+      tS[t] = slo;
+      tSh[t] = shi;
+      mlo = max(mlo, cnt_of(v));
     }
+    if (deferred) {
+      for (int t = tid; t < T; t += kThreads) {
+        if (tC[t] != INT_MIN) continue;
+        const uint32_t pr = H[t];
+        const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
+        const Model m = fit2(sx[i], sy[i], sx[j], sy[j], dxs[i], dys[i], dxs[j], dys[j]);
+        int cnt = 0;
+        const float S32 = score_fast(m, P, N, tq, cnt);
+        double slo, shi;
+        s64_bracket(S32, N, slo, shi);
+        if (!(slo >= 1e-30 && shi <= 1e30)) flag = 1;
+        tC[t] = cnt;
+        tS[t] = slo;
+        tSh[t] = shi;
+        mlo = max(mlo, cnt);
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      mlo = max(mlo, __shfl_xor(mlo, o));
+      flag |= __shfl_xor(flag, o);
+    }
+    if (lane == 0) s_cnt[wave] = (mlo + 1) | (flag << 30);  // counts <= kMaxN
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) {
+      const int v = s_cnt[w];
+      flag |= v >> 30;
+      mlo = max(mlo, (v & 0x3fffffff) - 1);
+    }
+    __syncthreads();  // s_cnt is reused
+    // phase A2: the exact count of every trial the undecided points could lift to mlo, each
+    // by a whole wave (the points over the lanes, fp64 as score_fast computes them)
+    for (int t0 = wave * 64; t0 < T; t0 += kThreads) {
+      const int t = t0 + lane;
+      uint64_t need = __ballot(!flag && t < T && und_of(tC[t]) > 0 && cnt_of(tC[t]) + und_of(tC[t]) >= mlo);
+      while (need) {
+        const int tc = t0 + __builtin_ctzll(need);
+        need &= need - 1;
+        const uint32_t pr = H[tc];
+        const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
+        const Model m = fit2(sx[i], sy[i], sx[j], sy[j], dxs[i], dys[i], dxs[j], dys[j]);
+        int c = 0;
+        double sq = 0.0;
+        for (int k = lane; k < N; k += 64) {
+          const double x = sx[k], y = sy[k];
+          const double xp = fma(y, -m.s, x * m.c) + m.tx;
+          const double yp = fma(y, m.c, x * m.s) + m.ty;
+          const double ex = xp - dxs[k], ey = yp - dys[k];
+          const double q = ex * ex + ey * ey;
+          c += (q < tq) ? 1 : 0;
+          sq += q;
+        }
+        c = wave_sum_i(c);
+        double slo, shi;
+        sd_bracket(wave_sum(sq), N, slo, shi);
+        if (!(slo >= 1e-30 && shi <= 1e30)) flag = 1;
+        if (lane == 0) {
+          tC[tc] = c;
+          tS[tc] = slo;
+          tSh[tc] = shi;
+        }
+      }
+    }
+    __syncthreads();  // the A2 results of the other waves' lanes
+    for (int t = tid; t < T; t += kThreads) mcount = max(mcount, cnt_of(tC[t]));
   }
   for (int o = 32; o > 0; o >>= 1) {
     mcount = max(mcount, __shfl_xor(mcount, o));
@@ -271,10 +355,9 @@ __device__ __forceinline__ void ransac_rigid_frame(
       }
     }
   } else {
-    const double eps = s32_eps(N);
     double lm = INFINITY;
     for (int t = tid; t < T; t += kThreads)
-      if (tC[t] == mcount) lm = fmin(lm, tS[t] * (1.0 + eps));
+      if (cnt_of(tC[t]) == mcount) lm = fmin(lm, tSh[t]);
     for (int o = 32; o > 0; o >>= 1) lm = fmin(lm, __shfl_xor(lm, o));
     if (lane == 0) s_min[wave] = lm;
     __syncthreads();
@@ -284,7 +367,7 @@ __device__ __forceinline__ void ransac_rigid_frame(
     // phase B: this wave's candidate trials (t = t0 + lane), each scored by the whole wave
     for (int t0 = wave * 64; t0 < T; t0 += kThreads) {
       const int t = t0 + lane;
-      uint64_t cand = __ballot(t < T && tC[t] == mcount && tS[t] * (1.0 - eps) <= minhi);
+      uint64_t cand = __ballot(t < T && cnt_of(tC[t]) == mcount && tS[t] <= minhi);
       while (cand) {
         const int tc = t0 + __builtin_ctzll(cand);
         cand &= cand - 1;
@@ -425,7 +508,7 @@ __device__ __forceinline__ void ransac_rigid_frame(
 // Workgroup g scores frames g, g + grid, ... (the product launches one workgroup per frame;
 // narrower grids measured slower beside the warp).
 template <bool LARGE>
-__global__ __launch_bounds__(kThreads) void ransac_rigid_kernel(
+__global__ __launch_bounds__(kThreads, 4) void ransac_rigid_kernel(
     int n_frames, const double* __restrict__ src, const double* __restrict__ dst, const int32_t* __restrict__ pt_idx,
     const int32_t* __restrict__ pt_off, int src_stride, const uint32_t* __restrict__ hyp,
     const int32_t* __restrict__ hyp_off, int hyp_off_len,
@@ -460,9 +543,10 @@ static int ransac_rigid_impl(kcmc_ctx* ctx, const double* src, const double* dst
                                  std::to_string(trials) + " (call kcmc_ransac_prepare)");
   const int n_small = need < 128 ? need : 128;
   const size_t wvals = (size_t)kThreads / 64 * 128 * sizeof(double);
-  const size_t lds_small = (size_t)n_small * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) +
+  // per point 4 f64 + one f32x4, per trial 2 f64 + one i32
+  const size_t lds_small = (size_t)n_small * (4 * sizeof(double) + 16) + (size_t)trials * (2 * sizeof(double) + sizeof(int)) +
                            wvals + (size_t)n_small + 16;
-  const size_t lds_large = (size_t)need * 4 * sizeof(double) + (size_t)trials * (sizeof(double) + sizeof(int)) +
+  const size_t lds_large = (size_t)need * (4 * sizeof(double) + 16) + (size_t)trials * (2 * sizeof(double) + sizeof(int)) +
                            (size_t)kMaxStack * kThreads * sizeof(double) + wvals + (size_t)need + 16;
   const double tq = inlier_bound(thresh);
   if ((max_n > 128 ? lds_large : lds_small) > 150 * 1024)

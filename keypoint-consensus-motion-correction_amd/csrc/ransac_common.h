@@ -143,6 +143,188 @@ __device__ __forceinline__ double wave_pairwise(R2 r2, int N, const Plan& plan, 
 __device__ __forceinline__ double s32_eps(int N) { return (double)(N + 2) * 0x1p-22; }
 __device__ __forceinline__ bool s32_certain(float S32) { return S32 >= 1e-30f && S32 <= 1e30f; }
 
+// ---------------------------------------------------------------- phase A in fp32
+// The rigid scorer decides phase A in fp32 (round 6; fp64 VALU was 65 % of the scorers'
+// instructions): a trial's map (X, Y) = a x + b y + t is rounded to fp32 and
+// every point's residual e = (X - u, Y - v) and q = ex^2 + ey^2 are computed in fp32 from
+// fp32 copies of the points centred on the frame's bounding boxes (x' = x - c_x, ...; the
+// map's translation becomes t' = a c_x + b c_y + t - c_u, in fp64).  With
+// M' = |a_x| h_x + |b_x| h_y + |t'_x| + h_u (h = the boxes' half extents, likewise for Y)
+// and F = the same with the uncentred maxima, every |e32 - e| <= be = 7.01 2^-24 M' +
+// 2^-49 F (the roundings of the inputs, of the map and of the three fp32 operations, plus
+// the fp64 ones of the centring and of the reference's own e), so near q = tq
+//   |q32 - q| <= B = 2 be sqrt(8 tq) + 2 be^2 + 8.5 2^-24 tq    (used with a 1.25 margin),
+// and whenever B <= tq / 4: q32 < tq - B is an inlier, q32 > tq + B an outlier, for certain
+// (far from tq the bound is relatively smaller still); points in between are counted as
+// undecided, and a trial whose count the undecided points could lift to the best certain
+// count is counted again in fp64 by a whole wave (phase A2).  S = sum r^2 is bracketed by
+//   |S - S32| <= 2 be sqrt(2 N S') + 2 N be^2 + ((N + 2.1) 2^-24 + (N + 3) 2^-53) S'
+// (Cauchy-Schwarz over the points; S' bounds the sum of the q32 from the fp32 sum S32).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+struct Mag {  // the frame's bounding boxes: centres, half extents, max magnitudes
+  double cx, cy, cu, cv;  // (x, y): frame points; (u, v): template points
+  double hx, hy, hu, hv;
+  double X, Y, U, V;
+};
+
+struct Lin32 {
+  f32x2 a, b, t;  // (X - u, Y - v) = a x' + b y' + t - u' in centred coordinates
+  float lo, hi;   // certain inlier: q32 < lo; certain outlier: q32 > hi
+  double be;
+};
+
+__device__ __forceinline__ bool lin32_make(double ax, double bx, double tx, double ay, double by, double ty,
+                                           const Mag& mg, double tq, Lin32& L) {
+  const double tpx = ax * mg.cx + bx * mg.cy + tx - mg.cu;
+  const double tpy = ay * mg.cx + by * mg.cy + ty - mg.cv;
+  const double Mx = fabs(ax) * mg.hx + fabs(bx) * mg.hy + fabs(tpx) + mg.hu;
+  const double My = fabs(ay) * mg.hx + fabs(by) * mg.hy + fabs(tpy) + mg.hv;
+  const double Fx = fabs(ax) * mg.X + fabs(bx) * mg.Y + fabs(tx) + mg.U;
+  const double Fy = fabs(ay) * mg.X + fabs(by) * mg.Y + fabs(ty) + mg.V;
+  const double be = 7.01 * 0x1p-24 * fmax(Mx, My) + 0x1p-49 * fmax(Fx, Fy);
+  const double B = 1.25 * (2.0 * be * sqrt(8.0 * tq) + 2.0 * be * be + 8.5 * 0x1p-24 * tq);
+  if (!(B <= 0.25 * tq) || !(tq < 1e30)) return false;  // NaN / huge maps and coordinates: fp64
+  L.a = f32x2{(float)ax, (float)ay};
+  L.b = f32x2{(float)bx, (float)by};
+  L.t = f32x2{(float)tpx, (float)tpy};
+  float lo = (float)(tq - B), hi = (float)(tq + B);
+  // directed to the safe side (both positive: tq - B >= 3 tq / 4 > 0): one ulp down / up
+  if ((double)lo > tq - B) lo = __int_as_float(__float_as_int(lo) - 1);
+  if ((double)hi < tq + B) hi = __int_as_float(__float_as_int(hi) + 1);
+  L.lo = lo;
+  L.hi = hi;
+  L.be = be;
+  return true;
+}
+
+// The centred fp32 copy of point (x, y) -> (u, v).
+__device__ __forceinline__ float4 centred32(double x, double y, double u, double v, const Mag& mg) {
+  return make_float4((float)(x - mg.cx), (float)(y - mg.cy), (float)(u - mg.cu), (float)(v - mg.cv));
+}
+
+// Phase A of one trial in fp32 over the centred points (x', y', u', v') as float4 in LDS:
+// returns S32, adds the certain inliers to clo and the certain-or-undecided ones to chi.
+// Two points per iteration, so the reads of a pair are in flight together.
+__device__ __forceinline__ float score32(const float4* __restrict__ pk, int N, const Lin32& L, int& clo, int& chi) {
+  float S = 0.f;
+  auto one = [&](const float4 p) {
+    f32x2 e = L.t - f32x2{p.z, p.w};
+    e = __builtin_elementwise_fma(L.b, f32x2{p.y, p.y}, e);
+    e = __builtin_elementwise_fma(L.a, f32x2{p.x, p.x}, e);
+    const float q = __builtin_fmaf(e.x, e.x, e.y * e.y);
+    S += q;
+    clo += q < L.lo ? 1 : 0;
+    chi += q <= L.hi ? 1 : 0;
+  };
+  int k = 0;
+  for (; k + 2 <= N; k += 2) {
+    const float4 a = pk[k], b = pk[k + 1];
+    one(a);
+    one(b);
+  }
+  if (k < N) one(pk[k]);
+  return S;
+}
+
+// [lo, hi] around numpy's S of a trial scored by score32 (the bound above, 1e-9 margins).
+__device__ __forceinline__ void s32_bracket(float S32, int N, double be, double& lo, double& hi) {
+  const double S = (double)S32;
+  const double Sp = S * (1.0 + 1.01 * N * 0x1p-24);
+  const double E = 2.0 * be * sqrt(2.02 * N * Sp) + 2.0 * N * be * be + ((N + 2.1) * 0x1p-24 + (N + 3) * 0x1p-53) * Sp;
+  lo = (S - E) * (1.0 - 1e-9);
+  hi = (S + E) * (1.0 + 1e-9);
+}
+
+// The fp64 phase A's bracket (s32_eps) in the same form.
+__device__ __forceinline__ void s64_bracket(float S32, int N, double& lo, double& hi) {
+  const double eps = s32_eps(N);
+  lo = (double)S32 * (1.0 - eps);
+  hi = (double)S32 * (1.0 + eps);
+}
+
+// The bracket of a wave's fp64 sum Sd of the q (phase A2): numpy's S is within
+// (N + 3) 2^-53 S of the sum of the q, any summation order within (N - 1) 2^-53 (2x margin).
+__device__ __forceinline__ void sd_bracket(double Sd, int N, double& lo, double& hi) {
+  const double eps = (double)(2 * N + 8) * 0x1p-52;
+  lo = Sd * (1.0 - eps);
+  hi = Sd * (1.0 + eps);
+}
+
+// Phase A's per-trial record in the tC array: the certain inlier count and the undecided
+// points (cnt | und << 16, counts <= kMaxN < 2^16), -1 for a trial without a model.
+__device__ __forceinline__ int pack_cnt(int cnt, int und) { return cnt | (und << 16); }
+__device__ __forceinline__ int cnt_of(int v) { return v < 0 ? v : (v & 0xffff); }
+__device__ __forceinline__ int und_of(int v) { return v < 0 ? 0 : (v >> 16); }
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// The frame's bounding boxes for lin32_make: workgroup min / max over the staged points.
+// A NaN or infinite coordinate makes the half extents infinite (every trial then runs the
+// fp64 phase A).
+// The result goes to the shared `out` (read per trial, not held in registers).
+__device__ inline void frame_mag(const double* sx, const double* sy, const double* dx, const double* dy, int N,
+                                 double* red, Mag& out) {
+  double lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  bool bad = false;
+  for (int k = threadIdx.x; k < N; k += kThreads) {
+    const double c[4] = {sx[k], sy[k], dx[k], dy[k]};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bad |= !(fabs(c[i]) < INFINITY);
+      lo[i] = fmin(lo[i], c[i]);
+      hi[i] = fmax(hi[i], c[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (bad) {
+      lo[i] = -INFINITY;
+      hi[i] = INFINITY;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      lo[i] = fmin(lo[i], __shfl_xor(lo[i], o));
+      hi[i] = fmax(hi[i], __shfl_xor(hi[i], o));
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      red[8 * wave + i] = lo[i];
+      red[8 * wave + 4 + i] = hi[i];
+    }
+  __syncthreads();
+  double L[4], Hh[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    L[i] = red[i];
+    Hh[i] = red[4 + i];
+    for (int w = 1; w < kThreads / 64; ++w) {
+      L[i] = fmin(L[i], red[8 * w + i]);
+      Hh[i] = fmax(Hh[i], red[8 * w + 4 + i]);
+    }
+  }
+  double c[4], h[4], m[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool fin = fabs(L[i]) < INFINITY && fabs(Hh[i]) < INFINITY;
+    c[i] = fin ? 0.5 * L[i] + 0.5 * Hh[i] : 0.0;
+    h[i] = fin ? fmax(Hh[i] - c[i], c[i] - L[i]) * (1.0 + 0x1p-50) : INFINITY;  // >= every |x - c|
+    m[i] = fmax(fabs(L[i]), fabs(Hh[i]));
+  }
+  if (threadIdx.x == 0) {
+    out.cx = c[0]; out.cy = c[1]; out.cu = c[2]; out.cv = c[3];
+    out.hx = h[0]; out.hy = h[1]; out.hu = h[2]; out.hv = h[3];
+    out.X = m[0]; out.Y = m[1]; out.U = m[2]; out.V = m[3];
+  }
+  __syncthreads();  // out is visible, red is free
+}
+
 __device__ inline double block_sum(double v, double* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

@@ -724,12 +724,13 @@ def brightest_px(frames, percentile: float = 99.99) -> np.float64:
         hs = []
         for p in parts:  # queued on every device before the first host read
             dev = _device_of(p)
-            h = torch.empty(256, dtype=torch.int64, device=dev)
-            if p.numel():
-                _lib.check(L.kcmc_histogram_u16(_ctx(dev).handle, _ptr(p), p.numel(), shift, hb, _ptr(h),
-                                                _stream(dev)))
-            else:
-                h.zero_()
+            with torch.cuda.device(dev):  # the launch, its workspace and h on the part's device
+                h = torch.empty(256, dtype=torch.int64, device=dev)
+                if p.numel():
+                    _lib.check(L.kcmc_histogram_u16(_ctx(dev).handle, _ptr(p), p.numel(), shift, hb, _ptr(h),
+                                                    _stream(dev)))
+                else:
+                    h.zero_()
             hs.append(h)
         return np.sum([h.cpu().numpy() for h in hs], axis=0)
 

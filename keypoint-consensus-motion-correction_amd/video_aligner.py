@@ -267,7 +267,10 @@ class VideoAligner:
         assert (images.dtype == torch.uint16) if on_device else (np.asarray(images).dtype == np.uint16)  # VA:104
         parts = _md.split_to_devices(images if on_device else np.asarray(images), ranges, devices)
         brightest_px = stages.brightest_px(parts, self.IMAGE_NORM_MAX_PERCENTILE)
-        u8_parts = [self._max_scale_images(p, None, brightest_px, np.uint8)[0] for p in parts]
+        u8_parts = []
+        for p in parts:  # each slab's work under its own device (launches, workspaces, allocations)
+            with _md._on(p):
+                u8_parts.append(self._max_scale_images(p, None, brightest_px, np.uint8)[0])
         _, template_i8 = self._max_scale_images(None, template, brightest_px, np.uint8)
         detector = self.DETECTOR_CONSTRUCTOR_DICT[detector_algorithm]()
         on_gpu = isinstance(detector, GpuOrbDetector) and parts[0].dim() == 3
@@ -278,15 +281,20 @@ class VideoAligner:
         cfg = self._config(n_kp_global, rate)
         if on_gpu:  # f1 per device: each slab's sample frames detected where they live
             tpl_u8 = np.ascontiguousarray(template_i8)
-            samples = [_pl.downsample_u8(u, torch.from_numpy(tpl_u8).to(u.device)[None], rate,
-                                         self.SPATIAL_DOWNSAMPLE_RATE) for u in u8_parts]
-            kt = stages.detect_orb(samples[0][1], detector.params)
+            samples = []
+            for u in u8_parts:
+                with _md._on(u):
+                    samples.append(_pl.downsample_u8(u, torch.from_numpy(tpl_u8).to(u.device)[None], rate,
+                                                     self.SPATIAL_DOWNSAMPLE_RATE))
+            with _md._on(samples[0][1]):
+                kt = stages.detect_orb(samples[0][1], detector.params)
             n_t = int(kt.count.cpu()[0])
             self._kp_template = kt.kp[0, :n_t].cpu().numpy()
             self._des_template = kt.des[0, :n_t].cpu().numpy()
             slabs = []
             for fr, (smp, _) in zip(parts, samples):
-                kp_q, des_q, q_off, q_off_host = stages.keypoints_csr(stages.detect_orb(smp, detector.params))
+                with _md._on(smp):
+                    kp_q, des_q, q_off, q_off_host = stages.keypoints_csr(stages.detect_orb(smp, detector.params))
                 dev = fr.device
                 slabs.append(_pl.SlabInputs(fr, torch.from_numpy(self._des_template).to(dev),
                                             torch.from_numpy(self._kp_template).to(dev), des_q, kp_q, q_off, q_off_host))

@@ -184,6 +184,51 @@ def test_ransac_rigid_fuzz_vs_oracle(dev, seed):
                                    equal_nan=True, err_msg=str((seed, f)))
 
 
+@pytest.mark.parametrize("model", ["rigid", "affine", "projective"])
+@pytest.mark.parametrize("scale", [1.0, 2000.0, 3e5])
+def test_ransac_threshold_band_vs_oracle(dev, model, scale):
+    """Points whose residual under the true map lies within 1e-12 .. 1e-2 of the threshold
+    (2 px), so the fp32 phase A (ransac_common.h score32) must leave them undecided and the
+    trials that reach the best count are counted again in fp64 (phase A2): counts, inliers,
+    winning trial bit-exact, params as the oracle.  Coordinates up to 3e5 px make the fp32
+    band wide (and past ~1e5 px the trials fall back to the fp64 phase A)."""
+    rng = np.random.default_rng(int(scale) + {"rigid": 0, "affine": 1, "projective": 2}[model])
+    tpls, qs = [], []
+    for f in range(6):
+        n_exact, n_band, n_out = 12 + 3 * f, 20, 10
+        tpl = rng.uniform(0.2, 1.0, (n_exact + n_band + n_out, 2)) * scale
+        a = rng.normal(0, 0.02)
+        A = np.array([[np.cos(a), -np.sin(a)], [np.sin(a), np.cos(a)]])
+        if model != "rigid":
+            A = A @ np.array([[1.01, 0.02], [0.0, 0.99]])
+        t = rng.normal(0, 5, 2)
+        q = (tpl - t) @ np.linalg.inv(A).T  # q maps onto tpl exactly: A q + t = tpl
+        # band points: displace the template point by 2 + d px along a random direction
+        d = rng.choice([-1e-2, -1e-5, -1e-9, -1e-12, 0.0, 1e-12, 1e-9, 1e-5, 1e-2], n_band)
+        ang = rng.uniform(0, 2 * np.pi, n_band)
+        sl = slice(n_exact, n_exact + n_band)
+        tpl[sl] += (2.0 + d)[:, None] * np.stack([np.cos(ang), np.sin(ang)], 1)
+        tpl[n_exact + n_band:] += rng.uniform(5, 50, (n_out, 2))
+        tpls.append(tpl)
+        qs.append(q)
+    off = _csr(qs)
+    args = (_t(np.concatenate(qs), dev), _t(np.concatenate(tpls), dev), _t(off, dev), off)
+    r = stages.ransac_rigid(*args) if model == "rigid" else stages.ransac_model(*args, model=model)
+    params, inl = r.params.cpu().numpy(), r.inliers.cpu().numpy().astype(bool)
+    nin, best = r.n_inliers.cpu().numpy(), r.best_trial.cpu().numpy()
+    for f in range(len(qs)):
+        if model == "rigid":
+            p, i_ref, bt, ni = oracle.ransac_rigid(qs[f], tpls[f])
+        else:
+            p, i_ref, bt, ni = oracle.ransac_model(qs[f], tpls[f], model)
+        assert best[f] == bt and nin[f] == ni, (model, scale, f, best[f], bt, nin[f], ni)
+        assert np.array_equal(inl[off[f]:off[f + 1]], i_ref), (model, scale, f)
+        if model == "rigid":
+            np.testing.assert_allclose(params[f], p, rtol=1e-10, atol=1e-10 * scale)
+        else:
+            _check_refit(params[f], p, qs[f][i_ref], tpls[f][i_ref], model, ni, (model, scale, f))
+
+
 def _tls_model(A, Ns, Nd, model, v):
     H = np.zeros((3, 3))
     cols = [0, 1, 2, 3, 4, 5] if model == "affine" else list(range(8))
