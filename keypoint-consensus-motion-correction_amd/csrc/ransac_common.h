@@ -142,6 +142,11 @@ __device__ __forceinline__ double wave_pairwise(R2 r2, int N, const Plan& plan, 
 // [1e-30, 1e30], with a 2x margin.
 __device__ __forceinline__ double s32_eps(int N) { return (double)(N + 2) * 0x1p-22; }
 __device__ __forceinline__ bool s32_certain(float S32) { return S32 >= 1e-30f && S32 <= 1e30f; }
+// The same for a sequential fp64 sum Sd of the q (the model scorers' phase A): numpy's S is
+// within (N + 3) 2^-53 S of the exact sum of the q, Sd within (N - 1) 2^-53 (2x margin); the
+// range excludes every S == 0 (skimage's early exit) and the under / overflowing sums.
+__device__ __forceinline__ double sd_eps(int N) { return (double)(2 * N + 8) * 0x1p-52; }
+__device__ __forceinline__ bool sd_certain(double Sd) { return Sd >= 1e-290 && Sd <= 1e290; }
 
 // ---------------------------------------------------------------- phase A in fp32
 // The rigid scorer decides phase A in fp32 (round 6; fp64 VALU was 65 % of the scorers'

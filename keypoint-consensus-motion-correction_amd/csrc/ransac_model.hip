@@ -375,10 +375,13 @@ __device__ __forceinline__ double pw_leaf(const double (&h)[9], const Pts& P, in
 }
 
 // Phase A of the scoring (the rigid kernel's, ransac.hip): the exact inlier count through
-// q < tq (q computed as resid2 computes it) and the fp32 estimate S32 = sum (float)q_k.
+// q < tq (q computed as resid2 computes it) and the estimate Sd = sum q_k, summed in
+// sequence in fp64 (round 6; was an fp32 sum of (float)q_k): within sd_eps(N) of numpy's S,
+// so phase B re-scores only trials tied to ~1e-14 instead of ~1e-5 (one fp64 add per point
+// in place of a conversion and an fp32 add).
 template <int MODEL>
-__device__ __forceinline__ float score_fast(const double (&h)[9], const Pts& P, int N, double tq, int& cnt) {
-  float S = 0.f;
+__device__ __forceinline__ double score_fast(const double (&h)[9], const Pts& P, int N, double tq, int& cnt) {
+  double S = 0.0;
   for (int k = 0; k < N; ++k) {
     const double x = P.sx[k], y = P.sy[k];
     double X = fma(y, h[1], x * h[0]) + h[2];
@@ -392,7 +395,7 @@ __device__ __forceinline__ float score_fast(const double (&h)[9], const Pts& P, 
     const double ex = X - P.dx[k], ey = Y - P.dy[k];
     const double q = ex * ex + ey * ey;
     cnt += (q < tq) ? 1 : 0;
-    S += (float)q;
+    S += q;
   }
   return S;
 }
@@ -406,9 +409,9 @@ struct __attribute__((aligned(16))) PackedPt {
 };
 
 template <int MODEL>
-__device__ __forceinline__ float score_fast_packed(const double (&h)[9], const PackedPt* __restrict__ pk, int N,
-                                                   double tq, int& cnt) {
-  float S = 0.f;
+__device__ __forceinline__ double score_fast_packed(const double (&h)[9], const PackedPt* __restrict__ pk, int N,
+                                                    double tq, int& cnt) {
+  double S = 0.0;
   auto one = [&](const PackedPt p) {
     double X = fma(p.s.y, h[1], p.s.x * h[0]) + h[2];
     double Y = fma(p.s.y, h[4], p.s.x * h[3]) + h[5];
@@ -421,7 +424,7 @@ __device__ __forceinline__ float score_fast_packed(const double (&h)[9], const P
     const double ex = X - p.d.x, ey = Y - p.d.y;
     const double q = ex * ex + ey * ey;
     cnt += (q < tq) ? 1 : 0;
-    S += (float)q;
+    S += q;
   };
   int k = 0;
   for (; k + 2 <= N; k += 2) {
@@ -565,15 +568,15 @@ __device__ __forceinline__ void ransac_model_score_frame(
       bool need_exact;
       const HModel m = fit_trial_fast<MODEL>(P, H[t], need_exact);
       int cnt = -1;
-      float S32 = NAN;
+      double Sd = NAN;
       if (m.ok) {
         cnt = 0;
-        S32 = LARGE ? score_fast<MODEL>(m.h, P, N, tq, cnt) : score_fast_packed<MODEL>(m.h, pk, N, tq, cnt);
-        if (!s32_certain(S32)) flag = 1;
+        Sd = LARGE ? score_fast<MODEL>(m.h, P, N, tq, cnt) : score_fast_packed<MODEL>(m.h, pk, N, tq, cnt);
+        if (!sd_certain(Sd)) flag = 1;
       }
       deferred |= need_exact;
       tC[t] = need_exact ? INT_MIN : cnt;
-      tS[t] = (double)S32;
+      tS[t] = Sd;
       mcount = max(mcount, cnt);
     }
     // trials whose fast fit fell outside its ranges (in practice none): the reference fit
@@ -582,14 +585,14 @@ __device__ __forceinline__ void ransac_model_score_frame(
         if (tC[t] != INT_MIN) continue;
         const HModel m = fit_trial<MODEL>(P, H[t]);
         int cnt = -1;
-        float S32 = NAN;
+        double Sd = NAN;
         if (m.ok) {
           cnt = 0;
-          S32 = LARGE ? score_fast<MODEL>(m.h, P, N, tq, cnt) : score_fast_packed<MODEL>(m.h, pk, N, tq, cnt);
-          if (!s32_certain(S32)) flag = 1;
+          Sd = LARGE ? score_fast<MODEL>(m.h, P, N, tq, cnt) : score_fast_packed<MODEL>(m.h, pk, N, tq, cnt);
+          if (!sd_certain(Sd)) flag = 1;
         }
         tC[t] = cnt;
-        tS[t] = (double)S32;
+        tS[t] = Sd;
         mcount = max(mcount, cnt);
       }
     }
@@ -647,7 +650,7 @@ __device__ __forceinline__ void ransac_model_score_frame(
       }
     }
   } else {
-    const double eps = s32_eps(N);
+    const double eps = sd_eps(N);
     double lm = INFINITY;
     for (int t = tid; t < T; t += kThreads)
       if (tC[t] == mcount) lm = fmin(lm, tS[t] * (1.0 + eps));

@@ -502,8 +502,19 @@ class VideoAligner:
         return stages.warp_affine_u16(img, a).cpu().numpy()[0]
 
     def _parallelize(self, func: Callable, *sequences: Sequence, **kwargs) -> List:
-        """VA:460-465 kept for API compatibility (ordered map; the hot path is batched)."""
-        return [func(*[x[i] for x in sequences], **kwargs) for i in range(len(sequences[0]))]
+        """VA:460-465: func over the equal-length sequences, results in order, in a joblib
+        process pool of N_JOBS_PARALLEL workers (backend "multiprocessing", as the reference)
+        -- for a subclass's own (picklable, CPU) per-frame function.  This package's functions
+        run in this process instead: they are GPU-backed, a forked worker cannot use the
+        parent's GPU context, and the hot path batches them anyway."""
+        r = range(len(sequences[0]))
+        mod = getattr(func, "__module__", "") or ""
+        if mod.split(".")[0] == __name__.split(".")[0] or int(self.N_JOBS_PARALLEL) <= 1 or len(r) <= 1:
+            return [func(*[x[i] for x in sequences], **kwargs) for i in r]
+        from joblib import Parallel, delayed
+
+        with Parallel(n_jobs=int(self.N_JOBS_PARALLEL), backend="multiprocessing") as parallel:
+            return list(parallel(delayed(func)(*[x[i] for x in sequences], **kwargs) for i in r))
 
     def _parallelize_i(self, func: Callable, *sequences: Sequence, **kwargs) -> List:
         r = range(len(sequences[0]))

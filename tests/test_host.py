@@ -359,3 +359,21 @@ def test_fill_gaps_slab_equals_global_interpolation(lerp):
         assert sk == ref_sk and it == ref_it
     with pytest.raises(VideoAligner.AlignmentError):
         affines.fill_gaps_slab(np.full((3, 2, 3), np.nan), 4, None, None, True)
+
+
+def _square_plus(i, x, k=0):  # module level: picklable for the process pool
+    return i * 1000 + x * x + k
+
+
+def test_parallelize_is_an_ordered_process_pool_map():
+    """VA:460-471: _parallelize / _parallelize_i map a picklable per-frame function over equal
+    sequences in a joblib multiprocessing pool of N_JOBS_PARALLEL workers, results in order;
+    one worker (or this package's own GPU-backed functions) runs in this process."""
+    va = VideoAligner()
+    xs = list(range(37))
+    assert va._parallelize_i(_square_plus, xs, k=5) == [i * 1000 + i * i + 5 for i in xs]
+
+    class One(VideoAligner):
+        N_JOBS_PARALLEL = 1
+
+    assert One()._parallelize(_square_plus, [1, 2], [3, 4]) == [1009, 2016]
