@@ -46,7 +46,10 @@ class SlabStages:
     lookup(keep_bits, n_tpl, choice) -> stages.Consensus with the point lists of these frames;
     ransac(kp_ordered, kp_tpl, cons, cfg) -> params [F, 2, 3] / [F, 3, 3] f64 tensor;
     boundary(params) -> [2 + 2E] f64 tensor (kcmc_params_boundary);
-    warp(frames, affines_host [F, ...]) -> aligned tensor."""
+    warp(frames, affines_host [F, ...]) -> aligned tensor;
+    warp_params(frames, params) -> aligned tensor: the warp with ransac's own parameters
+    where they lie (a frame without a model -- NaN parameters -- comes out as zeros), or
+    None when the stages have no such warp."""
 
     match: Callable
     vote: Callable
@@ -54,6 +57,7 @@ class SlabStages:
     ransac: Callable
     boundary: Callable
     warp: Callable
+    warp_params: Optional[Callable] = None
 
 
 def _hip_match(inp: _pl.SlabInputs, cfg: _pl.AlignConfig):
@@ -81,7 +85,12 @@ def _hip_warp(frames: torch.Tensor, affines: np.ndarray) -> torch.Tensor:
     return _pl.warp_stage(frames, affines)
 
 
-HIP_STAGES = SlabStages(_hip_match, _hip_vote, _hip_lookup, _hip_ransac, stages.params_boundary, _hip_warp)
+def _hip_warp_params(frames: torch.Tensor, params: torch.Tensor) -> torch.Tensor:
+    return _pl.warp_frames(frames, params)
+
+
+HIP_STAGES = SlabStages(_hip_match, _hip_vote, _hip_lookup, _hip_ransac, stages.params_boundary, _hip_warp,
+                        _hip_warp_params)
 
 
 def _all_gather_rows(t: torch.Tensor, counts: List[int], group=None) -> torch.Tensor:

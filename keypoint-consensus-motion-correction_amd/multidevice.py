@@ -12,12 +12,14 @@ form) and keeps every cross-frame step on the host exactly once:
      GLOBAL first sample index, kcmc_consensus_vote), the votes copied to the host;
   2. host: the votes of every slab merged ONCE (Counter.most_common + set(consensus) order,
      VA:224-249, kcmc_consensus_merge) -- the same merge a one-device run makes;
-  3. per slab, queued on every device: the consensus lookup (VA:251-286) + K2 RANSAC;
+  3. per slab, queued on every device: the consensus lookup (VA:251-286) + K2 RANSAC, and
+     without temporal downsampling the K3 warp right behind it with the parameters where
+     RANSAC left them (a frame with a model keeps its own parameters through step 4);
   4. host: the parameters of every slab concatenated in frame order and post-processed once
      (NaN padding for temporal downsampling, gap interpolation across slab boundaries,
-     VA:143-145);
-  5. per slab: K3 warp of its full-rate frames with its rows of the global maps, the
-     result copied into its slice of one output.
+     VA:143-145), while the warps of step 3 run;
+  5. per slab: K3 warp of its full-rate frames with its rows of the global maps (after a
+     step-3 warp: only the frames without a model, which it left at zero).
 Every per-frame stage is independent of the other frames, so the result equals
 ``pipeline.align_slab`` over the whole stack bit for bit (tests/test_gpu_multidevice.py
 runs two slabs on one GPU against one slab).  A device may appear more than once in the
@@ -133,26 +135,62 @@ def align_split(slabs: Sequence[_pl.SlabInputs], ranges: Sequence[SlabRange], cf
     # 2. one merge of every slab's votes on the host
     votes = np.stack([v.cpu().numpy() for _, _, v in matched])
     choice = _pl.choose_consensus(votes, n_tpl, n_sample, cfg, logger)
-    # 3. lookup + RANSAC of every slab
-    fitted = []
+    for inp, r in zip(slabs, ranges):
+        if inp.frames.shape[0] != r.f1 - r.f0:
+            raise ValueError("align_split: a slab's frames do not match its SlabRange")
+    # 3. lookup + RANSAC of every slab.  Without temporal downsampling a frame with a model
+    # keeps its own parameters through the post-processing (VA:143-145), so each slab's warp
+    # is queued right behind its RANSAC with the parameters where RANSAC left them, and the
+    # host post-processes while it runs; only the frames without a model (warped to zeros)
+    # wait for the host's gap-filled maps.
+    device_maps = impl.warp_params is not None and int(cfg.frame_downsample_rate) == 1
+    fitted, aligned = [], []
     for inp, (keep_bits, kp_ordered, _) in zip(slabs, matched):
         with _on(inp.kp_tpl):
             cons = impl.lookup(keep_bits, n_tpl, choice)
-            fitted.append((cons, impl.ransac(kp_ordered, inp.kp_tpl, cons, cfg)))
+            params = _to_host_async(impl.ransac(kp_ordered, inp.kp_tpl, cons, cfg))
+            fitted.append((cons, params))
+            if device_maps:
+                aligned.append(impl.warp_params(inp.frames, params[0]))
     if logger is not None and logger.isEnabledFor(logging.INFO):
         for (cons, _), r in zip(fitted, ranges):
             _pl._log_low_counts(logger, np.diff(cons.pt_off), cfg, r.s0)
     # 4. the global post-processing, once
-    params = np.concatenate([p.cpu().numpy() for _, p in fitted])
+    params = np.concatenate([_host_array(p) for _, p in fitted])
     affines, skipped, interpolated, eu = _pl.postprocess_affines(params, cfg)
-    # 5. the warp of every slab with its rows of the global maps
-    aligned = []
-    for inp, r in zip(slabs, ranges):
-        if inp.frames.shape[0] != r.f1 - r.f0:
-            raise ValueError("align_split: a slab's frames do not match its SlabRange")
-        with _on(inp.kp_tpl):
-            aligned.append(impl.warp(inp.frames, np.ascontiguousarray(affines[r.f0:r.f1])))
+    # 5. the warp of every slab with its rows of the global maps (device maps: only the
+    # frames without a model)
+    if device_maps:
+        redo = np.zeros(len(affines), bool)
+        redo[np.asarray(skipped, dtype=np.int64)] = True
+        for inp, r, out in zip(slabs, ranges, aligned):
+            with _on(inp.kp_tpl):
+                for a, b in _pl._runs(redo[r.f0:r.f1]):
+                    out[a:b] = impl.warp(inp.frames[a:b], np.ascontiguousarray(affines[r.f0 + a:r.f0 + b]))
+    else:
+        for inp, r in zip(slabs, ranges):
+            with _on(inp.kp_tpl):
+                aligned.append(impl.warp(inp.frames, np.ascontiguousarray(affines[r.f0:r.f1])))
     return SplitResult(aligned, list(ranges), affines, eu, skipped, interpolated)
+
+
+def _to_host_async(t: torch.Tensor):
+    """(t, its host copy, an event after the copy): a device tensor is copied into pinned
+    memory on the current stream without blocking the host; a host tensor is its own copy."""
+    if t.device.type != "cuda":
+        return t, t, None
+    host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    host.copy_(t, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    return t, host, ev
+
+
+def _host_array(p) -> np.ndarray:
+    _, host, ev = p
+    if ev is not None:
+        ev.synchronize()
+    return host.numpy()
 
 
 def visible_devices() -> List[int]:

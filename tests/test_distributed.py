@@ -74,7 +74,13 @@ def _oracle_stages(model="euclidean", no_model=False):
         fn = oracle.warp_perspective_u16 if model == "projective" else oracle.warp_affine_u16
         return torch.from_numpy(np.stack([fn(fr[f], affines[f]) for f in range(len(fr))]))
 
-    return kdist.SlabStages(match, vote, lookup, ransac, _boundary_np, warp)
+    def warp_params(frames, params):  # the HIP warp's contract: a frame without a model -> zeros
+        p = params.numpy()
+        out = warp(frames, np.nan_to_num(p)).numpy()
+        out[np.isnan(p).reshape(len(p), -1).any(axis=1)] = 0
+        return torch.from_numpy(out)
+
+    return kdist.SlabStages(match, vote, lookup, ransac, _boundary_np, warp, warp_params)
 
 
 def _slab(rank, n_frames, model="euclidean"):

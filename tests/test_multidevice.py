@@ -6,6 +6,8 @@ infrastructure; tests/test_distributed.py's).  Splitting a stack into 1, 2 or 3 
 not change a single value, also when the frames around a slab boundary have no model (the
 NaN gap is interpolated across the boundary) and with temporal downsampling (rate 2: the
 NaN padding of VA:338-344 stays inside a slab)."""
+import dataclasses
+
 import numpy as np
 import pytest
 import torch
@@ -72,9 +74,11 @@ def test_split_equals_one_slab(model, rate, blind):
     ref = md.align_split(_cpu_slabs(ks, frames, md.split_frames(len(frames), rate, 1)),
                          md.split_frames(len(frames), rate, 1), cfg, impl=st)
     assert len(ref.skipped) >= len(blind)  # the premise: frames without a model
-    for parts in (2, 3, 4):
+    # parts 1 with the warp behind the post-processing for every frame (no warp_params):
+    # the device-map warp plus the re-warp of the frames without a model must equal it
+    for parts, impl in ((1, dataclasses.replace(st, warp_params=None)), (2, st), (3, st), (4, st)):
         rs = md.split_frames(len(frames), rate, parts)
-        got = md.align_split(_cpu_slabs(ks, frames, rs), rs, cfg, impl=st)
+        got = md.align_split(_cpu_slabs(ks, frames, rs), rs, cfg, impl=impl)
         np.testing.assert_array_equal(got.affines, ref.affines)
         np.testing.assert_array_equal(got.euclidean, ref.euclidean)
         assert got.skipped == ref.skipped and got.interpolated == ref.interpolated

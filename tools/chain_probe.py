@@ -9,7 +9,9 @@ could give.
     python tools/chain_probe.py <stages> -- <bench.py arguments>
     stages: comma list of match, vote, merge, lookup, ransac (or "none"); "spin" in
     the list makes the host poll the pipeline's events (hipEventQuery) instead of
-    blocking on them (hipEventSynchronize)
+    blocking on them (hipEventSynchronize); "hostmaps" makes multidevice.align_split (bench.py
+    --single-process) warp every frame behind the host post-processing, as before round 6's
+    device-map warp
 
 e.g. python tools/chain_probe.py lookup -- --config c3 --steps 60 --warmup 5 --cpu-sample 0
 """
@@ -33,7 +35,7 @@ def main():
     a = sys.argv[1:]
     split = a.index("--") if "--" in a else len(a)
     skip = {s for s in (a[0].split(",") if split > 0 else []) if s and s != "none"}
-    unknown = skip - {"match", "vote", "merge", "lookup", "ransac", "spin"}
+    unknown = skip - {"match", "vote", "merge", "lookup", "ransac", "spin", "hostmaps"}
     if unknown:
         raise SystemExit(f"chain_probe: unknown stages {sorted(unknown)}")
     import time
@@ -41,6 +43,12 @@ def main():
     import bench
     from kcmc_amd import pipeline, stages
 
+    if "hostmaps" in skip:  # not a stage: align_split warps behind the host post-processing
+        import dataclasses
+
+        from kcmc_amd import distributed as kdist
+
+        kdist.HIP_STAGES = dataclasses.replace(kdist.HIP_STAGES, warp_params=None)
     if "spin" in skip:  # not a stage: the host polls its events instead of blocking on them
         def _wait(self, ev):
             t0 = time.perf_counter()
