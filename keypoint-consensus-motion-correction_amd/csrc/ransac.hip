@@ -156,6 +156,7 @@ __device__ __forceinline__ void ransac_rigid_frame(
     }
     return;
   }
+  const uint32_t* H = hyp + hoff;
 
   // LDS: sx, sy, dx, dy [N] f64 | the points as (x, y, u, v) [N] f32x4 | trial S (low bound)
   //      [T] f64 | trial S high bound [T] f64 | [LARGE: stack [kMaxStack][256] f64]
@@ -176,7 +177,7 @@ __device__ __forceinline__ void ransac_rigid_frame(
     plan_gen<kPwDepth>(s_plan, 0, N);
   }
 
-  for (int k = tid; k < N; k += kThreads) {
+  auto gather = [&](int k, double (&c)[4]) {
     size_t si, di;
     if (pt_idx) {
       const int q = pt_idx[p0 + k];
@@ -185,20 +186,60 @@ __device__ __forceinline__ void ransac_rigid_frame(
     } else {
       si = di = (size_t)(p0 + k);
     }
-    sx[k] = src[2 * si];
-    sy[k] = src[2 * si + 1];
-    dxs[k] = dst[2 * di];
-    dys[k] = dst[2 * di + 1];
-  }
+    c[0] = src[2 * si];
+    c[1] = src[2 * si + 1];
+    c[2] = dst[2 * di];
+    c[3] = dst[2 * di + 1];
+  };
   if (tid == 0) s_any_zero = 0;
-  __syncthreads();
   __shared__ Mag mg;
-  frame_mag(sx, sy, dxs, dys, N, red, mg);
-  for (int k = tid; k < N; k += kThreads) pk32[k] = centred32(sx[k], sy[k], dxs[k], dys[k], mg);
-  __syncthreads();
+  if (!LARGE) {
+    // N <= 128: wave 0 stages every point (k = lane, lane + 64), takes the frame's boxes by
+    // wave reductions (min / max: the same bounds in any order) and writes the fp32 copies,
+    // behind one barrier (the workgroup form takes five)
+    if (wave == 0) {
+      double c[2][4], lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      bool bad = false;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = lane + 64 * h;
+        if (k < N) {
+          gather(k, c[h]);
+          mag_add(c[h], lo, hi, bad);
+        }
+      }
+      wave_bounds(lo, hi, bad);
+      const Mag m = mag_of(lo, hi);
+      if (lane == 0) mg = m;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = lane + 64 * h;
+        if (k < N) {
+          sx[k] = c[h][0];
+          sy[k] = c[h][1];
+          dxs[k] = c[h][2];
+          dys[k] = c[h][3];
+          pk32[k] = centred32(c[h][0], c[h][1], c[h][2], c[h][3], m);
+        }
+      }
+    }
+    __syncthreads();
+  } else {
+    for (int k = tid; k < N; k += kThreads) {
+      double c[4];
+      gather(k, c);
+      sx[k] = c[0];
+      sy[k] = c[1];
+      dxs[k] = c[2];
+      dys[k] = c[3];
+    }
+    __syncthreads();
+    frame_mag(sx, sy, dxs, dys, N, red, mg);
+    for (int k = tid; k < N; k += kThreads) pk32[k] = centred32(sx[k], sy[k], dxs[k], dys[k], mg);
+    __syncthreads();
+  }
 
   const Pts P{sx, sy, dxs, dys};
-  const uint32_t* H = hyp + hoff;
 
   // ---- phase A: every trial's inlier count and a bracket [tS, tSh] of its S.  In fp32
   // (ransac_common.h score32: certain inliers, outliers and the undecided points between
@@ -456,34 +497,73 @@ __device__ __forceinline__ void ransac_rigid_frame(
   }
   __syncthreads();
   // refit on the inliers (skimage fit.py:871-875 -> _umeyama over d[best_inliers])
-  double s0 = 0, s1 = 0, s2 = 0, s3 = 0, cntd = 0;
-  for (int k = tid; k < N; k += kThreads)
-    if (inl[k]) {
-      s0 += sx[k];
-      s1 += sy[k];
-      s2 += dxs[k];
-      s3 += dys[k];
-      cntd += 1.0;
+  double n_in, ms0, ms1, md0, md1, a00 = 0, a01 = 0, a10 = 0, a11 = 0;
+  if (!LARGE) {
+    // N <= 128: wave 0 alone, with no barrier.  Lane l holds points l and l + 64, the
+    // points threads l and l + 64 hold in the workgroup form below; each half goes through
+    // the same butterfly as there, and the halves are added as block_sum adds its four wave
+    // sums (0 + wave 0 + wave 1 + 0 + 0), so every sum is the same to the bit.
+    if (wave != 0) return;
+    const int k1 = lane + 64;
+    const bool i0 = lane < N && inl[lane], i1 = k1 < N && inl[k1];
+    auto half_sums = [&](double lo, double hi) {
+      for (int o = 32; o > 0; o >>= 1) {
+        lo += __shfl_xor(lo, o);
+        hi += __shfl_xor(hi, o);
+      }
+      return (((0.0 + lo) + hi) + 0.0) + 0.0;
+    };
+    n_in = half_sums(i0 ? 1.0 : 0.0, i1 ? 1.0 : 0.0);
+    ms0 = half_sums(i0 ? 0.0 + sx[lane] : 0.0, i1 ? 0.0 + sx[k1] : 0.0) / n_in;
+    ms1 = half_sums(i0 ? 0.0 + sy[lane] : 0.0, i1 ? 0.0 + sy[k1] : 0.0) / n_in;
+    md0 = half_sums(i0 ? 0.0 + dxs[lane] : 0.0, i1 ? 0.0 + dxs[k1] : 0.0) / n_in;
+    md1 = half_sums(i0 ? 0.0 + dys[lane] : 0.0, i1 ? 0.0 + dys[k1] : 0.0) / n_in;
+    double b[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = h ? k1 : lane;
+      if (h ? i1 : i0) {
+        const double u0 = sx[k] - ms0, u1 = sy[k] - ms1;
+        const double v0 = dxs[k] - md0, v1 = dys[k] - md1;
+        b[h][0] = 0.0 + v0 * u0;
+        b[h][1] = 0.0 + v0 * u1;
+        b[h][2] = 0.0 + v1 * u0;
+        b[h][3] = 0.0 + v1 * u1;
+      }
     }
-  const double n_in = block_sum(cntd, red);
-  const double ms0 = block_sum(s0, red) / n_in;
-  const double ms1 = block_sum(s1, red) / n_in;
-  const double md0 = block_sum(s2, red) / n_in;
-  const double md1 = block_sum(s3, red) / n_in;
-  double a00 = 0, a01 = 0, a10 = 0, a11 = 0;
-  for (int k = tid; k < N; k += kThreads)
-    if (inl[k]) {
-      const double u0 = sx[k] - ms0, u1 = sy[k] - ms1;
-      const double v0 = dxs[k] - md0, v1 = dys[k] - md1;
-      a00 += v0 * u0;
-      a01 += v0 * u1;
-      a10 += v1 * u0;
-      a11 += v1 * u1;
-    }
-  a00 = block_sum(a00, red);
-  a01 = block_sum(a01, red);
-  a10 = block_sum(a10, red);
-  a11 = block_sum(a11, red);
+    a00 = half_sums(b[0][0], b[1][0]);
+    a01 = half_sums(b[0][1], b[1][1]);
+    a10 = half_sums(b[0][2], b[1][2]);
+    a11 = half_sums(b[0][3], b[1][3]);
+  } else {
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0, cntd = 0;
+    for (int k = tid; k < N; k += kThreads)
+      if (inl[k]) {
+        s0 += sx[k];
+        s1 += sy[k];
+        s2 += dxs[k];
+        s3 += dys[k];
+        cntd += 1.0;
+      }
+    n_in = block_sum(cntd, red);
+    ms0 = block_sum(s0, red) / n_in;
+    ms1 = block_sum(s1, red) / n_in;
+    md0 = block_sum(s2, red) / n_in;
+    md1 = block_sum(s3, red) / n_in;
+    for (int k = tid; k < N; k += kThreads)
+      if (inl[k]) {
+        const double u0 = sx[k] - ms0, u1 = sy[k] - ms1;
+        const double v0 = dxs[k] - md0, v1 = dys[k] - md1;
+        a00 += v0 * u0;
+        a01 += v0 * u1;
+        a10 += v1 * u0;
+        a11 += v1 * u1;
+      }
+    a00 = block_sum(a00, red);
+    a01 = block_sum(a01, red);
+    a10 = block_sum(a10, red);
+    a11 = block_sum(a11, red);
+  }
   if (tid == 0) {
     double* o = out_params + 6 * (size_t)f;
     const double a = a00 + a11, b = a10 - a01;

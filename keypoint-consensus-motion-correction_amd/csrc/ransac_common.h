@@ -267,23 +267,36 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   return v;
 }
 
-// The frame's bounding boxes for lin32_make: workgroup min / max over the staged points.
-// A NaN or infinite coordinate makes the half extents infinite (every trial then runs the
-// fp64 phase A).
-// The result goes to the shared `out` (read per trial, not held in registers).
-__device__ inline void frame_mag(const double* sx, const double* sy, const double* dx, const double* dy, int N,
-                                 double* red, Mag& out) {
-  double lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  bool bad = false;
-  for (int k = threadIdx.x; k < N; k += kThreads) {
-    const double c[4] = {sx[k], sy[k], dx[k], dy[k]};
+// The boxes' centres, half extents and magnitudes from their bounds (lo, hi) per coordinate.
+__device__ __forceinline__ Mag mag_of(const double (&L)[4], const double (&Hh)[4]) {
+  double c[4], h[4], m[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bad |= !(fabs(c[i]) < INFINITY);
-      lo[i] = fmin(lo[i], c[i]);
-      hi[i] = fmax(hi[i], c[i]);
-    }
+  for (int i = 0; i < 4; ++i) {
+    const bool fin = fabs(L[i]) < INFINITY && fabs(Hh[i]) < INFINITY;
+    c[i] = fin ? 0.5 * L[i] + 0.5 * Hh[i] : 0.0;
+    h[i] = fin ? fmax(Hh[i] - c[i], c[i] - L[i]) * (1.0 + 0x1p-50) : INFINITY;  // >= every |x - c|
+    m[i] = fmax(fabs(L[i]), fabs(Hh[i]));
   }
+  Mag out;
+  out.cx = c[0]; out.cy = c[1]; out.cu = c[2]; out.cv = c[3];
+  out.hx = h[0]; out.hy = h[1]; out.hu = h[2]; out.hv = h[3];
+  out.X = m[0]; out.Y = m[1]; out.U = m[2]; out.V = m[3];
+  return out;
+}
+
+// One point's contribution to the bounds (a NaN or infinite coordinate makes them infinite).
+__device__ __forceinline__ void mag_add(const double (&c)[4], double (&lo)[4], double (&hi)[4], bool& bad) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    bad |= !(fabs(c[i]) < INFINITY);
+    lo[i] = fmin(lo[i], c[i]);
+    hi[i] = fmax(hi[i], c[i]);
+  }
+}
+
+// The wave's bounds in every lane (min / max: exact in any order; a lane that saw a NaN or
+// infinite coordinate contributes infinite bounds).
+__device__ __forceinline__ void wave_bounds(double (&lo)[4], double (&hi)[4], bool bad) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (bad) {
@@ -295,6 +308,21 @@ __device__ inline void frame_mag(const double* sx, const double* sy, const doubl
       hi[i] = fmax(hi[i], __shfl_xor(hi[i], o));
     }
   }
+}
+
+// The frame's bounding boxes for lin32_make: workgroup min / max over the staged points.
+// A NaN or infinite coordinate makes the half extents infinite (every trial then runs the
+// fp64 phase A).
+// The result goes to the shared `out` (read per trial, not held in registers).
+__device__ inline void frame_mag(const double* sx, const double* sy, const double* dx, const double* dy, int N,
+                                 double* red, Mag& out) {
+  double lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  bool bad = false;
+  for (int k = threadIdx.x; k < N; k += kThreads) {
+    const double c[4] = {sx[k], sy[k], dx[k], dy[k]};
+    mag_add(c, lo, hi, bad);
+  }
+  wave_bounds(lo, hi, bad);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __syncthreads();
   if (lane == 0)
@@ -314,19 +342,7 @@ __device__ inline void frame_mag(const double* sx, const double* sy, const doubl
       Hh[i] = fmax(Hh[i], red[8 * w + 4 + i]);
     }
   }
-  double c[4], h[4], m[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const bool fin = fabs(L[i]) < INFINITY && fabs(Hh[i]) < INFINITY;
-    c[i] = fin ? 0.5 * L[i] + 0.5 * Hh[i] : 0.0;
-    h[i] = fin ? fmax(Hh[i] - c[i], c[i] - L[i]) * (1.0 + 0x1p-50) : INFINITY;  // >= every |x - c|
-    m[i] = fmax(fabs(L[i]), fabs(Hh[i]));
-  }
-  if (threadIdx.x == 0) {
-    out.cx = c[0]; out.cy = c[1]; out.cu = c[2]; out.cv = c[3];
-    out.hx = h[0]; out.hy = h[1]; out.hu = h[2]; out.hv = h[3];
-    out.X = m[0]; out.Y = m[1]; out.U = m[2]; out.V = m[3];
-  }
+  if (threadIdx.x == 0) out = mag_of(L, Hh);
   __syncthreads();  // out is visible, red is free
 }
 

@@ -27,6 +27,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--device-lists", action="store_true",
+                    help="the pipelines' form: device consensus lists (kcmc_ransac_lists, max_n = n_kp_global)")
     a = ap.parse_args()
     bc = bench.CONFIGS[a.config]
     dev = torch.device("cuda", 0)
@@ -37,9 +39,13 @@ def main():
                               torch.from_numpy(ks.q_off).to(dev), ks.q_off)
     cfg = pipeline.AlignConfig(n_kp_global=bc.n_kp_global, ransac_model=bc.model)
     m = pipeline.match_stage(inp, cfg)
-    keep = m.keep_bits.cpu().numpy()
-    cons = pipeline.consensus_stage(keep, bc.n_tpl, keep.shape[0], cfg)
-    lists = pipeline.consensus_to_device(cons, dev)
+    if a.device_lists:
+        cons = pipeline.device_consensus(m, bc.n_tpl, bc.frames_per_gpu, cfg)
+        lists = None
+    else:
+        keep = m.keep_bits.cpu().numpy()
+        cons = pipeline.consensus_stage(keep, bc.n_tpl, keep.shape[0], cfg)
+        lists = pipeline.consensus_to_device(cons, dev)
     rr = pipeline.ransac_stage(m, inp.kp_tpl, cons, cfg, lists_dev=lists)
     torch.cuda.synchronize()
     ts = []
@@ -55,7 +61,7 @@ def main():
         h.update(np.ascontiguousarray(t.cpu().numpy()).tobytes())
     n_fit = int((np.diff(cons.pt_off) >= cfg.effective_frame_skip).sum())
     med = float(np.median(ts))
-    print(json.dumps({"config": a.config, "lib": os.environ.get("KCMC_LIB_PATH", "in-tree"), "frames": bc.frames_per_gpu,
+    print(json.dumps({"config": a.config, "lists": "device" if a.device_lists else "host", "lib": os.environ.get("KCMC_LIB_PATH", "in-tree"), "frames": bc.frames_per_gpu,
                       "frames_fitted": n_fit, "mean_points": float(np.diff(cons.pt_off).mean()),
                       "ms_median": round(med, 4), "ms_best": round(min(ts), 4),
                       "hypotheses_per_s": round(n_fit * cfg.ransac_trials / (med * 1e-3), 1),
