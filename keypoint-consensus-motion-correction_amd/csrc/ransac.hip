@@ -18,7 +18,8 @@
 // rare frames where some S == 0.  The hypothesis (sample pair) of trial t is the
 // t-th RandomState(seed).choice(N, 2, replace=False), precomputed on the host per N
 // (kcmc_ransac_prepare) -- it depends on N only because every frame reseeds.
-// Refit: rigid Umeyama over the best inlier set with workgroup reductions.
+// Refit: rigid Umeyama over the best inlier set (wave 0 alone for N <= 128, workgroup
+// reductions above; the same sums in the same order either way).
 #include <cfloat>
 #include <cmath>
 
