@@ -189,7 +189,8 @@ def test_ransac_bit_exact_selection_vs_oracle(dev):
     including N > 128 (numpy's recursive pairwise order)."""
     rng = np.random.default_rng(21)
     tpls, qs = [], []
-    for N in [3, 4, 5, 8, 9, 50, 100, 127, 128, 129, 136, 200, 255, 256, 257, 300, 500, 777, 1024, 2000]:
+    # 63 / 64 / 65: the one-wave staging and refit (N <= 128) hold points lane and lane + 64
+    for N in [3, 4, 5, 8, 9, 50, 63, 64, 65, 100, 127, 128, 129, 136, 200, 255, 256, 257, 300, 500, 777, 1024, 2000]:
         tpl = rng.uniform(0, 1000, (N, 2))
         A = synthetic.rigid(rng.normal(0, 0.02), rng.normal(0, 5), rng.normal(0, 5))
         q = (tpl - A[:, 2]) @ A[:, :2] + rng.normal(0, rng.uniform(0.1, 1.5), (N, 2))
