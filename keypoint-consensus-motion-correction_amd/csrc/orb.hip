@@ -17,10 +17,11 @@
 //   * steered BRIEF: 256 point pairs of a fixed pattern rotated to the bin's centre
 //     angle (host table), compared on a 5x5 binomial smoothing -> 32-byte descriptors.
 //
-// orb_candidates_kernel  one workgroup per 64x16 tile: image + 4-px halo in LDS, FAST
-//                        scores for the tile + 1-px halo, NMS, Harris -- each step on
-//                        the compacted survivors of the previous one (block scans), so
-//                        the candidates keep raster order inside the tile.
+// orb_candidates_kernel  one workgroup per kSub vertically stacked 64x16 tiles: image +
+//                        4-px halo in LDS, FAST scores for the region + 1-px halo, NMS,
+//                        Harris -- each step on the compacted survivors of the previous
+//                        one (block scans), so the candidates keep tile order and raster
+//                        order inside the tile.
 // orb_offsets_kernel +   per frame: tile prefix offsets, then one wave per tile copies
 // orb_gather_kernel      its candidates into the frame's compact list (candidate order).
 // orb_select_kernel      one workgroup per frame: radix select of the n_features-th
@@ -35,12 +36,16 @@ namespace kcmc {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kTW = 64, kTH = 16;          // candidate tile
+constexpr int kTW = 64, kTH = 16;          // candidate tile (the candidate order's unit)
+constexpr int kSub = 2;                    // tiles per workgroup, stacked vertically (4: slower)
+constexpr int kRH = kTH * kSub;            // rows of a workgroup's region
 constexpr int kHalo = 4;                   // FAST radius 3 + NMS 1; Harris 3 + Sobel 1
 constexpr int kPW = kTW + 2 * kHalo;       // 72
-constexpr int kPH = kTH + 2 * kHalo;       // 24
-constexpr int kSW = kTW + 2, kSH = kTH + 2;  // scores of the tile + 1-px halo
-constexpr int kSlots = kTW * kTH / 4;      // NMS leaves at most one candidate per 2x2 block
+constexpr int kPH = kRH + 2 * kHalo;
+constexpr int kSW = kTW + 2, kSH = kRH + 2;  // scores of the region + 1-px halo
+constexpr int kSlots = kTW * kTH / 4;      // per tile: NMS leaves at most one candidate per 2x2 block
+constexpr int kNmsPx = kTW * kRH / kThreads;  // region pixels per thread in the NMS (one tile's run)
+static_assert(kNmsPx <= 32 && (kTW * kTH) % kNmsPx == 0, "NMS: a thread's pixels lie in one tile");
 
 __constant__ int8_t c_circle[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},  {3, 0},  {3, -1}, {2, -2}, {1, -3},
                                        {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
@@ -102,13 +107,16 @@ __device__ __forceinline__ int fast_score9(const uint8_t (*img)[kPW], int py, in
   return best;
 }
 
-// One workgroup per 64x16 tile.  Candidates are sparse, so every expensive step runs on
-// a compacted list instead of on all pixels (a wave would otherwise pay for its single
-// candidate with 63 idle lanes): (1) stage the image + 4-px halo; (2) the compass
-// pre-test on the tile + 1-px halo, survivors listed; (3) FAST scores of the listed
-// pixels; (4) 3x3 NMS of the tile pixels, survivors listed in raster order; (5) integer
-// Harris of the listed candidates, 8 lanes per candidate (one 7-pixel window row each,
-// shuffle reduction); (6) the keys and positions stored in list (= raster) order.
+// One workgroup per kSub vertically stacked 64x16 tiles (a 64 x kRH region: the barriers
+// and the halo of one tile's worth of work are shared by kSub tiles).  Candidates are
+// sparse, so every expensive step runs on a compacted list instead of on all pixels (a
+// wave would otherwise pay for its single candidate with 63 idle lanes): (1) stage the
+// image + 4-px halo; (2) the compass pre-test on the region + 1-px halo, survivors
+// listed; (3) FAST scores of the listed pixels; (4) 3x3 NMS of the region's pixels,
+// survivors listed in raster order -- which is tile order, then raster order inside the
+// tile, the candidate order; (5) integer Harris of the listed candidates, 8 lanes per
+// candidate (one 7-pixel window row each, shuffle reduction); (6) the keys and positions
+// stored per tile, in list order.
 __global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t* __restrict__ frames, int H, int W,
                                                                   int threshold, double harris_k, int edge,
                                                                   uint64_t* __restrict__ cand_key,
@@ -117,12 +125,13 @@ __global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t*
   __shared__ __attribute__((aligned(16))) uint8_t img[kPH][kPW];
   __shared__ int16_t sc[kSH][kSW];
   __shared__ uint16_t plist[kSH * kSW];  // pre-test survivors (score-region index)
-  __shared__ uint16_t nlist[kTW * kTH];  // NMS survivors (tile pixel index, raster order)
+  __shared__ uint16_t nlist[kTW * kRH];  // NMS survivors (region pixel index, raster order)
   __shared__ int s_warp[kThreads / 64];
-  const int ntx = gridDim.x, nty = gridDim.y;
+  __shared__ int s_start[kSub + 1];      // the first list entry of each tile; s_start[kSub] = total
+  const int ntx = gridDim.x;
+  const int nty = (H + kTH - 1) / kTH;   // tile rows of the frame (the last region may hold fewer)
   const int f = blockIdx.z;
-  const int tile = blockIdx.y * ntx + blockIdx.x;
-  const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH;
+  const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kRH;
   const int tid = threadIdx.x;
   const uint8_t* I = frames + (size_t)f * H * W;
 
@@ -180,11 +189,12 @@ __global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t*
   }
   __syncthreads();
 
-  // (4) NMS; thread t owns tile pixels 4t .. 4t+3 (raster order inside the tile)
-  int flags = 0;
+  // (4) NMS; thread t owns region pixels kNmsPx t .. kNmsPx t + kNmsPx - 1 (raster order),
+  // all in tile kNmsPx t / 1024
+  uint32_t flags = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int p = 4 * tid + q;
+  for (int q = 0; q < kNmsPx; ++q) {
+    const int p = kNmsPx * tid + q;
     const int r = p / kTW, c = p - r * kTW;
     const int y = y0 + r, x = x0 + c;
     if (y < edge || y >= H - edge || x < edge || x >= W - edge) continue;
@@ -200,17 +210,18 @@ __global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t*
         const bool later = dy > 0 || (dy == 0 && dx > 0);
         keep = keep && (s > o || (s == o && later));
       }
-    if (keep) flags |= 1 << q;
+    if (keep) flags |= 1u << q;
   }
   const int total = block_excl_scan(__builtin_popcount(flags), s_warp, excl);
+  if ((kNmsPx * tid) % (kTW * kTH) == 0) s_start[kNmsPx * tid / (kTW * kTH)] = excl;  // a tile's first thread
+  if (tid == 0) s_start[kSub] = total;
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (flags >> q & 1) nlist[excl++] = (uint16_t)(4 * tid + q);
+  for (int q = 0; q < kNmsPx; ++q)
+    if (flags >> q & 1) nlist[excl++] = (uint16_t)(kNmsPx * tid + q);
   __syncthreads();
 
   // (5) Harris over the 7x7 window of Sobel gradients, 8 lanes per candidate (lane row
   // 0..6 sums its window row, lane 7 idles), then (6) the stores in list order
-  const size_t base = ((size_t)f * nty * ntx + tile) * kSlots;
   const int grp = tid >> 3, row = tid & 7;
   for (int j0 = 0; j0 < total; j0 += kThreads / 8) {
     const int j = j0 + grp;
@@ -244,11 +255,15 @@ __global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t*
       const long long A = a, B = b, C = cc;
       const double sab = (double)(A + B);
       const int r = p / kTW, c = p - r * kTW;
-      cand_key[base + j] = order_key((double)(A * B - C * C) - harris_k * (sab * sab));
-      cand_pos[base + j] = ((uint32_t)(y0 + r) << 16) | (uint32_t)(x0 + c);
+      const int st = r / kTH;  // the candidate's tile in the region
+      const size_t o = ((size_t)f * nty * ntx + (size_t)(blockIdx.y * kSub + st) * ntx + blockIdx.x) * kSlots +
+                       (j - s_start[st]);
+      cand_key[o] = order_key((double)(A * B - C * C) - harris_k * (sab * sab));
+      cand_pos[o] = ((uint32_t)(y0 + r) << 16) | (uint32_t)(x0 + c);
     }
   }
-  if (tid == 0) cand_cnt[(size_t)f * nty * ntx + tile] = total;
+  if (tid < kSub && blockIdx.y * kSub + tid < nty)
+    cand_cnt[(size_t)f * nty * ntx + (size_t)(blockIdx.y * kSub + tid) * ntx + blockIdx.x] = s_start[tid + 1] - s_start[tid];
 }
 
 // Per frame, one wave per tile (in tile order): the tile's candidates are appended to
@@ -501,7 +516,7 @@ extern "C" int kcmc_orb_detect(kcmc_ctx* ctx, const uint8_t* frames, int n_frame
   for (int f0 = 0; f0 < n_frames && rc == KCMC_OK; f0 += batch) {
     const int nb = std::min(batch, n_frames - f0);
     const uint8_t* fr = frames + (size_t)f0 * H * W;
-    hipLaunchKernelGGL(orb_candidates_kernel, dim3(ntx, nty, nb), dim3(kThreads), 0, s, fr, H, W, threshold, harris_k,
+    hipLaunchKernelGGL(orb_candidates_kernel, dim3(ntx, ceil_div(nty, kSub), nb), dim3(kThreads), 0, s, fr, H, W, threshold, harris_k,
                        edge, ckey, cpos, ccnt);
     hipLaunchKernelGGL(orb_offsets_kernel, dim3(nb), dim3(kThreads), 0, s, ccnt, ntiles, toff, ctot);
     hipLaunchKernelGGL(orb_gather_kernel, dim3(ceil_div(ntiles, 4 * 8), nb), dim3(kThreads), 0, s, ckey, cpos, ccnt,

@@ -842,8 +842,11 @@ def keypoints_csr(k: Keypoints):
     F, N = k.kp.shape[:2]
     q_off = np.zeros(F + 1, np.int32)
     q_off[1:] = np.cumsum(counts)
-    rows = torch.from_numpy(np.concatenate([f * N + np.arange(c) for f, c in enumerate(counts)])
-                            if F else np.zeros(0, np.int64)).to(k.kp.device)
-    kp = k.kp.reshape(F * N, 2).index_select(0, rows).contiguous()
-    des = k.des.reshape(F * N, 32).index_select(0, rows).contiguous()
+    if F and (counts == N).all():  # every frame full (the common case): the arrays as they are
+        kp = k.kp.reshape(F * N, 2).contiguous()
+        des = k.des.reshape(F * N, 32).contiguous()
+    else:  # the first count[f] rows of every frame, in frame order (compacted on the device)
+        live = torch.arange(N, device=k.kp.device)[None, :] < k.count.to(torch.int64)[:, None]
+        kp = k.kp[live].contiguous()
+        des = k.des[live].contiguous()
     return kp, des, torch.from_numpy(q_off).to(k.kp.device), q_off

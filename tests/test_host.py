@@ -377,3 +377,23 @@ def test_parallelize_is_an_ordered_process_pool_map():
         N_JOBS_PARALLEL = 1
 
     assert One()._parallelize(_square_plus, [1, 2], [3, 4]) == [1009, 2016]
+
+
+@pytest.mark.parametrize("counts", [[3, 3, 3], [3, 0, 2], [0, 0], []])
+def test_keypoints_csr_compacts_in_frame_order(counts):
+    """stages.keypoints_csr: the first count[f] detections of every frame, frame by frame
+    (the matcher's CSR), whether every frame is full or not."""
+    import torch
+
+    F, N = len(counts), 3
+    kp = torch.arange(F * N * 2, dtype=torch.float64).reshape(F, N, 2)
+    des = torch.arange(F * N * 32, dtype=torch.int64).remainder(251).to(torch.uint8).reshape(F, N, 32)
+    k = stages.Keypoints(kp, des, torch.tensor(counts, dtype=torch.int32))
+    kp_q, des_q, q_off, q_off_host = stages.keypoints_csr(k)
+    rows = [(f, j) for f in range(F) for j in range(counts[f])]
+    assert q_off_host.tolist() == [0] + np.cumsum(counts).astype(int).tolist()
+    assert q_off.tolist() == q_off_host.tolist()
+    assert kp_q.shape == (len(rows), 2) and des_q.shape == (len(rows), 32)
+    for i, (f, j) in enumerate(rows):
+        assert kp_q[i].tolist() == kp[f, j].tolist()
+        assert des_q[i].tolist() == des[f, j].tolist()
