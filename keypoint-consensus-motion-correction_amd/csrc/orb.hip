@@ -117,7 +117,9 @@ __device__ __forceinline__ int fast_score9(const uint8_t (*img)[kPW], int py, in
 // tile, the candidate order; (5) integer Harris of the listed candidates, 8 lanes per
 // candidate (one 7-pixel window row each, shuffle reduction); (6) the keys and positions
 // stored per tile, in list order.
-__global__ __launch_bounds__(kThreads) void orb_candidates_kernel(const uint8_t* __restrict__ frames, int H, int W,
+// 8 waves per SIMD (<= 64 VGPRs, no spill): the workgroups are barrier- and latency-bound,
+// and the eighth wave slot took 15.4 -> 14.8 ms per 2000 c2 frames (profiles/r06_orb_subtiles_ab.txt)
+__global__ __launch_bounds__(kThreads, 8) void orb_candidates_kernel(const uint8_t* __restrict__ frames, int H, int W,
                                                                   int threshold, double harris_k, int edge,
                                                                   uint64_t* __restrict__ cand_key,
                                                                   uint32_t* __restrict__ cand_pos,
